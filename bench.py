@@ -1,0 +1,246 @@
+"""Benchmark: forward Gaussian-splat rasterization on MI355X.
+
+Metric (BASELINE.json): rendered splats/s (N Gaussians x frames/s) at 1080p on
+a 1M-Gaussian SH-degree-3 scene.  One "step" = one full frame of the hot path
+(cull + project + SH, depth radix sort, tile binning + sort, compositing) for
+one camera, inputs resident in HBM.  With --gpus N (torchrun, one process per
+GPU) the scene is generated on rank 0, broadcast once over RCCL/xGMI (untimed)
+and rank k renders view k (default camera yawed by k*45 deg):
+weak scaling, no per-frame collective.
+
+Prints ONE JSON line on rank 0.  Stage timings come from HIP events recorded
+by libgsr on the render stream during the timed region.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (N, sh_degree, width, height, description)
+    "c1": (100_000, 0, 640, 480, "100k random Gaussians, SH deg 0, 640x480"),
+    "c2": (1_000_000, 3, 1920, 1080, "1M Gaussians, SH deg 3, 1920x1080 (garden stand-in)"),
+    "c3": (6_000_000, 3, 1920, 1080, "6M Gaussians synthetic, SH deg 3, 1920x1080"),
+    "c5": (1_000_000, 3, 3840, 2160, "1M Gaussians, SH deg 3, 3840x2160"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_scene(cfg, n, deg):
+    from gsviewer_amd.gaussian_data import garden_standin, random_scene
+    if cfg == "c1":
+        return random_scene(n, sh_degree=deg, seed=0), "synthetic: random uniform (seed 0)"
+    seed = 2 if cfg == "c3" else 1
+    return garden_standin(n, seed=seed, sh_degree=deg), f"synthetic: garden stand-in (seed {seed}), no PLY offline"
+
+
+def cpu_baseline(g, cam, seconds):
+    """The C restatement of the reference OGL path (oracle/gl_oracle.c), full
+    frames of the same workload on the host cores, bounded to ~`seconds`."""
+    from oracle import c_oracle as C
+    from oracle import gl_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    U = O.default_uniforms(cam.get_view_matrix(), cam.get_project_matrix(),
+                           np.asarray(cam.get_htanfovxy_focal(), np.float32), cam.position, cam.w, cam.h)
+    flat = g.flat()
+    frames, t_total = 0, 0.0
+    while True:
+        t0 = time.perf_counter()
+        C.render(flat, g.sh_dim, U, threads=threads)
+        t_total += time.perf_counter() - t0
+        frames += 1
+        if t_total >= seconds or frames >= 50:
+            break
+    # the reference's own per-frame CPU sort (_sort_gaussian_cpu), single thread
+    t0 = time.perf_counter()
+    C.sort_depth(g.xyz, U["view"])
+    t_sort = time.perf_counter() - t0
+    return dict(value=len(g) * frames / t_total, unit="splats/s", cores=threads, kind="port",
+                sample=f"{frames} full frames of the same workload ({len(g)} Gaussians, {cam.w}x{cam.h}) "
+                       f"through oracle/gl_oracle.c (OGL-path restatement: vertex stage, qsort depth sort, "
+                       f"rect raster + fragment + blend)",
+                ms_per_frame=1e3 * t_total / frames, sort_only_ms_1thread=1e3 * t_sort)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--t-min", type=float, default=1e-4)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="do not record per-stage HIP events")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from gsviewer_amd import _lib
+    from gsviewer_amd.camera import view_for_rank
+    from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into
+
+    _lib.load()
+    n, deg, W, H, desc = CONFIGS[args.config]
+    n = args.n or n
+    W = args.width or W
+    H = args.height or H
+    k_coef = (deg + 1) ** 2
+
+    # ---- scene: generated on rank 0, broadcast once (RCCL over xGMI), untimed
+    t_gen = time.perf_counter()
+    if rank == 0:
+        g, data_desc = make_scene(args.config, n, deg)
+        tensors = [torch.from_numpy(np.ascontiguousarray(getattr(g, f))).to(dev)
+                   for f in ("xyz", "rot", "scale", "opacity", "sh")]
+    else:
+        g, data_desc = None, None
+        tensors = [torch.empty(s, dtype=torch.float32, device=dev)
+                   for s in ((n, 3), (n, 4), (n, 3), (n, 1), (n, 3 * k_coef))]
+    t_gen = time.perf_counter() - t_gen
+    bcast = None
+    if world > 1:
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for t in tensors:
+            dist.broadcast(t, src=0)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        nbytes = sum(t.numel() * 4 for t in tensors)
+        bcast = dict(bytes=nbytes, seconds=dt, GBps=nbytes / dt / 1e9)
+    scene = HipScene(*tensors)
+    del tensors
+    cam = view_for_rank(H, W, rank)
+    camc = camera_from(cam)
+    st = RenderSettings(t_min=args.t_min, out_layout=0)
+    ctx = HipContext()
+    lib = _lib.load()
+    out = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+
+    for _ in range(args.warmup):
+        render_into(ctx, scene, camc, st, out)
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        _lib.check(lib.gsr_context_set_profiling(ctx.handle, 1), "set_profiling")
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        render_into(ctx, scene, camc, st, out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    stats = ctx.stats()
+    stage = {}
+    if not args.no_profile:
+        import ctypes
+        ms = (ctypes.c_double * 8)()
+        frames = ctypes.c_int64()
+        _lib.check(lib.gsr_context_stage_times(ctx.handle, ms, ctypes.byref(frames)), "stage_times")
+        stage = {name: ms[i] / max(frames.value, 1) for i, name in enumerate(_lib.STAGES)}
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = 1e3 * elapsed / args.steps
+    fps = args.steps / elapsed
+    value = n * args.steps * world / elapsed
+    rec_bytes = 4 * (11 + 3 * k_coef)
+    b_frame = n * rec_bytes + W * H * 12
+
+    roof = None
+    if stage:
+        kernels = {k: v for k, v in stage.items() if k != "sync"}
+        dom = max(kernels, key=kernels.get)
+        inst = stats["n_instances"]
+        ntiles = stats["tiles_x"] * stats["tiles_y"]
+        nvis = stats["n_visible"]
+        # algorithmic bytes per launch of each stage (DESIGN.md "Roofline")
+        alg = {
+            "composite": inst * (64 + 4) + ntiles * 8 + W * H * 12,
+            "preprocess": n * 8 + nvis * (rec_bytes - 16 + 64 + 4),  # masks + visible attrs in, record+key out
+            "cull": n * 16 + (n // 64) * 12,
+            "depth_sort": nvis * 4 * 8 * 2 + nvis * 4 * 4,
+            "tile_sort": inst * 8 * 2 * 2 + inst * 4 * 2,
+            "binning": nvis * (4 + 16 + 4 + 4 + 4) + inst * 8,
+            "tile_ranges": inst * 4 * 2 + ntiles * 8,
+        }[dom]
+        achieved = alg / (stage[dom] * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg,
+                "ms_per_launch": stage[dom],
+                "frame": {"bytes": b_frame, "GBps": b_frame * fps / 1e9, "frac": b_frame * fps / 1e9 / HBM_PEAK_GBS}}
+
+    cpu = None
+    if not args.no_cpu_baseline and world == 1 and g is not None:
+        cpu = cpu_baseline(g, cam, args.cpu_seconds)
+
+    res = {
+        "metric": "rendered splats/sec/GPU + frames/sec at 1080p, 1M Gaussians" if args.config == "c2"
+        else f"rendered splats/sec ({desc})",
+        "value": value,
+        "unit": "splats/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "fps_per_gpu": fps,
+        "splats_per_s_per_gpu": value / world,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": data_desc,
+        "config": {"workload": desc, "n_gaussians": n, "sh_degree": deg, "width": W, "height": H,
+                   "views": "view k = default camera yawed k*45 deg (one per GPU)", "t_min": args.t_min,
+                   "parallelism": f"replicated scene, {world} independent views"},
+        "frame_stats": stats,
+        "stage_ms": stage,
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "broadcast": bcast,
+        "scene_gen_s": t_gen,
+    }
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,129 @@
+"""ctypes binding of the C ABI in ``include/gsr.h`` (``gsviewer_amd/libgsr.so``).
+
+The shared library is the product: there is no Python or CPU fallback.  If it
+is missing or fails to load, every entry point raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libgsr.so")
+
+
+class GsrCamera(ctypes.Structure):
+    _fields_ = [
+        ("view", ctypes.c_float * 16),
+        ("proj", ctypes.c_float * 16),
+        ("campos", ctypes.c_float * 3),
+        ("hfovxy_focal", ctypes.c_float * 3),
+        ("width", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+    ]
+
+
+class GsrSettings(ctypes.Structure):
+    _fields_ = [
+        ("scale_modifier", ctypes.c_float),
+        ("screen_scale", ctypes.c_float),
+        ("render_mod", ctypes.c_int32),
+        ("dc_factor", ctypes.c_float),
+        ("extra_factor", ctypes.c_float),
+        ("color_scale", ctypes.c_float * 3),
+        ("rot_modifier", ctypes.c_float * 4),
+        ("light_rotation", ctypes.c_float * 3),
+        ("enable_aabb", ctypes.c_int32),
+        ("enable_obb", ctypes.c_int32),
+        ("cube_rotation", ctypes.c_float * 9),
+        ("cube_min", ctypes.c_float * 3),
+        ("cube_max", ctypes.c_float * 3),
+        ("points_center", ctypes.c_float * 3),
+        ("bg", ctypes.c_float * 3),
+        ("t_min", ctypes.c_float),
+        ("out_layout", ctypes.c_int32),
+    ]
+
+
+class GsrFrameStats(ctypes.Structure):
+    _fields_ = [
+        ("n_gaussians", ctypes.c_int64),
+        ("n_visible", ctypes.c_int64),
+        ("n_instances", ctypes.c_int64),
+        ("tiles_x", ctypes.c_int32),
+        ("tiles_y", ctypes.c_int32),
+    ]
+
+
+# name -> (restype, argtypes); every symbol declared in include/gsr.h
+_P = ctypes.c_void_p
+SIGNATURES = {
+    "gsr_abi_version": (ctypes.c_int, []),
+    "gsr_last_error": (ctypes.c_char_p, []),
+    "gsr_settings_default": (None, [ctypes.POINTER(GsrSettings)]),
+    "gsr_scene_create": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int64, ctypes.c_int32, _P,
+                                        ctypes.POINTER(_P)]),
+    "gsr_scene_create_flat": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int32, _P, ctypes.POINTER(_P)]),
+    "gsr_scene_destroy": (ctypes.c_int, [_P]),
+    "gsr_scene_count": (ctypes.c_int64, [_P]),
+    "gsr_scene_sh_dim": (ctypes.c_int32, [_P]),
+    "gsr_context_create": (ctypes.c_int, [ctypes.POINTER(_P)]),
+    "gsr_context_destroy": (ctypes.c_int, [_P]),
+    "gsr_render": (ctypes.c_int, [_P, _P, ctypes.POINTER(GsrCamera), ctypes.POINTER(GsrSettings), _P, _P, _P]),
+    "gsr_context_stats": (ctypes.c_int, [_P, ctypes.POINTER(GsrFrameStats)]),
+    "gsr_sort_depth": (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_float * 16), _P, _P]),
+    "gsr_debug_copy": (ctypes.c_int64, [_P, ctypes.c_int32, _P, ctypes.c_int64, _P]),
+    "gsr_context_set_profiling": (ctypes.c_int, [_P, ctypes.c_int32]),
+    "gsr_context_stage_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+}
+
+STAGES = ["cull", "preprocess", "depth_sort", "binning", "tile_sort", "tile_ranges", "composite", "sync"]
+
+GSR_DEBUG_RECORDS, GSR_DEBUG_DEPTH_ORDER, GSR_DEBUG_TILE_RANGES, GSR_DEBUG_TILE_LIST = 0, 1, 2, 3
+
+ABI_VERSION = 1
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the library handle.  Raises RuntimeError."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"gsviewer_amd: HIP library {path} is missing; build it with "
+                "`python -m gsviewer_amd.build` (there is no CPU fallback)")
+        # Share the HIP runtime torch already loaded (same soname libamdhip64.so.7).
+        try:
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is part of the image
+            pass
+        try:
+            lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            raise RuntimeError(f"gsviewer_amd: failed to load {path}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.gsr_abi_version() != ABI_VERSION:
+            raise RuntimeError("gsviewer_amd: ABI version mismatch between libgsr.so and bindings")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().gsr_last_error()
+        raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def default_settings() -> GsrSettings:
+    s = GsrSettings()
+    load().gsr_settings_default(ctypes.byref(s))
+    return s

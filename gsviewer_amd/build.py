@@ -1,0 +1,76 @@
+"""Build the in-tree HIP shared library ``gsviewer_amd/libgsr.so`` for gfx950.
+
+Usage: ``python -m gsviewer_amd.build [--jobs N] [--debug]``.  The library is
+plain hipcc output (no torch extension machinery): a C-ABI ``.so`` whose
+entry points are declared in ``include/gsr.h``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+BUILD = os.path.join(ROOT, "build", "gsr")
+LIB = os.path.join(PKG, "libgsr.so")
+ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["api.hip", "scene.hip", "scan.hip", "radix_sort.hip", "preprocess.hip", "composite.hip"]
+# The per-Gaussian stage must evaluate exactly like the oracle: no contraction.
+EXTRA_FLAGS = {"preprocess.hip": ["-ffp-contract=off"]}
+
+
+def hipcc():
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (set HIPCC)")
+
+
+def _compile(src, debug):
+    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+    deps = [os.path.join(CSRC, src), os.path.join(CSRC, "gsr_internal.h"), os.path.join(INCLUDE, "gsr.h")]
+    if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
+        return obj
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-c",
+           "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function", "-Wno-bitwise-instead-of-logical",
+           "-I", INCLUDE, "-I", CSRC, os.path.join(CSRC, src), "-o", obj]
+    cmd += ["-O0", "-g"] if debug else ["-O3"]
+    cmd += EXTRA_FLAGS.get(src, [])
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if r.stderr.strip():
+        sys.stderr.write(r.stderr)
+    return obj
+
+
+def build(jobs=None, debug=False, verbose=True):
+    os.makedirs(BUILD, exist_ok=True)
+    jobs = jobs or min(len(SOURCES), os.cpu_count() or 4, 8)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, debug), SOURCES))
+    if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(o) for o in objs):
+        return LIB
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(LIB + ".tmp", LIB)
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("--debug", action="store_true")
+    a = ap.parse_args()
+    build(a.jobs, a.debug)

@@ -1,0 +1,481 @@
+// C ABI (include/gsr.h): scene lifetime, frame workspace, render orchestration.
+//
+// Frame pipeline on one stream (N = Gaussians, V = visible, D = instances):
+//   k_cull(N) -> scan(N/64 wave counts) -> k_preprocess(N)
+//   -> radix sort (depth key, record id) over V, 4 x 8-bit passes
+//   -> k_dup_count(V) -> scan(V) -> [one 8-byte D2H read of V, D]
+//   -> k_dup_write(V) -> stable radix sort by tile id over D (ceil(tile_bits/8) passes)
+//   -> k_tile_ranges(D) -> k_composite(tiles)
+// All kernels after the cull read V from device memory, so the only host
+// synchronisation is the read of D needed to size the tile sort.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "gsr_internal.h"
+
+namespace gsr {
+
+std::string& last_error_ref() {
+    static thread_local std::string s;
+    return s;
+}
+
+int set_error(int code, const std::string& msg) {
+    last_error_ref() = msg;
+    return code;
+}
+
+namespace {
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;  // elements
+    int ensure(size_t n, const char* what) {
+        if (n <= cap && p) return GSR_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = n < 64 ? 64 : n + n / 8;  // 12.5% headroom against regrowth
+        if (hipMalloc(&p, want * sizeof(T)) != hipSuccess) {
+            p = nullptr;
+            return set_error(GSR_ERR_NOMEM, std::string("context: hipMalloc failed for ") + what);
+        }
+        cap = want;
+        return GSR_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+}  // namespace gsr
+
+struct gsr_context {
+    gsr::DevBuf<uint64_t> vis_mask;
+    gsr::DevBuf<uint32_t> wave_counts;
+    gsr::DevBuf<uint32_t> scan_tmp;
+    gsr::DevBuf<gsr::SplatRec> recs;
+    gsr::DevBuf<uint32_t> keys_a, keys_b, vals_a, vals_b;   // depth sort (capacity N)
+    gsr::DevBuf<uint32_t> dup_off;                          // per sorted splat: tile count -> offset
+    gsr::DevBuf<uint32_t> tkeys_a, tkeys_b, tvals_a, tvals_b;  // tile sort (capacity D)
+    gsr::DevBuf<uint32_t> radix_tmp;
+    gsr::DevBuf<uint2> ranges;
+    gsr::DevBuf<uint32_t> counters;  // [0] = V, [1] = D
+    uint32_t* host_counters = nullptr;  // pinned
+    gsr_frame_stats stats{};
+    // last frame's result arrays (for gsr_debug_copy)
+    const uint32_t* last_depth_order = nullptr;
+    const uint32_t* last_tile_list = nullptr;
+    int64_t last_tiles = 0;
+    // profiling: 10 events per frame, two frames in flight
+    bool prof_on = false;
+    hipEvent_t ev[2][11] = {};
+    bool ev_pending[2] = {false, false};
+    int64_t frame_idx = 0;
+    double acc_ms[GSR_NUM_STAGES] = {};
+    int64_t prof_frames = 0;
+};
+
+namespace gsr {
+namespace {
+
+int frag_class_of(int mode) {
+    if (mode == -4 || mode == -1) return kFragBillboard;
+    if (mode == -5) return kFragFlatBall;
+    if (mode == -6) return kFragGaussBall;
+    return kFragGauss;
+}
+
+int build_uniforms(const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, FrameUniforms& u) {
+    if (cam->width <= 0 || cam->height <= 0 || cam->width > 32768 || cam->height > 32768)
+        return set_error(GSR_ERR_INVALID, "camera: width/height out of range");
+    std::memcpy(u.V, cam->view, sizeof(u.V));
+    std::memcpy(u.P, cam->proj, sizeof(u.P));
+    std::memcpy(u.hfov, cam->hfovxy_focal, sizeof(u.hfov));
+    std::memcpy(u.campos, cam->campos, sizeof(u.campos));
+    u.gsf = st->scale_modifier;
+    u.sdsf = st->screen_scale;
+    u.dc_factor = st->dc_factor;
+    u.extra_factor = st->extra_factor;
+    std::memcpy(u.cscale, st->color_scale, sizeof(u.cscale));
+    std::memcpy(u.rotmod, st->rot_modifier, sizeof(u.rotmod));
+    for (int k = 0; k < 3; ++k) {
+        // radians() in float32 (gau_vert.glsl:148), cos/sin once per frame
+        const float rad = st->light_rotation[k] * (float)(M_PI / 180.0);
+        u.lcos[k] = std::cos(rad);
+        u.lsin[k] = std::sin(rad);
+    }
+    std::memcpy(u.pcenter, st->points_center, sizeof(u.pcenter));
+    {
+        // inverse(cube_rotation) (gau_vert.glsl:180) in double, once per frame
+        const float* m = st->cube_rotation;
+        double a[9];
+        for (int k = 0; k < 9; ++k) a[k] = m[k];
+        const double c00 = a[4] * a[8] - a[5] * a[7], c01 = a[5] * a[6] - a[3] * a[8], c02 = a[3] * a[7] - a[4] * a[6];
+        const double det = a[0] * c00 + a[1] * c01 + a[2] * c02;
+        if (st->enable_obb == 1 && !(std::fabs(det) > 0.0))
+            return set_error(GSR_ERR_INVALID, "settings: cube_rotation is singular");
+        const double id = det != 0.0 ? 1.0 / det : 0.0;
+        const double inv[9] = {c00 * id, (a[2] * a[7] - a[1] * a[8]) * id, (a[1] * a[5] - a[2] * a[4]) * id,
+                               c01 * id, (a[0] * a[8] - a[2] * a[6]) * id, (a[2] * a[3] - a[0] * a[5]) * id,
+                               c02 * id, (a[1] * a[6] - a[0] * a[7]) * id, (a[0] * a[4] - a[1] * a[3]) * id};
+        for (int k = 0; k < 9; ++k) u.obb_inv[k] = (float)inv[k];
+    }
+    std::memcpy(u.cmin, st->cube_min, sizeof(u.cmin));
+    std::memcpy(u.cmax, st->cube_max, sizeof(u.cmax));
+    u.enable_aabb = st->enable_aabb;
+    u.enable_obb = st->enable_obb;
+    u.render_mod = st->render_mod;
+    u.sh_dim = sc->d.sh_dim;
+    u.width = cam->width;
+    u.height = cam->height;
+    u.tiles_x = (cam->width + kTile - 1) / kTile;
+    u.tiles_y = (cam->height + kTile - 1) / kTile;
+    return GSR_OK;
+}
+
+int bits_for(uint32_t v) {  // bits needed to represent values < v
+    int b = 0;
+    while (b < 32 && (1ull << b) < v) ++b;
+    return b;
+}
+
+int ensure_scene_buffers(gsr_context* c, size_t n) {
+    const size_t nw = (n + 63) / 64 + 4;
+    int rc;
+    if ((rc = c->vis_mask.ensure(nw, "vis_mask"))) return rc;
+    if ((rc = c->wave_counts.ensure(nw, "wave_counts"))) return rc;
+    const size_t scan_need = std::max(scan_tmp_elems(nw), scan_tmp_elems(n));
+    if ((rc = c->scan_tmp.ensure(scan_need, "scan_tmp"))) return rc;
+    if ((rc = c->recs.ensure(n, "recs"))) return rc;
+    if ((rc = c->keys_a.ensure(n, "keys"))) return rc;
+    if ((rc = c->keys_b.ensure(n, "keys"))) return rc;
+    if ((rc = c->vals_a.ensure(n, "vals"))) return rc;
+    if ((rc = c->vals_b.ensure(n, "vals"))) return rc;
+    if ((rc = c->dup_off.ensure(n, "dup_off"))) return rc;
+    if ((rc = c->radix_tmp.ensure(radix_tmp_elems(n), "radix_tmp"))) return rc;
+    if ((rc = c->counters.ensure(4, "counters"))) return rc;
+    if (!c->host_counters) {
+        if (hipHostMalloc(&c->host_counters, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+            c->host_counters = nullptr;
+            return set_error(GSR_ERR_NOMEM, "context: hipHostMalloc failed");
+        }
+    }
+    return GSR_OK;
+}
+
+// Event slots: 0 start | cull+scan | 1 | preprocess | 2 ~sync~ 3 | depth sort | 4 |
+// counts+scan | 5 ~sync~ 6 | instance write | 7 | tile sort | 8 | ranges | 9 | composite | (end = slot 0 of next)
+// We record the end of the composite in slot [9] and the ranges end in [8] etc.
+enum { EV_START = 0, EV_CULL, EV_PRE, EV_AFTER_SYNC1, EV_DSORT, EV_COUNTS, EV_AFTER_SYNC2, EV_DUPW, EV_TSORT,
+       EV_RANGES_END_COMPOSITE_START, EV_COUNT };
+
+int prof_record(gsr_context* c, int slot, int ev, hipStream_t s) {
+    if (!c->prof_on) return GSR_OK;
+    GSR_HIP_CHECK(hipEventRecord(c->ev[slot][ev], s));
+    return GSR_OK;
+}
+
+void prof_accumulate(gsr_context* c, int slot, bool wait) {
+    if (!c->ev_pending[slot]) return;
+    hipEvent_t* e = c->ev[slot];
+    if (wait) (void)hipEventSynchronize(e[EV_COUNT]);
+    else if (hipEventQuery(e[EV_COUNT]) != hipSuccess) return;
+    auto el = [&](int a, int b) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e[a], e[b]);
+        return (double)ms;
+    };
+    c->acc_ms[GSR_STAGE_CULL] += el(EV_START, EV_CULL);
+    c->acc_ms[GSR_STAGE_PREPROCESS] += el(EV_CULL, EV_PRE);
+    c->acc_ms[GSR_STAGE_SYNC] += el(EV_PRE, EV_AFTER_SYNC1) + el(EV_COUNTS, EV_AFTER_SYNC2);
+    c->acc_ms[GSR_STAGE_DEPTH_SORT] += el(EV_AFTER_SYNC1, EV_DSORT);
+    c->acc_ms[GSR_STAGE_BINNING] += el(EV_DSORT, EV_COUNTS) + el(EV_AFTER_SYNC2, EV_DUPW);
+    c->acc_ms[GSR_STAGE_TILE_SORT] += el(EV_DUPW, EV_TSORT);
+    c->acc_ms[GSR_STAGE_RANGES] += el(EV_TSORT, EV_RANGES_END_COMPOSITE_START);
+    c->acc_ms[GSR_STAGE_COMPOSITE] += el(EV_RANGES_END_COMPOSITE_START, EV_COUNT);
+    c->prof_frames += 1;
+    c->ev_pending[slot] = false;
+}
+
+}  // namespace
+}  // namespace gsr
+
+using namespace gsr;
+
+extern "C" {
+
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+
+const char* gsr_last_error(void) { return last_error_ref().c_str(); }
+
+void gsr_settings_default(gsr_settings* s) {
+    if (!s) return;
+    std::memset(s, 0, sizeof(*s));
+    s->scale_modifier = 1.f;   // main.py:131
+    s->screen_scale = 1.f;     // main.py:132
+    s->render_mod = 6;         // main.py:134 (g_render_mode - 3 = 6: SH 0..3)
+    s->dc_factor = 1.f;        // renderer_ogl.py:185
+    s->extra_factor = 1.f;     // renderer_ogl.py:187
+    s->color_scale[0] = s->color_scale[1] = s->color_scale[2] = 1.f;  // renderer_ogl.py:183
+    s->rot_modifier[3] = 1.f;  // euler_to_quaternion(0,0,0) -> (x,y,z,w) = (0,0,0,1)
+    s->cube_rotation[0] = s->cube_rotation[4] = s->cube_rotation[8] = 1.f;
+    s->t_min = 1e-4f;
+    s->out_layout = 0;
+}
+
+static int validate_sh_dim(int32_t sh_dim) {
+    if (sh_dim < 3 || sh_dim > 48 || sh_dim % 3 != 0)
+        return set_error(GSR_ERR_INVALID, "sh_dim must be a multiple of 3 in [3, 48]");
+    return GSR_OK;
+}
+
+static int make_scene(int64_t n, int32_t sh_dim, gsr_scene** out, gsr_scene** sc) {
+    if (!out) return set_error(GSR_ERR_INVALID, "out is null");
+    *out = nullptr;
+    if (n < 0 || n > (int64_t)0x7fffffff) return set_error(GSR_ERR_OVERFLOW, "n out of range [0, 2^31)");
+    int rc = validate_sh_dim(sh_dim);
+    if (rc) return rc;
+    *sc = new gsr_scene();
+    (*sc)->d.n = n;
+    (*sc)->d.sh_dim = sh_dim;
+    (*sc)->d.sh_planes = (sh_dim + 3) / 4;
+    (void)hipGetDevice(&(*sc)->device);
+    return GSR_OK;
+}
+
+int gsr_scene_create(const float* xyz, const float* rot, const float* scale, const float* opacity, const float* sh,
+                     int64_t n, int32_t sh_dim, void* stream, gsr_scene** out) {
+    gsr_scene* sc = nullptr;
+    int rc = make_scene(n, sh_dim, out, &sc);
+    if (rc) return rc;
+    if (n > 0 && (!xyz || !rot || !scale || !opacity || !sh)) {
+        delete sc;
+        return set_error(GSR_ERR_INVALID, "null device pointer");
+    }
+    rc = scene_repack_from_fields(sc->d, xyz, rot, scale, opacity, sh, (hipStream_t)stream);
+    if (rc) {
+        if (sc->d.block) (void)hipFree(sc->d.block);
+        delete sc;
+        return rc;
+    }
+    *out = sc;
+    return GSR_OK;
+}
+
+int gsr_scene_create_flat(const float* flat, int64_t n, int32_t sh_dim, void* stream, gsr_scene** out) {
+    gsr_scene* sc = nullptr;
+    int rc = make_scene(n, sh_dim, out, &sc);
+    if (rc) return rc;
+    if (n > 0 && !flat) {
+        delete sc;
+        return set_error(GSR_ERR_INVALID, "null device pointer");
+    }
+    rc = scene_repack_from_flat(sc->d, flat, (hipStream_t)stream);
+    if (rc) {
+        if (sc->d.block) (void)hipFree(sc->d.block);
+        delete sc;
+        return rc;
+    }
+    *out = sc;
+    return GSR_OK;
+}
+
+int gsr_scene_destroy(gsr_scene* scene) {
+    if (!scene) return GSR_OK;
+    if (scene->d.block) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(scene->d.block);
+    }
+    delete scene;
+    return GSR_OK;
+}
+
+int64_t gsr_scene_count(const gsr_scene* scene) { return scene ? scene->d.n : -1; }
+int32_t gsr_scene_sh_dim(const gsr_scene* scene) { return scene ? scene->d.sh_dim : -1; }
+
+int gsr_context_create(gsr_context** out) {
+    if (!out) return set_error(GSR_ERR_INVALID, "out is null");
+    *out = new gsr_context();
+    return GSR_OK;
+}
+
+int gsr_context_destroy(gsr_context* c) {
+    if (!c) return GSR_OK;
+    (void)hipDeviceSynchronize();
+    c->vis_mask.release(); c->wave_counts.release(); c->scan_tmp.release(); c->recs.release();
+    c->keys_a.release(); c->keys_b.release(); c->vals_a.release(); c->vals_b.release();
+    c->dup_off.release(); c->tkeys_a.release(); c->tkeys_b.release(); c->tvals_a.release();
+    c->tvals_b.release(); c->radix_tmp.release(); c->ranges.release(); c->counters.release();
+    if (c->host_counters) (void)hipHostFree(c->host_counters);
+    for (auto& row : c->ev)
+        for (auto& e : row)
+            if (e) (void)hipEventDestroy(e);
+    delete c;
+    return GSR_OK;
+}
+
+int gsr_context_stats(const gsr_context* c, gsr_frame_stats* out) {
+    if (!c || !out) return set_error(GSR_ERR_INVALID, "null argument");
+    *out = c->stats;
+    return GSR_OK;
+}
+
+int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, float* out,
+               int32_t* radii, void* stream) {
+    if (!c || !sc || !cam || !st || !out) return set_error(GSR_ERR_INVALID, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    FrameUniforms u;
+    int rc = build_uniforms(sc, cam, st, u);
+    if (rc) return rc;
+    const size_t n = (size_t)sc->d.n;
+    const int num_tiles = u.tiles_x * u.tiles_y;
+    if ((rc = ensure_scene_buffers(c, n))) return rc;
+    if ((rc = c->ranges.ensure((size_t)num_tiles, "ranges"))) return rc;
+    uint32_t* n_vis_dev = c->counters.p;
+    uint32_t* n_dup_dev = c->counters.p + 1;
+    const int slot = (int)(c->frame_idx & 1);
+    if (c->prof_on) prof_accumulate(c, slot, true);  // slot reuse: frame k-2 is long done
+
+    c->stats = gsr_frame_stats{};
+    c->stats.n_gaussians = (int64_t)n;
+    c->stats.tiles_x = u.tiles_x;
+    c->stats.tiles_y = u.tiles_y;
+    c->last_depth_order = c->last_tile_list = nullptr;
+    c->last_tiles = num_tiles;
+
+    if ((rc = prof_record(c, slot, EV_START, s))) return rc;
+    GSR_HIP_CHECK(hipMemsetAsync(c->ranges.p, 0, sizeof(uint2) * (size_t)num_tiles, s));
+    uint32_t n_vis = 0, n_dup = 0;
+    if (n > 0) {
+        const size_t nw = (n + 63) / 64;
+        if ((rc = launch_cull(sc->d, u, c->vis_mask.p, c->wave_counts.p, s))) return rc;
+        if ((rc = scan_exclusive(c->wave_counts.p, c->wave_counts.p, nw, c->scan_tmp.p, n_vis_dev, s))) return rc;
+    } else {
+        GSR_HIP_CHECK(hipMemsetAsync(n_vis_dev, 0, sizeof(uint32_t), s));
+    }
+    if ((rc = prof_record(c, slot, EV_CULL, s))) return rc;
+    if (n > 0 && (rc = launch_preprocess(sc->d, u, c->vis_mask.p, c->wave_counts.p, n_vis_dev, c->recs.p,
+                                         c->keys_a.p, radii, s)))
+        return rc;
+    if ((rc = prof_record(c, slot, EV_PRE, s))) return rc;
+    // V sizes the depth-sort grid: one 4-byte read-back.
+    GSR_HIP_CHECK(hipMemcpyAsync(c->host_counters, n_vis_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    GSR_HIP_CHECK(hipStreamSynchronize(s));
+    n_vis = c->host_counters[0];
+    if (c->prof_on) prof_accumulate(c, slot ^ 1, false);  // previous frame finished before this sync
+    if ((rc = prof_record(c, slot, EV_AFTER_SYNC1, s))) return rc;
+
+    uint32_t *ka = c->keys_a.p, *kb = c->keys_b.p, *va = c->vals_a.p, *vb = c->vals_b.p;
+    if (n_vis > 0) {
+        if ((rc = radix_sort_pairs(&ka, &va, &kb, &vb, true, n_vis, 0, 32, c->radix_tmp.p, s))) return rc;
+        c->last_depth_order = va;
+    }
+    if ((rc = prof_record(c, slot, EV_DSORT, s))) return rc;
+    if (n_vis > 0) {
+        if ((rc = launch_dup_count(va, c->recs.p, n_vis, c->dup_off.p, s))) return rc;
+        if ((rc = scan_exclusive(c->dup_off.p, c->dup_off.p, n_vis, c->scan_tmp.p, n_dup_dev, s))) return rc;
+        if ((rc = prof_record(c, slot, EV_COUNTS, s))) return rc;
+        GSR_HIP_CHECK(hipMemcpyAsync(c->host_counters + 1, n_dup_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        GSR_HIP_CHECK(hipStreamSynchronize(s));
+        n_dup = c->host_counters[1];
+    } else {
+        if ((rc = prof_record(c, slot, EV_COUNTS, s))) return rc;
+    }
+    if ((rc = prof_record(c, slot, EV_AFTER_SYNC2, s))) return rc;
+
+    uint32_t* tile_list = c->tvals_a.p;
+    if (n_dup > 0) {
+        if ((rc = c->tkeys_a.ensure(n_dup, "tile_keys"))) return rc;
+        if ((rc = c->tkeys_b.ensure(n_dup, "tile_keys"))) return rc;
+        if ((rc = c->tvals_a.ensure(n_dup, "tile_vals"))) return rc;
+        if ((rc = c->tvals_b.ensure(n_dup, "tile_vals"))) return rc;
+        if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(n_dup), radix_tmp_elems(n)), "radix_tmp")))
+            return rc;
+        if ((rc = launch_dup_write(va, c->recs.p, n_vis, c->dup_off.p, u.tiles_x, c->tkeys_a.p, c->tvals_a.p, s)))
+            return rc;
+    }
+    if ((rc = prof_record(c, slot, EV_DUPW, s))) return rc;
+    uint32_t *tka = c->tkeys_a.p, *tkb = c->tkeys_b.p, *tva = c->tvals_a.p, *tvb = c->tvals_b.p;
+    if (n_dup > 0) {
+        const int tbits = bits_for((uint32_t)num_tiles);
+        if (tbits > 0 && (rc = radix_sort_pairs(&tka, &tva, &tkb, &tvb, false, n_dup, 0, tbits, c->radix_tmp.p, s)))
+            return rc;
+        tile_list = tva;
+        c->last_tile_list = tva;
+    }
+    if ((rc = prof_record(c, slot, EV_TSORT, s))) return rc;
+    if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, c->ranges.p, s))) return rc;
+    if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
+    if ((rc = launch_composite(c->ranges.p, tile_list, c->recs.p, u, frag_class_of(u.render_mod), st->t_min, st->bg,
+                               st->out_layout, out, s)))
+        return rc;
+    if ((rc = prof_record(c, slot, EV_COUNT, s))) return rc;
+    if (c->prof_on) c->ev_pending[slot] = true;
+    c->frame_idx += 1;
+    c->stats.n_visible = n_vis;
+    c->stats.n_instances = n_dup;
+    return GSR_OK;
+}
+
+int gsr_context_set_profiling(gsr_context* c, int32_t enable) {
+    if (!c) return set_error(GSR_ERR_INVALID, "null argument");
+    if (enable && !c->ev[0][0]) {
+        for (int a = 0; a < 2; ++a)
+            for (int b = 0; b <= EV_COUNT; ++b) GSR_HIP_CHECK(hipEventCreate(&c->ev[a][b]));
+    }
+    c->prof_on = enable != 0;
+    c->ev_pending[0] = c->ev_pending[1] = false;
+    for (double& v : c->acc_ms) v = 0.0;
+    c->prof_frames = 0;
+    return GSR_OK;
+}
+
+int gsr_context_stage_times(gsr_context* c, double* ms_out, int64_t* frames_out) {
+    if (!c || !ms_out) return set_error(GSR_ERR_INVALID, "null argument");
+    for (int k = 0; k < 2; ++k) prof_accumulate(c, (int)((c->frame_idx + k) & 1), true);
+    for (int k = 0; k < GSR_NUM_STAGES; ++k) ms_out[k] = c->acc_ms[k];
+    if (frames_out) *frames_out = c->prof_frames;
+    return GSR_OK;
+}
+
+int64_t gsr_debug_copy(const gsr_context* c, int32_t what, void* dst, int64_t max_bytes, void* stream) {
+    if (!c || !dst || max_bytes < 0) return set_error(GSR_ERR_INVALID, "null argument");
+    const void* src = nullptr;
+    int64_t bytes = 0;
+    switch (what) {
+        case GSR_DEBUG_RECORDS: src = c->recs.p; bytes = c->stats.n_visible * (int64_t)sizeof(SplatRec); break;
+        case GSR_DEBUG_DEPTH_ORDER: src = c->last_depth_order; bytes = c->stats.n_visible * 4; break;
+        case GSR_DEBUG_TILE_RANGES: src = c->ranges.p; bytes = c->last_tiles * 8; break;
+        case GSR_DEBUG_TILE_LIST: src = c->last_tile_list; bytes = c->stats.n_instances * 4; break;
+        default: return set_error(GSR_ERR_INVALID, "unknown debug array");
+    }
+    if (!src || bytes == 0) return 0;
+    if (bytes > max_bytes) bytes = max_bytes;
+    GSR_HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return bytes;
+}
+
+int gsr_sort_depth(gsr_context* c, const gsr_scene* sc, const float view[16], int32_t* index_dev, void* stream) {
+    if (!c || !sc || !view || !index_dev) return set_error(GSR_ERR_INVALID, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t n = (size_t)sc->d.n;
+    if (n == 0) return GSR_OK;
+    int rc = ensure_scene_buffers(c, n);
+    if (rc) return rc;
+    if ((rc = launch_depth_keys_all(sc->d, view, c->keys_a.p, s))) return rc;
+    uint32_t *ka = c->keys_a.p, *kb = c->keys_b.p, *va = c->vals_a.p, *vb = c->vals_b.p;
+    if ((rc = radix_sort_pairs(&ka, &va, &kb, &vb, true, n, 0, 32, c->radix_tmp.p, s))) return rc;
+    GSR_HIP_CHECK(hipMemcpyAsync(index_dev, va, n * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    return GSR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,169 @@
+// Internal definitions shared by the gsr HIP translation units (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+#include "gsr.h"
+
+namespace gsr {
+
+constexpr int kTile = 16;              // composite tile edge (pixels)
+constexpr int kWave = 64;              // CDNA wavefront
+
+// One visible splat after preprocess: 64 bytes, read wave-uniformly by the
+// compositor (scalar loads), so it is kept a single 64-B line.
+struct alignas(16) SplatRec {
+    float cx, cy;       // quad centre, window coords (origin bottom-left)
+    float sx, sy;       // coordxy = (pixel - centre) * s  (affine varying)
+    float A, B, C;      // conic (gau_vert.glsl:240)
+    float opacity;      // alpha varying
+    float r, g, b;      // colour varying (clamped to [0,1] unless mode -6)
+    int32_t x0, x1;     // covered pixel columns, inclusive (image coords)
+    int32_t r0, r1;     // covered pixel rows, inclusive (image coords, row 0 = top)
+    int32_t pad;
+};
+static_assert(sizeof(SplatRec) == 64, "SplatRec must be 64 bytes");
+
+// Render-mode classes of the fragment stage (gau_frag.glsl:16-52).
+enum FragClass : int { kFragGauss = 0, kFragBillboard = 1, kFragFlatBall = 2, kFragGaussBall = 3 };
+
+// Everything the per-Gaussian stage needs, passed by value (kernarg).
+struct FrameUniforms {
+    float V[16];            // row-major view
+    float P[16];            // row-major projection
+    float hfov[3];          // tan(fovx/2), tan(fovy/2), focal
+    float campos[3];
+    float gsf;              // gaussian_scale_factor
+    float sdsf;             // screen_display_scale_factor
+    float dc_factor, extra_factor;
+    float cscale[3];
+    float rotmod[4];        // (x,y,z,w)
+    float lcos[3], lsin[3]; // light rotation cos/sin per axis
+    float pcenter[3];
+    float obb_inv[9];       // row-major inverse(cube_rotation)
+    float cmin[3], cmax[3];
+    int32_t enable_aabb, enable_obb;
+    int32_t render_mod;
+    int32_t sh_dim;         // floats of SH per Gaussian (3, 12, 27, 48)
+    int32_t width, height;
+    int32_t tiles_x, tiles_y;
+};
+
+struct SceneData {
+    int64_t n = 0;
+    int32_t sh_dim = 0;
+    int32_t sh_planes = 0;      // ceil(sh_dim/4) float4 planes
+    float4* pos_op = nullptr;   // (x, y, z, opacity)            [n]
+    float4* rot = nullptr;      // (w, x, y, z)                  [n]
+    float4* scale = nullptr;    // (sx, sy, sz, 0)               [n]
+    float4* sh = nullptr;       // plane p at sh + p*n           [planes][n]
+    void* block = nullptr;      // single allocation backing all of the above
+};
+
+// ---------------------------------------------------------------- helpers
+std::string& last_error_ref();
+int set_error(int code, const std::string& msg);
+
+#define GSR_HIP_CHECK(expr)                                                      \
+    do {                                                                         \
+        hipError_t e_ = (expr);                                                  \
+        if (e_ != hipSuccess)                                                    \
+            return ::gsr::set_error(GSR_ERR_HIP, std::string(#expr) + ": " +    \
+                                                     hipGetErrorString(e_));     \
+    } while (0)
+
+#define GSR_LAUNCH_CHECK(what)                                                   \
+    do {                                                                         \
+        hipError_t e_ = hipGetLastError();                                       \
+        if (e_ != hipSuccess)                                                    \
+            return ::gsr::set_error(GSR_ERR_HIP, std::string("launch ") + what + \
+                                                     ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---------------------------------------------------------------- device utils
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const int l = __lane_id();
+    return (l == 0) ? 0ull : (~0ull >> (64 - l));
+}
+
+// Lanes of the wave holding the same 8-bit digit (only `valid` lanes).
+__device__ __forceinline__ uint64_t match_digit8(uint32_t digit, bool valid) {
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const bool bit = (digit >> b) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+    }
+    return peers;
+}
+
+// Inclusive wave scan (64 lanes).
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if (__lane_id() >= o) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_reduce_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// ---------------------------------------------------------------- host launchers
+// scan.hip: exclusive scan of n uint32 (in may equal out). Writes the total to
+// *total_dev (device) when non-null. tmp must hold scan_tmp_elems(n) uint32.
+size_t scan_tmp_elems(size_t n);
+int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
+                   uint32_t* total_dev, hipStream_t s);
+
+// radix_sort.hip: stable LSD sort of (key, val) by bits [begin_bit, end_bit).
+// Buffers are ping-ponged; the sorted result ends in (*keys_io, *vals_io)
+// (pointers swapped as needed). vals_in == nullptr means vals = 0..n-1.
+size_t radix_tmp_elems(size_t n);
+int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt,
+                     uint32_t** vals_alt, bool identity_vals, size_t n, int begin_bit,
+                     int end_bit, uint32_t* tmp, hipStream_t s);
+
+// scene.hip
+int scene_repack_from_fields(SceneData& sd, const float* xyz, const float* rot,
+                             const float* scale, const float* opacity, const float* sh,
+                             hipStream_t s);
+int scene_repack_from_flat(SceneData& sd, const float* flat, hipStream_t s);
+
+// preprocess.hip
+int launch_cull(const SceneData& sd, const FrameUniforms& u, uint64_t* vis_mask,
+                uint32_t* wave_counts, hipStream_t s);
+int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_t* vis_mask,
+                      const uint32_t* wave_off, const uint32_t* n_vis_dev, SplatRec* recs,
+                      uint32_t* depth_keys, int32_t* radii, hipStream_t s);
+int launch_depth_keys_all(const SceneData& sd, const float* V, uint32_t* keys, hipStream_t s);
+
+// composite.hip
+int launch_dup_count(const uint32_t* sorted_ids, const SplatRec* recs, uint32_t n_vis,
+                     uint32_t* counts, hipStream_t s);
+int launch_dup_write(const uint32_t* sorted_ids, const SplatRec* recs, uint32_t n_vis,
+                     const uint32_t* offsets, int tiles_x, uint32_t* tile_keys,
+                     uint32_t* tile_vals, hipStream_t s);
+int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
+                       hipStream_t s);
+int launch_composite(const uint2* ranges, const uint32_t* tile_vals, const SplatRec* recs,
+                     const FrameUniforms& u, int frag_class, float t_min, const float* bg,
+                     int out_layout, float* out, hipStream_t s);
+
+}  // namespace gsr
+
+struct gsr_scene {
+    gsr::SceneData d;
+    int device = 0;
+};

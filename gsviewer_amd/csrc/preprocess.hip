@@ -1,0 +1,426 @@
+// Per-Gaussian stage: box cull, view/projection + frustum cull, 3D->2D
+// covariance (EWA), conic, quad rectangle, SH->RGB.  The arithmetic restates
+// shaders/gau_vert.glsl:75-331 (and the fixed-function viewport transform)
+// in float32 with a fixed left-to-right evaluation order and NO contraction
+// (this file is compiled with -ffp-contract=off), so that per-splat values
+// match the CPU oracle (oracle/gl_oracle.py) bit for bit.
+//
+// Two launches per frame:
+//   k_cull        reads pos_op only (16 B/Gaussian), writes one visibility
+//                 ballot + count per wave;  -> scan of the wave counts
+//   k_preprocess  recomputes the cull for its lane, and for visible lanes
+//                 loads rot/scale/SH planes (coalesced float4), writes the
+//                 64-B SplatRec and the depth key at its compacted slot.
+// Compaction slot = n_vis-1-(rank in Gaussian-index order), so a stable
+// ascending depth sort resolves exact depth ties in DESCENDING index order:
+// the exact reverse of the GL draw order (renderer_ogl.py:24, ascending z,
+// ties by ascending index), i.e. front-to-back.
+#pragma clang fp contract(off)
+#include "gsr_internal.h"
+
+namespace gsr {
+namespace {
+
+constexpr int kThreads = 256;
+
+// gau_vert.glsl:3-18
+constexpr float SH_C0 = 0.28209479177387814f;
+constexpr float SH_C1 = 0.4886025119029199f;
+constexpr float SH_C2_0 = 1.0925484305920792f;
+constexpr float SH_C2_1 = -1.0925484305920792f;
+constexpr float SH_C2_2 = 0.31539156525252005f;
+constexpr float SH_C2_3 = -1.0925484305920792f;
+constexpr float SH_C2_4 = 0.5462742152960396f;
+constexpr float SH_C3_0 = -0.5900435899266435f;
+constexpr float SH_C3_1 = 2.890611442640554f;
+constexpr float SH_C3_2 = -0.4570457994644658f;
+constexpr float SH_C3_3 = 0.3731763325901154f;
+constexpr float SH_C3_4 = -0.4570457994644658f;
+constexpr float SH_C3_5 = 1.445305721320277f;
+constexpr float SH_C3_6 = -0.5900435899266435f;
+
+// isInsideRotatedCube (gau_vert.glsl:172-191)
+__device__ __forceinline__ bool inside_box(float x, float y, float z, const FrameUniforms& u) {
+    if (u.enable_obb == 1) {
+        const float dx = x - u.pcenter[0], dy = y - u.pcenter[1], dz = z - u.pcenter[2];
+        const float* M = u.obb_inv;
+        const float t0 = (M[0] * dx + M[1] * dy) + M[2] * dz;
+        const float t1 = (M[3] * dx + M[4] * dy) + M[5] * dz;
+        const float t2 = (M[6] * dx + M[7] * dy) + M[8] * dz;
+        return (t0 >= u.cmin[0]) & (t0 <= u.cmax[0]) & (t1 >= u.cmin[1]) & (t1 <= u.cmax[1]) &
+               (t2 >= u.cmin[2]) & (t2 <= u.cmax[2]);
+    }
+    if (u.enable_aabb == 1) {
+        const float t0 = x - u.pcenter[0], t1 = y - u.pcenter[1], t2 = z - u.pcenter[2];
+        return (t0 >= u.pcenter[0] + u.cmin[0]) & (t0 <= u.pcenter[0] + u.cmax[0]) &
+               (t1 >= u.pcenter[1] + u.cmin[1]) & (t1 <= u.pcenter[1] + u.cmax[1]) &
+               (t2 >= u.pcenter[2] + u.cmin[2]) & (t2 <= u.pcenter[2] + u.cmax[2]);
+    }
+    return true;
+}
+
+struct Projected {
+    float pv[4];
+    float ndc[3];
+    bool vis;
+};
+
+// gau_vert.glsl:209-218 + GL clip of |z_ndc| > 1 (all quad vertices share z).
+__device__ __forceinline__ Projected project(float x, float y, float z, const FrameUniforms& u) {
+    Projected o;
+    const float* V = u.V;
+    const float* P = u.P;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o.pv[i] = ((V[4 * i] * x + V[4 * i + 1] * y) + V[4 * i + 2] * z) + V[4 * i + 3];
+    float pc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        pc[i] = ((P[4 * i] * o.pv[0] + P[4 * i + 1] * o.pv[1]) + P[4 * i + 2] * o.pv[2]) + P[4 * i + 3] * o.pv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) o.ndc[k] = pc[k] / pc[3];
+    const float lim = 1.3f;
+    o.vis = (fabsf(o.ndc[0]) <= lim) & (fabsf(o.ndc[1]) <= lim) & (fabsf(o.ndc[2]) <= lim) &
+            (o.ndc[2] >= -1.0f) & (o.ndc[2] <= 1.0f);
+    o.vis = o.vis & inside_box(x, y, z, u);
+    return o;
+}
+
+// Exact integer span [p0,p1] of pixel indices p with lo <= p+0.5 < hi.
+__device__ __forceinline__ void pixel_span(float lo, float hi, int limit, int& p0, int& p1) {
+    if (!(lo == lo) || !(hi == hi)) {
+        p0 = limit;
+        p1 = -1;
+        return;
+    }
+    lo = fminf(fmaxf(lo, -1048576.f), 1048576.f);
+    hi = fminf(fmaxf(hi, -1048576.f), 1048576.f);
+    int a = (int)ceilf(lo - 0.5f);
+    if ((float)(a - 1) + 0.5f >= lo) --a;
+    if ((float)a + 0.5f < lo) ++a;
+    int b = (int)ceilf(hi - 0.5f) - 1;
+    if ((float)(b + 1) + 0.5f < hi) ++b;
+    if ((float)b + 0.5f >= hi) --b;
+    p0 = min(max(a, -1), limit);
+    p1 = min(max(b, -1), limit);
+}
+
+__device__ __forceinline__ uint32_t float_order_key(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+__global__ __launch_bounds__(kThreads) void k_cull(const float4* __restrict__ pos_op, int64_t n, FrameUniforms u,
+                                                   uint64_t* __restrict__ vis_mask, uint32_t* __restrict__ wave_counts) {
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    bool vis = false;
+    if (i < n) {
+        const float4 p = pos_op[i];
+        vis = project(p.x, p.y, p.z, u).vis;
+    }
+    const uint64_t m = __ballot(vis);
+    if (__lane_id() == 0) {
+        vis_mask[i >> 6] = m;
+        wave_counts[i >> 6] = (uint32_t)__popcll(m);
+    }
+}
+
+struct V3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ V3 normalize3(float vx, float vy, float vz) {
+    const float nn = sqrtf((vx * vx + vy * vy) + vz * vz);
+    return V3{vx / nn, vy / nn, vz / nn};
+}
+
+__device__ __forceinline__ float4 load_plane(const float4* __restrict__ sh, int64_t n, int p, int64_t i) {
+    return sh[(int64_t)p * n + i];
+}
+
+// Colour varying, gau_vert.glsl:251-330 (modes other than -3 / -2).
+__device__ __forceinline__ V3 sh_color(const float4* __restrict__ sh, int64_t n, int64_t i, float x, float y, float z,
+                                       const FrameUniforms& u) {
+    // dir = normalize(g_pos.xyz - cam_pos), rotateLightDirection
+    V3 d = normalize3(x - u.campos[0], y - u.campos[1], z - u.campos[2]);
+    float dx = d.x, dy = d.y, dz = d.z;
+    {
+        const float ry = dy * u.lcos[0] - dz * u.lsin[0];
+        const float rz = dy * u.lsin[0] + dz * u.lcos[0];
+        dy = ry;
+        dz = rz;
+    }
+    {
+        const float rx = dx * u.lcos[1] + dz * u.lsin[1];
+        const float rz = -dx * u.lsin[1] + dz * u.lcos[1];
+        dx = rx;
+        dz = rz;
+    }
+    {
+        const float rx = dx * u.lcos[2] - dy * u.lsin[2];
+        const float ry = dx * u.lsin[2] + dy * u.lcos[2];
+        dx = rx;
+        dy = ry;
+    }
+    const int sh_dim = u.sh_dim;
+    const int mode = u.render_mod;
+    // Load the SH floats needed at this degree: g[k] = coefficient k RGB.
+    float f[48];
+    const int need = (sh_dim > 27 && mode >= 3) ? 48 : (sh_dim > 12 && mode >= 2) ? 27 : (sh_dim > 3 && mode >= 1) ? 12 : 3;
+    const int planes = (need + 3) >> 2;
+#pragma unroll
+    for (int p = 0; p < 12; ++p) {
+        if (p < planes) {
+            const float4 t = load_plane(sh, n, p, i);
+            f[4 * p + 0] = t.x;
+            f[4 * p + 1] = t.y;
+            f[4 * p + 2] = t.z;
+            f[4 * p + 3] = t.w;
+        } else {
+            f[4 * p + 0] = f[4 * p + 1] = f[4 * p + 2] = f[4 * p + 3] = 0.f;
+        }
+    }
+#define G(k, c) f[3 * (k) + (c)]
+    float col[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) col[c] = SH_C0 * G(0, c);
+    if (sh_dim > 3 && mode >= 1) {
+        const float X = dx, Y = dy, Z = dz;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            col[c] = ((col[c] - (SH_C1 * Y) * G(1, c)) + (SH_C1 * Z) * G(2, c)) - (SH_C1 * X) * G(3, c);
+            col[c] = col[c] * u.dc_factor;
+        }
+        if (sh_dim > 12 && mode >= 2) {
+            const float xx = X * X, yy = Y * Y, zz = Z * Z;
+            const float xy = X * Y, yz = Y * Z, xz = X * Z;
+            const float k4 = SH_C2_0 * xy, k5 = SH_C2_1 * yz, k6 = SH_C2_2 * ((2.0f * zz - xx) - yy);
+            const float k7 = SH_C2_3 * xz, k8 = SH_C2_4 * (xx - yy);
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                col[c] = ((((col[c] + k4 * G(4, c)) + k5 * G(5, c)) + k6 * G(6, c)) + k7 * G(7, c)) + k8 * G(8, c);
+            if (sh_dim > 27 && mode >= 3) {
+                const float k9 = (SH_C3_0 * Y) * (3.0f * xx - yy);
+                const float k10 = (SH_C3_1 * xy) * Z;
+                const float k11 = (SH_C3_2 * Y) * ((4.0f * zz - xx) - yy);
+                const float k12 = (SH_C3_3 * Z) * ((2.0f * zz - 3.0f * xx) - 3.0f * yy);
+                const float k13 = (SH_C3_4 * X) * ((4.0f * zz - xx) - yy);
+                const float k14 = (SH_C3_5 * Z) * (xx - yy);
+                const float k15 = (SH_C3_6 * X) * (xx - 3.0f * yy);
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    col[c] = ((((((col[c] + k9 * G(9, c)) + k10 * G(10, c)) + k11 * G(11, c)) + k12 * G(12, c)) +
+                               k13 * G(13, c)) +
+                              k14 * G(14, c)) +
+                             k15 * G(15, c);
+            }
+#pragma unroll
+            for (int c = 0; c < 3; ++c) col[c] = col[c] * u.extra_factor;
+        }
+    }
+#undef G
+    V3 o;
+    o.x = (col[0] + 0.5f) * u.cscale[0];
+    o.y = (col[1] + 0.5f) * u.cscale[1];
+    o.z = (col[2] + 0.5f) * u.cscale[2];
+    return o;
+}
+
+__device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
+
+__global__ __launch_bounds__(kThreads) void k_preprocess(const float4* __restrict__ pos_op, const float4* __restrict__ rot,
+                                                         const float4* __restrict__ scale, const float4* __restrict__ sh,
+                                                         int64_t n, FrameUniforms u,
+                                                         const uint64_t* __restrict__ vis_mask,
+                                                         const uint32_t* __restrict__ wave_off,
+                                                         const uint32_t* __restrict__ n_vis_dev,
+                                                         SplatRec* __restrict__ recs, uint32_t* __restrict__ depth_keys,
+                                                         int32_t* __restrict__ radii) {
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t m = vis_mask[i >> 6];
+    const bool vis = (m >> __lane_id()) & 1ull;
+    if (!vis) {
+        if (radii) radii[i] = 0;
+        return;
+    }
+    const uint32_t slot = n_vis_dev[0] - 1u - (wave_off[i >> 6] + (uint32_t)__popcll(m & lanemask_lt()));
+
+    const float4 po = pos_op[i];
+    const float x = po.x, y = po.y, z = po.z;
+    const Projected pr = project(x, y, z, u);
+
+    // quatMultiply(g_rot, rot_modifier) (gau_vert.glsl:134-141, :224)
+    const float4 q1 = rot[i];
+    const float q1x = q1.x, q1y = q1.y, q1z = q1.z, q1w = q1.w;
+    const float q2x = u.rotmod[0], q2y = u.rotmod[1], q2z = u.rotmod[2], q2w = u.rotmod[3];
+    const float qx = ((q1w * q2x + q1x * q2w) + q1y * q2z) - q1z * q2y;
+    const float qy = ((q1w * q2y - q1x * q2z) + q1y * q2w) + q1z * q2x;
+    const float qz = ((q1w * q2z + q1x * q2y) - q1y * q2x) + q1z * q2w;
+    const float qw = ((q1w * q2w - q1x * q2x) - q1y * q2y) - q1z * q2z;
+
+    // computeCov3D (gau_vert.glsl:75-95): (r,x,y,z) = q.xyzw
+    const float4 sc4 = scale[i];
+    const float s[3] = {sc4.x * u.gsf, sc4.y * u.gsf, sc4.z * u.gsf};
+    const float r = qx, qx_ = qy, qy_ = qz, qz_ = qw;
+    const float R[3][3] = {
+        {1.0f - 2.0f * (qy_ * qy_ + qz_ * qz_), 2.0f * (qx_ * qy_ + r * qz_), 2.0f * (qx_ * qz_ - r * qy_)},
+        {2.0f * (qx_ * qy_ - r * qz_), 1.0f - 2.0f * (qx_ * qx_ + qz_ * qz_), 2.0f * (qy_ * qz_ + r * qx_)},
+        {2.0f * (qx_ * qz_ + r * qy_), 2.0f * (qy_ * qz_ - r * qx_), 1.0f - 2.0f * (qx_ * qx_ + qy_ * qy_)}};
+    float M[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) M[a][b] = s[a] * R[a][b];
+    float S[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = a; b < 3; ++b) {
+            S[a][b] = (M[0][a] * M[0][b] + M[1][a] * M[1][b]) + M[2][a] * M[2][b];
+            S[b][a] = S[a][b];
+        }
+
+    // computeCov2D (gau_vert.glsl:97-122)
+    const float fx = u.hfov[2], fy = u.hfov[2];
+    float tx = pr.pv[0], ty = pr.pv[1];
+    const float tz = pr.pv[2];
+    const float limx = 1.3f * u.hfov[0];
+    const float limy = 1.3f * u.hfov[1];
+    const float txtz = tx / tz;
+    const float tytz = ty / tz;
+    tx = fminf(limx, fmaxf(-limx, txtz)) * tz;
+    ty = fminf(limy, fmaxf(-limy, tytz)) * tz;
+    const float tz2 = tz * tz;
+    const float j0[3] = {fx / tz, 0.0f, -(fx * tx) / tz2};
+    const float j1[3] = {0.0f, fy / tz, -(fy * ty) / tz2};
+    const float* V = u.V;
+    float uu[3], vv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        uu[k] = (V[0 + k] * j0[0] + V[4 + k] * j0[1]) + V[8 + k] * j0[2];
+        vv[k] = (V[0 + k] * j1[0] + V[4 + k] * j1[1]) + V[8 + k] * j1[2];
+    }
+    float Su[3], Sv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        Su[k] = (S[k][0] * uu[0] + S[k][1] * uu[1]) + S[k][2] * uu[2];
+        Sv[k] = (S[k][0] * vv[0] + S[k][1] * vv[1]) + S[k][2] * vv[2];
+    }
+    const float ca = ((uu[0] * Su[0] + uu[1] * Su[1]) + uu[2] * Su[2]) + 0.3f;
+    const float cb = (vv[0] * Su[0] + vv[1] * Su[1]) + vv[2] * Su[2];
+    const float cc = ((vv[0] * Sv[0] + vv[1] * Sv[1]) + vv[2] * Sv[2]) + 0.3f;
+
+    // conic (gau_vert.glsl:235-240)
+    const float det = ca * cc - cb * cb;
+    const float det_inv = 1.0f / det;
+    SplatRec rec;
+    rec.A = cc * det_inv;
+    rec.B = -cb * det_inv;
+    rec.C = ca * det_inv;
+    rec.opacity = po.w;
+
+    // quad (gau_vert.glsl:225, 242-245) + viewport transform
+    const float wh[2] = {(2.0f * u.hfov[0]) * u.hfov[2], (2.0f * u.hfov[1]) * u.hfov[2]};
+    const float qs[2] = {3.0f * sqrtf(ca), 3.0f * sqrtf(cc)};
+    const float half[2] = {(float)u.width * 0.5f, (float)u.height * 0.5f};
+    float lo[2], hi[2], cw[2], sc[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const float qn = qs[k] / wh[k] * 2.0f;
+        const float off = qn * u.sdsf;
+        lo[k] = (pr.ndc[k] + (-off)) * half[k] + half[k];
+        hi[k] = (pr.ndc[k] + off) * half[k] + half[k];
+        cw[k] = pr.ndc[k] * half[k] + half[k];
+        sc[k] = qs[k] / ((hi[k] - lo[k]) * 0.5f);
+    }
+    rec.cx = cw[0];
+    rec.cy = cw[1];
+    rec.sx = sc[0];
+    rec.sy = sc[1];
+    int x0, x1, j0i, j1i;
+    pixel_span(lo[0], hi[0], u.width, x0, x1);
+    pixel_span(lo[1], hi[1], u.height, j0i, j1i);
+    x0 = max(x0, 0);
+    x1 = min(x1, u.width - 1);
+    j0i = max(j0i, 0);
+    j1i = min(j1i, u.height - 1);
+    rec.x0 = x0;
+    rec.x1 = x1;
+    rec.r0 = (u.height - 1) - j1i;
+    rec.r1 = (u.height - 1) - j0i;
+    rec.pad = 0;
+
+    // colour varying
+    const int mode = u.render_mod;
+    V3 col;
+    if (mode == -3) {  // depth (gau_vert.glsl:252-259)
+        float d = -pr.pv[2];
+        d = (d < 0.05f) ? 1.0f : d;
+        d = 1.0f / d;
+        col = V3{d, d, d};
+    } else if (mode == -2 || mode == -1) {
+        // -2: normal colour (gau_vert.glsl:265-272); -1: billboard normal
+        // fragment colour = 0.5*(normalize(approxNormal)+1) (gau_frag.glsl:23-27)
+        V3 nrm = normalize3(u.campos[0] - x, u.campos[1] - y, u.campos[2] - z);
+        if (mode == -1) nrm = normalize3(nrm.x, nrm.y, nrm.z);
+        col = V3{0.5f * (nrm.x + 1.0f), 0.5f * (nrm.y + 1.0f), 0.5f * (nrm.z + 1.0f)};
+    } else {
+        col = sh_color(sh, n, i, x, y, z, u);
+    }
+    if (mode != -6) {  // unorm target clamps the fragment colour
+        col.x = clamp01(col.x);
+        col.y = clamp01(col.y);
+        col.z = clamp01(col.z);
+    }
+    rec.r = col.x;
+    rec.g = col.y;
+    rec.b = col.z;
+
+    float4* dst = reinterpret_cast<float4*>(recs + slot);
+    dst[0] = make_float4(rec.cx, rec.cy, rec.sx, rec.sy);
+    dst[1] = make_float4(rec.A, rec.B, rec.C, rec.opacity);
+    dst[2] = make_float4(rec.r, rec.g, rec.b, __int_as_float(rec.x0));
+    dst[3] = make_float4(__int_as_float(rec.x1), __int_as_float(rec.r0), __int_as_float(rec.r1), 0.f);
+    depth_keys[slot] = float_order_key(-pr.pv[2]);
+    if (radii) {
+        const float rr = ceilf(fmaxf(qs[0], qs[1]));
+        radii[i] = (rr >= 0.f && rr < 2147483520.f) ? (int32_t)rr : 0;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_depth_keys_all(const float4* __restrict__ pos_op, int64_t n, float v8,
+                                                             float v9, float v10, float v11, uint32_t* __restrict__ keys) {
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = pos_op[i];
+    keys[i] = float_order_key(((v8 * p.x + v9 * p.y) + v10 * p.z) + v11);
+}
+
+}  // namespace
+
+int launch_cull(const SceneData& sd, const FrameUniforms& u, uint64_t* vis_mask, uint32_t* wave_counts,
+                hipStream_t s) {
+    const unsigned grid = (unsigned)((sd.n + kThreads - 1) / kThreads);
+    k_cull<<<grid, kThreads, 0, s>>>(sd.pos_op, sd.n, u, vis_mask, wave_counts);
+    GSR_LAUNCH_CHECK("cull");
+    return GSR_OK;
+}
+
+int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_t* vis_mask,
+                      const uint32_t* wave_off, const uint32_t* n_vis_dev, SplatRec* recs, uint32_t* depth_keys,
+                      int32_t* radii, hipStream_t s) {
+    const unsigned grid = (unsigned)((sd.n + kThreads - 1) / kThreads);
+    k_preprocess<<<grid, kThreads, 0, s>>>(sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, u, vis_mask, wave_off, n_vis_dev,
+                                           recs, depth_keys, radii);
+    GSR_LAUNCH_CHECK("preprocess");
+    return GSR_OK;
+}
+
+int launch_depth_keys_all(const SceneData& sd, const float* V, uint32_t* keys, hipStream_t s) {
+    const unsigned grid = (unsigned)((sd.n + kThreads - 1) / kThreads);
+    k_depth_keys_all<<<grid, kThreads, 0, s>>>(sd.pos_op, sd.n, V[8], V[9], V[10], V[11], keys);
+    GSR_LAUNCH_CHECK("depth_keys_all");
+    return GSR_OK;
+}
+
+}  // namespace gsr

@@ -1,0 +1,320 @@
+"""Drop-in rasterizer front-ends over the HIP C ABI.
+
+* ``GaussianRasterizationSettings`` / ``GaussianRasterizer`` -- the interface
+  ``render/renderer_cuda.py`` binds (``renderer_cuda.py:13, 76-89, 107-120,
+  230-243``): same field names, same call signature, returns
+  ``(color[3,H,W], radii[N])``.
+* ``render(scene, camera, settings)`` -- ``CUDARenderer.draw``'s tensor result
+  (``renderer_cuda.py:245-247`` without the GL interop): ``[H,W,3]``.
+* ``HipScene`` -- a device-resident static Gaussian set (``gsr_scene``).
+
+Everything computes on the GPU through ``libgsr.so``; there is no fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import NamedTuple, Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from .camera import euler_to_quaternion, euler_to_rotation_matrix
+
+F = np.float32
+
+# GaussianData / GaussianDataCUDA field order (renderer_cuda.py:60-73)
+_FIELDS = ("xyz", "rot", "scale", "opacity", "sh")
+
+
+def _stream_handle(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _dev_f32(t: torch.Tensor, name: str, shape_tail=None) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        t = torch.as_tensor(np.asarray(t, np.float32))
+    if not t.is_cuda:
+        t = t.cuda()
+    t = t.float().contiguous()
+    if shape_tail is not None and tuple(t.shape[1:]) != tuple(shape_tail):
+        raise RuntimeError(f"{name}: expected shape [N, {', '.join(map(str, shape_tail))}], got {tuple(t.shape)}")
+    return t
+
+
+class HipScene:
+    """Static Gaussian set repacked once into SoA float4 planes in HBM."""
+
+    def __init__(self, xyz, rot, scale, opacity, sh, stream=None):
+        lib = _lib.load()
+        n = int(xyz.shape[0])
+        sh = sh.reshape(n, -1) if isinstance(sh, torch.Tensor) else np.asarray(sh).reshape(n, -1)
+        self._keep = [_dev_f32(xyz, "xyz", (3,)), _dev_f32(rot, "rot", (4,)), _dev_f32(scale, "scale", (3,)),
+                      _dev_f32(opacity, "opacity").reshape(n, 1), _dev_f32(sh, "sh")]
+        self.n = n
+        self.sh_dim = int(self._keep[4].shape[1])
+        h = ctypes.c_void_p()
+        _lib.check(lib.gsr_scene_create(*[ctypes.c_void_p(t.data_ptr()) for t in self._keep], n, self.sh_dim,
+                                        _stream_handle(stream), ctypes.byref(h)), "gsr_scene_create")
+        self._h = h
+        self._keep = None  # repack is stream-ordered; torch's caching allocator keeps the memory valid
+
+    @classmethod
+    def from_gaussian_data(cls, g, stream=None):
+        return cls(*(getattr(g, f) for f in _FIELDS), stream=stream)
+
+    @classmethod
+    def from_flat(cls, flat, sh_dim: int, stream=None):
+        lib = _lib.load()
+        obj = cls.__new__(cls)
+        flat = _dev_f32(flat, "flat", (11 + sh_dim,))
+        obj.n, obj.sh_dim = int(flat.shape[0]), int(sh_dim)
+        h = ctypes.c_void_p()
+        _lib.check(lib.gsr_scene_create_flat(ctypes.c_void_p(flat.data_ptr()), obj.n, obj.sh_dim,
+                                             _stream_handle(stream), ctypes.byref(h)), "gsr_scene_create_flat")
+        obj._h = h
+        obj._keep = None
+        return obj
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().gsr_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return self.n
+
+
+class HipContext:
+    """Per-stream frame workspace (``gsr_context``)."""
+
+    def __init__(self):
+        h = ctypes.c_void_p()
+        _lib.check(_lib.load().gsr_context_create(ctypes.byref(h)), "gsr_context_create")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def stats(self) -> dict:
+        st = _lib.GsrFrameStats()
+        _lib.check(_lib.load().gsr_context_stats(self._h, ctypes.byref(st)), "gsr_context_stats")
+        return {f: getattr(st, f) for f, _ in st._fields_}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().gsr_context_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class RenderSettings:
+    """Uniform state of the OGL path (gau_vert.glsl:47-67) with the reference
+    start-up defaults (main.py:128-137, renderer_ogl.py:183-187)."""
+
+    def __init__(self, **kw):
+        self.scale_modifier = 1.0
+        self.screen_scale = 1.0
+        self.render_mod = 6
+        self.dc_factor = 1.0
+        self.extra_factor = 1.0
+        self.color_scale = [1.0, 1.0, 1.0]
+        self.rot_modifier = [0.0, 0.0, 0.0, 1.0]   # (x,y,z,w)
+        self.light_rotation = [0.0, 0.0, 0.0]
+        self.enable_aabb = 0
+        self.enable_obb = 0
+        self.cube_rotation = np.eye(3)
+        self.cube_min = [0.0, 0.0, 0.0]
+        self.cube_max = [0.0, 0.0, 0.0]
+        self.points_center = [0.0, 0.0, 0.0]
+        self.bg = [0.0, 0.0, 0.0]
+        self.t_min = 1e-4
+        self.out_layout = 1
+        for k, v in kw.items():
+            if not hasattr(self, k):
+                raise KeyError(k)
+            setattr(self, k, v)
+
+    def set_rot_modifier_euler(self, euler_deg):
+        self.rot_modifier = list(euler_to_quaternion(*euler_deg))
+
+    def set_cube_rotation_euler(self, euler_deg):
+        self.cube_rotation = euler_to_rotation_matrix(euler_deg)
+
+    def to_c(self) -> _lib.GsrSettings:
+        s = _lib.GsrSettings()
+        s.scale_modifier = float(self.scale_modifier)
+        s.screen_scale = float(self.screen_scale)
+        s.render_mod = int(self.render_mod)
+        s.dc_factor = float(self.dc_factor)
+        s.extra_factor = float(self.extra_factor)
+        s.color_scale[:] = [float(v) for v in self.color_scale]
+        s.rot_modifier[:] = [float(v) for v in self.rot_modifier]
+        s.light_rotation[:] = [float(v) for v in self.light_rotation]
+        s.enable_aabb = int(self.enable_aabb)
+        s.enable_obb = int(self.enable_obb)
+        s.cube_rotation[:] = [float(v) for v in np.asarray(self.cube_rotation, np.float32).reshape(9)]
+        s.cube_min[:] = [float(v) for v in self.cube_min]
+        s.cube_max[:] = [float(v) for v in self.cube_max]
+        s.points_center[:] = [float(v) for v in self.points_center]
+        s.bg[:] = [float(v) for v in self.bg]
+        s.t_min = float(self.t_min)
+        s.out_layout = int(self.out_layout)
+        return s
+
+
+def camera_struct(view, proj, campos, hfovxy_focal, width, height) -> _lib.GsrCamera:
+    c = _lib.GsrCamera()
+    c.view[:] = [float(v) for v in np.asarray(view, np.float32).reshape(16)]
+    c.proj[:] = [float(v) for v in np.asarray(proj, np.float32).reshape(16)]
+    c.campos[:] = [float(v) for v in np.asarray(campos, np.float32).reshape(3)]
+    c.hfovxy_focal[:] = [float(v) for v in np.asarray(hfovxy_focal, np.float32).reshape(3)]
+    c.width, c.height = int(width), int(height)
+    return c
+
+
+def camera_from(camera) -> _lib.GsrCamera:
+    """gsr_camera from a ``gsviewer_amd.camera.Camera`` (util.Camera twin)."""
+    V = camera.get_view_matrix()
+    return camera_struct(V, camera.get_project_matrix(), camera.position, camera.get_htanfovxy_focal(),
+                         camera.w, camera.h)
+
+
+def render_into(ctx: HipContext, scene: HipScene, cam: _lib.GsrCamera, settings: RenderSettings,
+                out: torch.Tensor, radii: Optional[torch.Tensor] = None, stream=None):
+    """Render one frame into a preallocated float32 CUDA tensor (3*H*W)."""
+    if not (out.is_cuda and out.dtype == torch.float32 and out.is_contiguous()):
+        raise RuntimeError("out must be a contiguous float32 CUDA tensor")
+    if out.numel() != 3 * cam.width * cam.height:
+        raise RuntimeError("out has the wrong number of elements")
+    rp = ctypes.c_void_p(radii.data_ptr()) if radii is not None else None
+    st = settings.to_c()
+    _lib.check(_lib.load().gsr_render(ctx.handle, scene.handle, ctypes.byref(cam), ctypes.byref(st),
+                                      ctypes.c_void_p(out.data_ptr()), rp, _stream_handle(stream)), "gsr_render")
+    return out
+
+
+_default_ctx = {}
+
+
+def _ctx_for_device():
+    dev = torch.cuda.current_device()
+    if dev not in _default_ctx:
+        _default_ctx[dev] = HipContext()
+    return _default_ctx[dev]
+
+
+def render(scene: HipScene, camera, settings: Optional[RenderSettings] = None) -> torch.Tensor:
+    """``CUDARenderer.draw`` image (renderer_cuda.py:245-247): [H, W, 3] float32,
+    row 0 = top of the screen."""
+    settings = settings or RenderSettings()
+    cam = camera if isinstance(camera, _lib.GsrCamera) else camera_from(camera)
+    s = RenderSettings(**{k: getattr(settings, k) for k in vars(settings)})
+    s.out_layout = 1
+    out = torch.empty((cam.height, cam.width, 3), dtype=torch.float32, device="cuda")
+    return render_into(_ctx_for_device(), scene, cam, s, out)
+
+
+def depth_order(scene: HipScene, view) -> torch.Tensor:
+    """Back-to-front order (ascending view z) of all Gaussians: the
+    ``_sort_gaussian_*`` service of renderer_ogl.py:16-59, as int32 [N, 1]."""
+    out = torch.empty((scene.n, 1), dtype=torch.int32, device="cuda")
+    v = (ctypes.c_float * 16)(*[float(x) for x in np.asarray(view, np.float32).reshape(16)])
+    _lib.check(_lib.load().gsr_sort_depth(_ctx_for_device().handle, scene.handle, ctypes.byref(v),
+                                          ctypes.c_void_p(out.data_ptr()), _stream_handle()), "gsr_sort_depth")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# diff_gaussian_rasterization-compatible interface (renderer_cuda.py:76-89, 230-243)
+# ---------------------------------------------------------------------------
+class GaussianRasterizationSettings(NamedTuple):
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool = False
+    debug: bool = False
+
+
+_FLIP = np.diag([-1.0, 1.0, -1.0, 1.0])
+
+
+def gl_matrices_from_settings(rs: GaussianRasterizationSettings):
+    """Invert CUDARenderer's camera conversion (renderer_cuda.py:196-213):
+    viewmatrix = V'^T, projmatrix = (P V')^T with V' = diag(-1,1,-1,1) V.
+    Returns the GL-convention (V, P) the OGL shaders use."""
+    Vp = np.asarray(rs.viewmatrix.detach().cpu().numpy(), np.float64).T
+    PVp = np.asarray(rs.projmatrix.detach().cpu().numpy(), np.float64).T
+    V = _FLIP @ Vp
+    P = PVp @ np.linalg.inv(Vp)
+    return V.astype(np.float32), P.astype(np.float32)
+
+
+class GaussianRasterizer(torch.nn.Module):
+    """Same constructor and forward signature as
+    ``diff_gaussian_rasterization.GaussianRasterizer`` as bound by
+    renderer_cuda.py:230-243.  Returns ``(color[3,H,W], radii[N] int32)``.
+
+    Arithmetic is the reference OpenGL path's;
+    ``sh_degree`` caps the SH degree like render_mod does in gau_vert.glsl.
+    The static scene is repacked only when an input tensor changes."""
+
+    def __init__(self, raster_settings: GaussianRasterizationSettings):
+        super().__init__()
+        self.raster_settings = raster_settings
+        self._scene = None
+        self._scene_key = None
+
+    def _scene_for(self, tensors):
+        key = tuple((t.data_ptr(), tuple(t.shape), t._version) for t in tensors)
+        if key != self._scene_key:
+            self._scene = HipScene(*tensors)
+            self._scene_key = key
+        return self._scene
+
+    def forward(self, means3D, means2D=None, opacities=None, shs=None, colors_precomp=None, scales=None,
+                rotations=None, cov3D_precomp=None):
+        if colors_precomp is not None or cov3D_precomp is not None:
+            raise RuntimeError("colors_precomp / cov3D_precomp are not part of the reference path "
+                               "(renderer_cuda.py:234-243 passes None)")
+        if shs is None or scales is None or rotations is None or opacities is None:
+            raise RuntimeError("means3D, opacities, shs, scales and rotations are required")
+        rs = self.raster_settings
+        n = means3D.shape[0]
+        scene = self._scene_for([means3D.contiguous(), rotations.contiguous(), scales.contiguous(),
+                                 opacities.contiguous(), shs.reshape(n, -1).contiguous()])
+        V, P = gl_matrices_from_settings(rs)
+        campos = rs.campos.detach().cpu().numpy()
+        H, W = int(rs.image_height), int(rs.image_width)
+        focal = H / (2.0 * float(rs.tanfovy))
+        cam = camera_struct(V, P, campos, [rs.tanfovx, rs.tanfovy, focal], W, H)
+        st = RenderSettings(scale_modifier=rs.scale_modifier, render_mod=int(rs.sh_degree),
+                            bg=[float(v) for v in rs.bg.detach().cpu().numpy().reshape(3)], out_layout=0)
+        color = torch.empty((3, H, W), dtype=torch.float32, device=means3D.device)
+        radii = torch.empty((n,), dtype=torch.int32, device=means3D.device)
+        render_into(_ctx_for_device(), scene, cam, st, color, radii)
+        return color, radii

@@ -1,0 +1,173 @@
+/*
+ * gsr.h -- C ABI of the MI355X-native Gaussian-splat forward rasterizer.
+ *
+ * This library is the drop-in for ONE path of Lucasmogsan/GSViewer: the
+ * per-frame forward rasterization of a static Gaussian set for one camera,
+ * i.e. what `render/renderer_cuda.py:230-243` hands to the third-party
+ * `diff_gaussian_rasterization.GaussianRasterizer`, with the arithmetic of the
+ * reference's OpenGL path (`shaders/gau_vert.glsl`, `shaders/gau_frag.glsl`,
+ * GL blend state `render/renderer_ogl.py:178-180`).
+ *
+ * Conventions
+ *  - every pointer argument named *_dev is DEVICE memory (HIP, the caller's
+ *    device); everything else is host memory.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *  - functions return GSR_OK (0) or a negative gsr_status; the message of the
+ *    most recent failure on the calling thread is gsr_last_error().
+ *  - matrices are float[16] ROW-MAJOR math matrices (M[r*4+c]), i.e. exactly
+ *    the NumPy arrays the reference builds (`util.py:61-93`) before
+ *    `util.set_uniform_mat4` transposes them for the column-major GL upload
+ *    (`util.py:364-375`).
+ *
+ * Thread safety: a gsr_scene is immutable after creation and may be rendered
+ * concurrently from several gsr_context objects (one per stream). A
+ * gsr_context must not be used by two threads at once.
+ */
+#ifndef GSR_H_
+#define GSR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_ABI_VERSION 1
+
+typedef enum gsr_status {
+    GSR_OK = 0,
+    GSR_ERR_INVALID = -1,   /* bad argument (null pointer, size, layout) */
+    GSR_ERR_HIP = -2,       /* HIP runtime error (launch / alloc / copy)  */
+    GSR_ERR_NOMEM = -3,     /* device allocation failed                   */
+    GSR_ERR_OVERFLOW = -4   /* a capacity would exceed 2^31 entries       */
+} gsr_status;
+
+typedef struct gsr_scene gsr_scene;      /* static Gaussian set, SoA in HBM   */
+typedef struct gsr_context gsr_context;  /* per-stream frame workspace        */
+
+/* Camera for one frame.
+ * Replaces the uniforms view_matrix / projection_matrix / cam_pos /
+ * hfovxy_focal (gau_vert.glsl:47-50, uploaded by renderer_ogl.py:282-292)
+ * and the viewmatrix/projmatrix/campos/tanfov fields of the raster settings
+ * (renderer_cuda.py:196-213). */
+typedef struct gsr_camera {
+    float view[16];          /* V: world -> GL camera (lookAt, util.py:61-76)      */
+    float proj[16];          /* P: GL perspective, z_ndc in [-1,1] (util.py:78-93) */
+    float campos[3];         /* camera position in world space                      */
+    float hfovxy_focal[3];   /* tan(fovx/2), tan(fovy/2), focal (util.py:181-185)   */
+    int32_t width, height;   /* image size in pixels                                */
+} gsr_camera;
+
+/* Appearance / culling state: the remaining uniforms of gau_vert.glsl:51-67
+ * and the OGL renderer setters (renderer_ogl.py:246-318). */
+typedef struct gsr_settings {
+    float scale_modifier;        /* gaussian_scale_factor (set_scale_modifier)           */
+    float screen_scale;          /* screen_display_scale_factor (set_screen_scale_factor) */
+    int32_t render_mod;          /* render_mod: 0..3 SH degree cap (>=3: full), -1 billboard
+                                    normal, -2 normal, -3 depth, -4 billboard, -5 flat ball,
+                                    -6 gaussian ball (gs_elements_control.py:175 maps UI) */
+    float dc_factor;             /* adjust_dc_features                                    */
+    float extra_factor;          /* adjust_extra_features                                 */
+    float color_scale[3];        /* color_scale_factors (update_color_factor)             */
+    float rot_modifier[4];       /* quaternion uniform (x,y,z,w) (set_rot_modifier)       */
+    float light_rotation[3];     /* degrees about X,Y,Z (set_light_rotation)              */
+    int32_t enable_aabb;         /* set_enable_aabb                                       */
+    int32_t enable_obb;          /* set_enable_obb                                        */
+    float cube_rotation[9];      /* row-major R (set_cube_rotation, util.py:453-479)      */
+    float cube_min[3];           /* cubeMin                                               */
+    float cube_max[3];           /* cubeMax                                               */
+    float points_center[3];      /* points_center (set_points_center)                     */
+    float bg[3];                 /* background (clear colour (0,0,0), main.py:197)        */
+    float t_min;                 /* stop a pixel once transmittance < t_min (0 = never)   */
+    int32_t out_layout;          /* 0: planar [3,H,W] (rasterizer output, renderer_cuda.py:234)
+                                    1: interleaved [H,W,3] (renderer_cuda.py:245)          */
+} gsr_settings;
+
+/* Per-frame statistics of the last gsr_render on a context. */
+typedef struct gsr_frame_stats {
+    int64_t n_gaussians;     /* N                                          */
+    int64_t n_visible;       /* passed box + frustum cull                  */
+    int64_t n_instances;     /* (splat, 16x16 tile) pairs composited       */
+    int32_t tiles_x, tiles_y;
+} gsr_frame_stats;
+
+int gsr_abi_version(void);
+const char* gsr_last_error(void);
+
+/* Reference start-up uniform state (main.py:128-137, renderer_ogl.py:183-187). */
+void gsr_settings_default(gsr_settings* s);
+
+/* Create a scene from device arrays in the GaussianData layout
+ * (util_gau.py:10-42, GaussianDataCUDA renderer_cuda.py:60-101):
+ *   xyz [n,3], rot [n,4] (w,x,y,z), scale [n,3] (activated), opacity [n,1]
+ *   (activated), sh [n, sh_dim] coefficient-major RGB-interleaved.
+ * sh_dim is GaussianData.sh_dim (3, 12, 27 or 48). The data is repacked once
+ * into library-owned SoA planes; inputs may be freed afterwards. Ordered on
+ * `stream`. Replaces OpenGLRenderer.update_gaussian_data (renderer_ogl.py:235)
+ * and CUDARenderer.update_gaussian_data (renderer_cuda.py:147). */
+int gsr_scene_create(const float* xyz_dev, const float* rot_dev, const float* scale_dev,
+                     const float* opacity_dev, const float* sh_dev, int64_t n, int32_t sh_dim,
+                     void* stream, gsr_scene** out);
+
+/* Same, from the flat() AoS record buffer the OGL path uploads as SSBO 0:
+ * [n, 11 + sh_dim] floats (util_gau.py:40-42, gau_vert.glsl:28-42). */
+int gsr_scene_create_flat(const float* flat_dev, int64_t n, int32_t sh_dim, void* stream,
+                          gsr_scene** out);
+
+int gsr_scene_destroy(gsr_scene* scene);
+int64_t gsr_scene_count(const gsr_scene* scene);
+int32_t gsr_scene_sh_dim(const gsr_scene* scene);
+
+/* Frame workspace. Device buffers grow on demand and are reused. */
+int gsr_context_create(gsr_context** out);
+int gsr_context_destroy(gsr_context* ctx);
+
+/* Render one frame: cull + project + SH (preprocess), depth radix sort,
+ * tile binning + stable tile sort, 16x16-tile front-to-back compositing.
+ * out_image_dev: float32, 3*H*W, layout per settings->out_layout, row 0 = top.
+ * radii_dev: optional int32 [n]; 0 for culled Gaussians, else
+ *            ceil(max(quad half-width, half-height)) in pixels.
+ * Replaces CUDARenderer.draw's rasterizer call (renderer_cuda.py:230-243) and
+ * OpenGLRenderer.draw + sort_and_update (renderer_ogl.py:263-268, 406-412). */
+int gsr_render(gsr_context* ctx, const gsr_scene* scene, const gsr_camera* cam,
+               const gsr_settings* settings, float* out_image_dev, int32_t* radii_dev,
+               void* stream);
+
+int gsr_context_stats(const gsr_context* ctx, gsr_frame_stats* out);
+
+/* Back-to-front Gaussian order for a view matrix: the renderer_ogl
+ * _sort_gaussian_{cpu,torch,cupy} service (renderer_ogl.py:16-59) as a device
+ * radix sort. Writes index_dev[n] (int32, ascending view-space z; ties keep
+ * ascending index). */
+int gsr_sort_depth(gsr_context* ctx, const gsr_scene* scene, const float view[16],
+                   int32_t* index_dev, void* stream);
+
+/* Optional per-stage GPU timing with HIP events recorded on the render stream
+ * (no extra synchronisation in the frame; accumulated lazily).
+ * Stages: cull (+ visible-count scan), preprocess, depth sort, binning
+ * (tile counts, scan, instance write), tile sort, tile ranges, composite, and
+ * `sync` = GPU idle time while the host reads the visible/instance counts. */
+enum { GSR_STAGE_CULL = 0, GSR_STAGE_PREPROCESS = 1, GSR_STAGE_DEPTH_SORT = 2, GSR_STAGE_BINNING = 3,
+       GSR_STAGE_TILE_SORT = 4, GSR_STAGE_RANGES = 5, GSR_STAGE_COMPOSITE = 6, GSR_STAGE_SYNC = 7,
+       GSR_NUM_STAGES = 8 };
+int gsr_context_set_profiling(gsr_context* ctx, int32_t enable);   /* resets the accumulators */
+/* Sum of per-stage milliseconds over the profiled frames since the last reset
+ * (waits for the last profiled frame's events). */
+int gsr_context_stage_times(gsr_context* ctx, double* ms_out /* [GSR_NUM_STAGES] */, int64_t* frames_out);
+
+/* Test hook: copy an internal array of the last gsr_render on `ctx` into
+ * dst_dev (device memory, at most max_bytes). Returns the number of bytes
+ * copied (>= 0) or a negative gsr_status.  what:
+ *   GSR_DEBUG_RECORDS      64-B splat records in compacted slot order
+ *                          (slot s = the s-th visible Gaussian in DESCENDING id order)
+ *   GSR_DEBUG_DEPTH_ORDER  uint32 record slots, front-to-back
+ *   GSR_DEBUG_TILE_RANGES  uint32 pairs [begin, end) per 16x16 tile (row-major tiles)
+ *   GSR_DEBUG_TILE_LIST    uint32 record slots of all (tile, splat) instances, by tile then depth */
+enum { GSR_DEBUG_RECORDS = 0, GSR_DEBUG_DEPTH_ORDER = 1, GSR_DEBUG_TILE_RANGES = 2, GSR_DEBUG_TILE_LIST = 3 };
+int64_t gsr_debug_copy(const gsr_context* ctx, int32_t what, void* dst_dev, int64_t max_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_H_ */

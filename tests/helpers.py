@@ -1,0 +1,97 @@
+"""Shared test helpers: run the same frame through the HIP path and the oracle."""
+from __future__ import annotations
+
+import numpy as np
+
+from gsviewer_amd.camera import Camera
+from oracle import gl_oracle as O
+
+# Stated float tolerances (north star: "pixel-for-pixel within a stated float
+# tolerance").  Exact mode (t_min = 0): per-splat records are bit-identical,
+# so image differences come only from blend order (front-to-back with T vs
+# back-to-front over) and exp() ulps.
+TOL_EXACT = 2e-5           # |GPU - oracle(float)| per channel, exact mode
+TOL_EXACT_FRAC = 0.999     # fraction of pixel-channels within TOL_EXACT
+TOL_MAX = 2e-2             # any pixel-channel (alpha = 1/255 threshold flips)
+TOL_TMIN = 1e-4            # extra error allowed by early termination at t_min = 1e-4
+
+
+def uniforms_for(cam: Camera, settings=None, **over):
+    """Oracle uniform dict from a Camera + RenderSettings (same inputs the GPU gets)."""
+    V = cam.get_view_matrix()
+    P = cam.get_project_matrix()
+    kw = {}
+    if settings is not None:
+        kw = dict(gaussian_scale_factor=np.float32(settings.scale_modifier),
+                  screen_display_scale_factor=np.float32(settings.screen_scale),
+                  dc_factor=np.float32(settings.dc_factor), extra_factor=np.float32(settings.extra_factor),
+                  color_scale_factors=np.asarray(settings.color_scale, np.float32),
+                  render_mod=int(settings.render_mod),
+                  rot_modifier=np.asarray(settings.rot_modifier, np.float32),
+                  light_rotation=np.asarray(settings.light_rotation, np.float32),
+                  points_center=np.asarray(settings.points_center, np.float32),
+                  enable_aabb=int(settings.enable_aabb), enable_obb=int(settings.enable_obb),
+                  cube_rotation=np.asarray(settings.cube_rotation, np.float32),
+                  cubeMin=np.asarray(settings.cube_min, np.float32),
+                  cubeMax=np.asarray(settings.cube_max, np.float32),
+                  bg=np.asarray(settings.bg, np.float32))
+    kw.update(over)
+    return O.default_uniforms(V, P, np.asarray(cam.get_htanfovxy_focal(), np.float32), cam.position, cam.w, cam.h,
+                              **kw)
+
+
+def gpu_frame(g, cam, settings, with_debug=False, radii=False):
+    """Render on the GPU through the C ABI; returns numpy image [H,W,3] (+extras)."""
+    import ctypes
+
+    import torch
+
+    from gsviewer_amd import _lib
+    from gsviewer_amd.rasterizer import HipContext, HipScene, camera_from, render_into
+
+    scene = HipScene.from_gaussian_data(g.astype32())
+    ctx = HipContext()
+    out = torch.empty((cam.h, cam.w, 3), dtype=torch.float32, device="cuda")
+    rad = torch.empty((len(g),), dtype=torch.int32, device="cuda") if radii else None
+    settings.out_layout = 1
+    render_into(ctx, scene, camera_from(cam), settings, out, rad)
+    torch.cuda.synchronize()
+    res = {"image": out.cpu().numpy(), "stats": ctx.stats()}
+    if radii:
+        res["radii"] = rad.cpu().numpy()
+    if with_debug:
+        lib = _lib.load()
+        st = res["stats"]
+        nv, nd, nt = st["n_visible"], st["n_instances"], st["tiles_x"] * st["tiles_y"]
+
+        def grab(what, nbytes, dtype):
+            buf = torch.empty(max(nbytes, 4) // 4 + 1, dtype=torch.int32, device="cuda")
+            got = lib.gsr_debug_copy(ctx.handle, what, ctypes.c_void_p(buf.data_ptr()), nbytes, None)
+            assert got >= 0, lib.gsr_last_error()
+            torch.cuda.synchronize()
+            return buf.cpu().numpy().view(np.uint8)[:got].view(dtype)
+
+        res["records"] = grab(_lib.GSR_DEBUG_RECORDS, nv * 64, np.uint8).reshape(nv, 64)
+        res["depth_order"] = grab(_lib.GSR_DEBUG_DEPTH_ORDER, nv * 4, np.uint32)
+        res["ranges"] = grab(_lib.GSR_DEBUG_TILE_RANGES, nt * 8, np.uint32).reshape(nt, 2)
+        res["tile_list"] = grab(_lib.GSR_DEBUG_TILE_LIST, nd * 4, np.uint32)
+    scene.close()
+    ctx.close()
+    return res
+
+
+def decode_records(raw):
+    f = raw.view(np.float32).reshape(-1, 16)
+    i = raw.view(np.int32).reshape(-1, 16)
+    return dict(center=f[:, 0:2], coord_scale=f[:, 2:4], conic=f[:, 4:7], opacity=f[:, 7], color=f[:, 8:11],
+                x0=i[:, 11], x1=i[:, 12], r0=i[:, 13], r1=i[:, 14])
+
+
+def compare_images(gpu, ref, tol=TOL_EXACT, frac=TOL_EXACT_FRAC, tol_max=TOL_MAX):
+    d = np.abs(gpu.astype(np.float64) - ref.astype(np.float64))
+    ok_frac = float((d <= tol).mean())
+    info = dict(max=float(d.max()), ok_frac=ok_frac, mean=float(d.mean()))
+    assert np.isfinite(gpu).all(), "non-finite pixels"
+    assert ok_frac >= frac, info
+    assert d.max() <= tol_max, info
+    return info

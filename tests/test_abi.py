@@ -1,0 +1,74 @@
+"""The C-ABI library loads, exports every symbol include/gsr.h declares, and the
+ctypes struct layouts match the C header (no GPU calls)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from gsviewer_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gsr.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gsr_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_entry_points():
+    names = header_functions()
+    for must in ("gsr_scene_create", "gsr_scene_create_flat", "gsr_scene_destroy", "gsr_context_create",
+                 "gsr_render", "gsr_sort_depth", "gsr_last_error", "gsr_settings_default"):
+        assert must in names
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    missing = [n for n in header_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(header_functions()) == set(_lib.SIGNATURES), "ctypes signatures out of sync with gsr.h"
+
+
+def test_abi_version_and_defaults():
+    lib = _lib.load()
+    assert lib.gsr_abi_version() == _lib.ABI_VERSION
+    s = _lib.default_settings()
+    assert s.render_mod == 6 and s.scale_modifier == 1.0 and list(s.rot_modifier) == [0, 0, 0, 1]
+    assert list(s.cube_rotation) == [1, 0, 0, 0, 1, 0, 0, 0, 1]
+
+
+def test_invalid_arguments_fail_loudly():
+    lib = _lib.load()
+    out = ctypes.c_void_p()
+    rc = lib.gsr_scene_create(None, None, None, None, None, 10, 48, None, ctypes.byref(out))
+    assert rc != 0 and b"null" in lib.gsr_last_error()
+    rc = lib.gsr_scene_create_flat(None, 10, 7, None, ctypes.byref(out))
+    assert rc != 0 and b"sh_dim" in lib.gsr_last_error()
+    with pytest.raises(RuntimeError):
+        _lib.check(rc, "gsr_scene_create_flat")
+
+
+def test_struct_layout_matches_header(tmp_path):
+    prog = tmp_path / "sz.c"
+    prog.write_text(r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "gsr.h"
+int main(void){
+ printf("%zu %zu %zu\n", sizeof(gsr_camera), sizeof(gsr_settings), sizeof(gsr_frame_stats));
+ printf("%zu %zu %zu %zu\n", offsetof(gsr_settings, cube_rotation), offsetof(gsr_settings, bg),
+        offsetof(gsr_settings, t_min), offsetof(gsr_settings, out_layout));
+ printf("%zu %zu\n", offsetof(gsr_camera, hfovxy_focal), offsetof(gsr_camera, height));
+ return 0;}
+''')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
+    got = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    S, C, FS = _lib.GsrSettings, _lib.GsrCamera, _lib.GsrFrameStats
+    want = [ctypes.sizeof(C), ctypes.sizeof(S), ctypes.sizeof(FS), S.cube_rotation.offset, S.bg.offset,
+            S.t_min.offset, S.out_layout.offset, C.hfovxy_focal.offset, C.height.offset]
+    assert [int(x) for x in got] == want

@@ -1,0 +1,154 @@
+"""GPU parity: the HIP rasterizer (through the C ABI) against the CPU oracle of
+the reference's OpenGL path, on the same seeded inputs."""
+import numpy as np
+import pytest
+
+from gsviewer_amd.camera import Camera, euler_to_rotation_matrix
+from gsviewer_amd.gaussian_data import garden_standin, naive_gaussian, random_scene
+from oracle import gl_oracle as O
+from helpers import TOL_TMIN, compare_images, decode_records, gpu_frame, uniforms_for
+
+pytestmark = pytest.mark.gpu
+
+
+def _settings(**kw):
+    from gsviewer_amd.rasterizer import RenderSettings
+    return RenderSettings(**kw)
+
+
+def _check(g, cam, st, mode="float", **cmp):
+    res = gpu_frame(g, cam, st, with_debug=True, radii=True)
+    U = uniforms_for(cam, st)
+    vs = O.vertex_stage(g.flat().astype(np.float32), g.sh_dim, U)
+    ref = O.composite(vs, U, mode=mode)
+    info = compare_images(res["image"], ref, **cmp)
+    return res, vs, U, ref, info
+
+
+def test_naive_scene_default_camera(gpu):
+    g = naive_gaussian()
+    for (w, h) in [(1280, 720), (640, 480)]:
+        res, vs, U, ref, info = _check(g, Camera(h, w), _settings(t_min=0.0))
+        assert res["stats"]["n_visible"] == 4
+        # the four splats are clearly drawn: centre pixel of Gaussian 0 is magenta-ish
+        assert res["image"][h // 2, w // 2].max() > 0.5
+
+
+@pytest.mark.parametrize("deg", [0, 1, 2, 3])
+def test_random_scene_exact_mode(gpu, deg):
+    g = random_scene(2500, sh_degree=deg, seed=10 + deg)
+    res, vs, U, ref, info = _check(g, Camera(120, 160), _settings(t_min=0.0))
+    assert res["stats"]["n_visible"] == int(vs["visible"].sum())
+
+
+def test_preprocess_records_bit_exact(gpu):
+    g = random_scene(3000, sh_degree=3, seed=3)
+    cam = Camera(96, 128).yaw(20)
+    res = gpu_frame(g, cam, _settings(t_min=0.0), with_debug=True)
+    U = uniforms_for(cam)
+    vs = O.vertex_stage(g.flat(), 48, U)
+    vis_desc = np.nonzero(vs["visible"])[0][::-1]          # slot s -> Gaussian id
+    rec = decode_records(res["records"])
+    assert len(vis_desc) == len(rec["opacity"])
+    np.testing.assert_array_equal(rec["center"], vs["center"][vis_desc])
+    np.testing.assert_array_equal(rec["coord_scale"], vs["coord_scale"][vis_desc])
+    np.testing.assert_array_equal(rec["conic"], vs["conic"][vis_desc])
+    np.testing.assert_array_equal(rec["opacity"], vs["opacity"][vis_desc])
+    np.testing.assert_array_equal(rec["color"], np.clip(vs["color"][vis_desc], 0, 1))
+    x0, x1, r0, r1 = O.splat_rects(vs, U)
+    for a, b in [(rec["x0"], x0), (rec["x1"], x1), (rec["r0"], r0), (rec["r1"], r1)]:
+        np.testing.assert_array_equal(a, b[vis_desc])
+
+
+def test_depth_order_and_tile_lists_exact(gpu):
+    g = random_scene(4000, sh_degree=0, seed=5)
+    cam = Camera(80, 112).yaw(-35)
+    res = gpu_frame(g, cam, _settings(t_min=0.0), with_debug=True)
+    U = uniforms_for(cam)
+    vs = O.vertex_stage(g.flat(), 3, U)
+    vis_desc = np.nonzero(vs["visible"])[0][::-1]
+    # global front-to-back order == reverse of the GL draw order
+    f2b = O.sort_back_to_front(vs["view_z"], vs["visible"])[::-1]
+    np.testing.assert_array_equal(vis_desc[res["depth_order"]], f2b)
+    # per-tile instance lists == GL order restricted to the tile, reversed
+    lists = O.tile_lists(vs, U)
+    ranges, tl = res["ranges"], res["tile_list"]
+    for t, want in enumerate(lists):
+        b, e = ranges[t]
+        got = vis_desc[tl[b:e]] if e > b else np.zeros(0, np.int64)
+        np.testing.assert_array_equal(got, np.asarray(want, np.int64), err_msg=f"tile {t}")
+    assert res["stats"]["n_instances"] == sum(len(x) for x in lists)
+
+
+def test_radii(gpu):
+    g = random_scene(2000, sh_degree=0, seed=8)
+    cam = Camera(120, 160)
+    res = gpu_frame(g, cam, _settings(), radii=True)
+    vs = O.vertex_stage(g.flat(), 3, uniforms_for(cam))
+    np.testing.assert_array_equal(res["radii"], O.radii(vs))
+
+
+def test_default_t_min_error_bound(gpu):
+    g = random_scene(3000, sh_degree=3, seed=11, scale_range=(0.02, 0.1))
+    cam = Camera(96, 128)
+    res, vs, U, ref, info = _check(g, cam, _settings(t_min=1e-4), tol=TOL_TMIN + 2e-5, frac=0.999)
+
+
+@pytest.mark.parametrize("mode", [-6, -5, -4, -3, -2, -1, 0, 1, 2, 3, 6])
+def test_render_modes(gpu, mode):
+    g = random_scene(1500, sh_degree=3, seed=20, scale_range=(0.01, 0.06))
+    _check(g, Camera(96, 128), _settings(render_mod=mode, t_min=0.0))
+
+
+def test_appearance_uniforms(gpu):
+    g = random_scene(1500, sh_degree=3, seed=21)
+    st = _settings(t_min=0.0, dc_factor=0.7, extra_factor=1.6, color_scale=[0.9, 1.1, 0.5],
+                   scale_modifier=1.7, screen_scale=1.3, light_rotation=[10.0, -25.0, 40.0], bg=[0.1, 0.2, 0.3])
+    st.set_rot_modifier_euler([15.0, -30.0, 5.0])
+    # light rotation cos/sin are computed by libm on the host vs numpy in the
+    # oracle: allow their last-ulp difference
+    _check(g, Camera(96, 128).yaw(30), st, tol=1e-4)
+
+
+def test_aabb_and_obb_cull(gpu):
+    g = random_scene(3000, sh_degree=1, seed=30)
+    cam = Camera(120, 160)
+    c = g.points_center
+    st = _settings(t_min=0.0, enable_aabb=1, points_center=c, cube_min=[-1.0, -0.5, -2.0], cube_max=[0.5, 1.0, 1.0])
+    res, vs, *_ = _check(g, cam, st)
+    assert 0 < vs["visible"].sum() < len(g)
+    st = _settings(t_min=0.0, enable_obb=1, points_center=c, cube_min=[-1.5] * 3, cube_max=[1.5] * 3,
+                   cube_rotation=euler_to_rotation_matrix([30, 15, 0]))
+    _check(g, cam, st)
+
+
+def test_gl8_framebuffer_closeness(gpu):
+    """Against the 8-bit-per-blend GL emulation."""
+    g = random_scene(2500, sh_degree=3, seed=12)
+    cam = Camera(120, 160)
+    res = gpu_frame(g, cam, _settings())
+    U = uniforms_for(cam)
+    ref8 = O.composite(O.vertex_stage(g.flat(), 48, U), U, mode="gl8")
+    d = np.abs(res["image"] - ref8)
+    assert (d <= 2.0 / 255).mean() >= 0.999, d.max()
+    mse = float((d ** 2).mean())
+    assert 10 * np.log10(1.0 / max(mse, 1e-20)) >= 45.0
+
+
+def test_empty_and_culled_scenes(gpu):
+    g = random_scene(100, sh_degree=0, seed=1)
+    g.xyz[:] = np.array([0, 0, 100.0], np.float32)  # behind the camera at z=5 looking -z
+    res = gpu_frame(g, Camera(48, 64), _settings(bg=[0.25, 0.5, 0.75]))
+    assert res["stats"]["n_visible"] == 0
+    assert np.all(res["image"] == np.array([0.25, 0.5, 0.75], np.float32))
+
+
+def test_ragged_image_sizes(gpu):
+    g = random_scene(1200, sh_degree=0, seed=2, scale_range=(0.02, 0.08))
+    for (w, h) in [(17, 9), (33, 47), (100, 1)]:
+        _check(g, Camera(h, w), _settings(t_min=0.0))
+
+
+def test_garden_standin_small(gpu):
+    g = garden_standin(6000, seed=1)
+    _check(g, Camera(90, 160), _settings(t_min=0.0))
