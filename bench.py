@@ -165,9 +165,19 @@ def main():
         elapsed = float(e.item())
 
     stats = ctx.stats()
+    # tile-list length distribution of the last frame (load balance of the compositor)
+    import ctypes
+    nt = stats["tiles_x"] * stats["tiles_y"]
+    rb = torch.empty(2 * nt, dtype=torch.int32, device=dev)
+    lib.gsr_debug_copy(ctx.handle, _lib.GSR_DEBUG_TILE_RANGES, ctypes.c_void_p(rb.data_ptr()), 8 * nt, None)
+    torch.cuda.synchronize()
+    rr = rb.cpu().numpy().reshape(nt, 2).astype(np.int64)
+    lens = rr[:, 1] - rr[:, 0]
+    stats["tile_len_max"] = int(lens.max())
+    stats["tile_len_p99"] = int(np.percentile(lens, 99))
+    stats["tile_len_mean"] = float(lens.mean())
     stage = {}
     if not args.no_profile:
-        import ctypes
         ms = (ctypes.c_double * 8)()
         frames = ctypes.c_int64()
         _lib.check(lib.gsr_context_stage_times(ctx.handle, ms, ctypes.byref(frames)), "stage_times")

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -68,6 +69,10 @@ struct gsr_context {
     gsr::DevBuf<uint32_t> tkeys_a, tkeys_b, tvals_a, tvals_b;  // tile sort (capacity D)
     gsr::DevBuf<uint32_t> radix_tmp;
     gsr::DevBuf<uint2> ranges;
+    gsr::DevBuf<uint32_t> chunk_cnt, chunk_off;   // per tile
+    gsr::DevBuf<uint4> chunk_desc;                // per chunk
+    gsr::DevBuf<float4> partial;                  // per chunk x 256 px (multi-chunk tiles)
+    uint32_t chunk = 256;                         // instances per compositing chunk
     gsr::DevBuf<uint32_t> counters;  // [0] = V, [1] = D
     uint32_t* host_counters = nullptr;  // pinned
     gsr_frame_stats stats{};
@@ -162,7 +167,7 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
     if ((rc = c->vals_b.ensure(n, "vals"))) return rc;
     if ((rc = c->dup_off.ensure(n, "dup_off"))) return rc;
     if ((rc = c->radix_tmp.ensure(radix_tmp_elems(n), "radix_tmp"))) return rc;
-    if ((rc = c->counters.ensure(4, "counters"))) return rc;
+    if ((rc = c->counters.ensure(4, "counters"))) return rc;  // [0] V, [1] D, [2] chunks
     if (!c->host_counters) {
         if (hipHostMalloc(&c->host_counters, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
             c->host_counters = nullptr;
@@ -305,6 +310,10 @@ int32_t gsr_scene_sh_dim(const gsr_scene* scene) { return scene ? scene->d.sh_di
 int gsr_context_create(gsr_context** out) {
     if (!out) return set_error(GSR_ERR_INVALID, "out is null");
     *out = new gsr_context();
+    if (const char* e = std::getenv("GSR_CHUNK")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 16 && v <= (1 << 20)) (*out)->chunk = (uint32_t)v;
+    }
     return GSR_OK;
 }
 
@@ -315,6 +324,7 @@ int gsr_context_destroy(gsr_context* c) {
     c->keys_a.release(); c->keys_b.release(); c->vals_a.release(); c->vals_b.release();
     c->dup_off.release(); c->tkeys_a.release(); c->tkeys_b.release(); c->tvals_a.release();
     c->tvals_b.release(); c->radix_tmp.release(); c->ranges.release(); c->counters.release();
+    c->chunk_cnt.release(); c->chunk_off.release(); c->chunk_desc.release(); c->partial.release();
     if (c->host_counters) (void)hipHostFree(c->host_counters);
     for (auto& row : c->ev)
         for (auto& e : row)
@@ -414,9 +424,21 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
     }
     if ((rc = prof_record(c, slot, EV_TSORT, s))) return rc;
     if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, c->ranges.p, s))) return rc;
+    // compositing chunks: at most one per tile plus one per `chunk` instances
+    const size_t max_chunks = (size_t)num_tiles + n_dup / c->chunk + 1;
+    if ((rc = c->chunk_cnt.ensure((size_t)num_tiles, "chunk_cnt"))) return rc;
+    if ((rc = c->chunk_off.ensure((size_t)num_tiles, "chunk_off"))) return rc;
+    if ((rc = c->chunk_desc.ensure(max_chunks, "chunk_desc"))) return rc;
+    if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
+    if ((rc = c->scan_tmp.ensure(std::max(scan_tmp_elems((size_t)num_tiles), scan_tmp_elems(n)), "scan_tmp")))
+        return rc;
+    if ((rc = launch_chunks(c->ranges.p, num_tiles, c->chunk, c->chunk_cnt.p, c->chunk_off.p, c->scan_tmp.p,
+                            c->counters.p + 2, c->chunk_desc.p, s)))
+        return rc;
     if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
-    if ((rc = launch_composite(c->ranges.p, tile_list, c->recs.p, u, frag_class_of(u.render_mod), st->t_min, st->bg,
-                               st->out_layout, out, s)))
+    if ((rc = launch_composite(c->chunk_desc.p, c->counters.p + 2, (uint32_t)max_chunks, c->chunk_off.p,
+                               c->chunk_cnt.p, tile_list, c->recs.p, u, frag_class_of(u.render_mod), st->t_min,
+                               st->bg, st->out_layout, out, c->partial.p, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_COUNT, s))) return rc;
     if (c->prof_on) c->ev_pending[slot] = true;

@@ -152,3 +152,13 @@ def test_ragged_image_sizes(gpu):
 def test_garden_standin_small(gpu):
     g = garden_standin(6000, seed=1)
     _check(g, Camera(90, 160), _settings(t_min=0.0))
+
+
+@pytest.mark.parametrize("chunk", ["16", "64"])
+def test_multi_chunk_merge(gpu, monkeypatch, chunk):
+    """Small compositing chunks force every busy tile through the partial
+    (C, T) + in-order merge path."""
+    monkeypatch.setenv("GSR_CHUNK", chunk)
+    g = random_scene(5000, sh_degree=3, seed=70, scale_range=(0.02, 0.09))
+    _check(g, Camera(96, 128), _settings(t_min=0.0))
+    _check(g, Camera(96, 128), _settings(t_min=1e-4), tol=TOL_TMIN + 2e-5)
