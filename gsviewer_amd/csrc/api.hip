@@ -1,13 +1,15 @@
 // C ABI (include/gsr.h): scene lifetime, frame workspace, render orchestration.
 //
 // Frame pipeline on one stream (N = Gaussians, V = visible, D = instances):
-//   k_cull(N) -> scan(N/64 wave counts) -> k_preprocess(N)
-//   -> radix sort (depth key, record id) over V, 4 x 8-bit passes
-//   -> k_dup_count(V) -> scan(V) -> [one 8-byte D2H read of V, D]
-//   -> k_dup_write(V) -> stable radix sort by tile id over D (ceil(tile_bits/8) passes)
-//   -> k_tile_ranges(D) -> k_composite(tiles)
-// All kernels after the cull read V from device memory, so the only host
-// synchronisation is the read of D needed to size the tile sort.
+//   memset(per-frame zero block: counters, radix totals, tile ranges, saturation words)
+//   k_cull(N) -> scan(N/64 wave counts; total = V on device)
+//   k_preprocess(N): records, depth keys, tile rects; D accumulated on device
+//   async copy (V, D) -> pinned host, event
+//   depth radix sort (grid sized by N, count V read on device), 4 x 8-bit passes
+//   [host waits for the (V, D) event while the GPU runs the depth sort]
+//   binning (reduce, scan, fused scan+write) -> stable tile radix sort over D
+//   k_tile_ranges -> chunk count / scan / write -> k_composite(chunks) -> k_merge
+// The only host wait overlaps GPU work, so no stage of the frame idles.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -65,21 +67,23 @@ struct gsr_context {
     gsr::DevBuf<uint32_t> scan_tmp;
     gsr::DevBuf<gsr::SplatRec> recs;
     gsr::DevBuf<uint32_t> keys_a, keys_b, vals_a, vals_b;   // depth sort (capacity N)
-    gsr::DevBuf<uint32_t> dup_off;                          // per sorted splat: tile count -> offset
+    gsr::DevBuf<uint2> trect;                               // per record: packed tile rectangle
+    gsr::DevBuf<uint32_t> bin_tmp;                          // binning block offsets
     gsr::DevBuf<uint32_t> tkeys_a, tkeys_b, tvals_a, tvals_b;  // tile sort (capacity D)
     gsr::DevBuf<uint32_t> radix_tmp;
-    gsr::DevBuf<uint2> ranges;
-    gsr::DevBuf<uint32_t> chunk_cnt, chunk_off;   // per tile
+    gsr::DevBuf<uint32_t> zero;                   // per-frame zeroed block (see zero_layout)
+    gsr::DevBuf<uint32_t> chunk_cnt, chunk_base;  // per tile
     gsr::DevBuf<uint4> chunk_desc;                // per chunk
     gsr::DevBuf<float4> partial;                  // per chunk x 256 px (multi-chunk tiles)
     uint32_t chunk = 256;                         // instances per compositing chunk
-    gsr::DevBuf<uint32_t> counters;  // [0] = V, [1] = D
     uint32_t* host_counters = nullptr;  // pinned
+    hipEvent_t counts_ready = nullptr;
     gsr_frame_stats stats{};
     // last frame's result arrays (for gsr_debug_copy)
     const uint32_t* last_depth_order = nullptr;
     const uint32_t* last_tile_list = nullptr;
     int64_t last_tiles = 0;
+    const uint2* last_ranges = nullptr;
     // profiling: 10 events per frame, two frames in flight
     bool prof_on = false;
     hipEvent_t ev[2][11] = {};
@@ -153,6 +157,17 @@ int bits_for(uint32_t v) {  // bits needed to represent values < v
     return b;
 }
 
+// Per-frame zero block (one memset): [0,4) counters {V, D, extra chunks, -},
+// [4, 4+2048) radix digit totals (depth passes, tile passes), then tile
+// ranges (uint2, 16-B aligned) and saturation words (4 per tile).
+struct ZeroLayout {
+    size_t counters = 0, totals_depth = 4, totals_tile = 4 + 1024, ranges = 2064, sat = 0, total = 0;
+    explicit ZeroLayout(int num_tiles) {
+        sat = ranges + 2 * (size_t)num_tiles;
+        total = sat + 4 * (size_t)num_tiles;
+    }
+};
+
 int ensure_scene_buffers(gsr_context* c, size_t n) {
     const size_t nw = (n + 63) / 64 + 4;
     int rc;
@@ -165,9 +180,10 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
     if ((rc = c->keys_b.ensure(n, "keys"))) return rc;
     if ((rc = c->vals_a.ensure(n, "vals"))) return rc;
     if ((rc = c->vals_b.ensure(n, "vals"))) return rc;
-    if ((rc = c->dup_off.ensure(n, "dup_off"))) return rc;
+    if ((rc = c->trect.ensure(n, "trect"))) return rc;
+    if ((rc = c->bin_tmp.ensure(bin_tmp_elems(n), "bin_tmp"))) return rc;
     if ((rc = c->radix_tmp.ensure(radix_tmp_elems(n), "radix_tmp"))) return rc;
-    if ((rc = c->counters.ensure(4, "counters"))) return rc;  // [0] V, [1] D, [2] chunks
+    if (!c->counts_ready) GSR_HIP_CHECK(hipEventCreateWithFlags(&c->counts_ready, hipEventDisableTiming));
     if (!c->host_counters) {
         if (hipHostMalloc(&c->host_counters, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
             c->host_counters = nullptr;
@@ -322,9 +338,10 @@ int gsr_context_destroy(gsr_context* c) {
     (void)hipDeviceSynchronize();
     c->vis_mask.release(); c->wave_counts.release(); c->scan_tmp.release(); c->recs.release();
     c->keys_a.release(); c->keys_b.release(); c->vals_a.release(); c->vals_b.release();
-    c->dup_off.release(); c->tkeys_a.release(); c->tkeys_b.release(); c->tvals_a.release();
-    c->tvals_b.release(); c->radix_tmp.release(); c->ranges.release(); c->counters.release();
-    c->chunk_cnt.release(); c->chunk_off.release(); c->chunk_desc.release(); c->partial.release();
+    c->trect.release(); c->bin_tmp.release(); c->tkeys_a.release(); c->tkeys_b.release(); c->tvals_a.release();
+    c->tvals_b.release(); c->radix_tmp.release(); c->zero.release();
+    c->chunk_cnt.release(); c->chunk_base.release();
+    if (c->counts_ready) (void)hipEventDestroy(c->counts_ready); c->chunk_desc.release(); c->partial.release();
     if (c->host_counters) (void)hipHostFree(c->host_counters);
     for (auto& row : c->ev)
         for (auto& e : row)
@@ -349,9 +366,11 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
     const size_t n = (size_t)sc->d.n;
     const int num_tiles = u.tiles_x * u.tiles_y;
     if ((rc = ensure_scene_buffers(c, n))) return rc;
-    if ((rc = c->ranges.ensure((size_t)num_tiles, "ranges"))) return rc;
-    uint32_t* n_vis_dev = c->counters.p;
-    uint32_t* n_dup_dev = c->counters.p + 1;
+    const ZeroLayout zl(num_tiles);
+    if ((rc = c->zero.ensure(zl.total, "zero block"))) return rc;
+    uint32_t* counters = c->zero.p + zl.counters;
+    uint2* ranges = reinterpret_cast<uint2*>(c->zero.p + zl.ranges);
+    uint32_t* sat = c->zero.p + zl.sat;
     const int slot = (int)(c->frame_idx & 1);
     if (c->prof_on) prof_accumulate(c, slot, true);  // slot reuse: frame k-2 is long done
 
@@ -361,46 +380,37 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
     c->stats.tiles_y = u.tiles_y;
     c->last_depth_order = c->last_tile_list = nullptr;
     c->last_tiles = num_tiles;
+    c->last_ranges = ranges;
 
     if ((rc = prof_record(c, slot, EV_START, s))) return rc;
-    GSR_HIP_CHECK(hipMemsetAsync(c->ranges.p, 0, sizeof(uint2) * (size_t)num_tiles, s));
-    uint32_t n_vis = 0, n_dup = 0;
+    GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * zl.total, s));
     if (n > 0) {
         const size_t nw = (n + 63) / 64;
         if ((rc = launch_cull(sc->d, u, c->vis_mask.p, c->wave_counts.p, s))) return rc;
-        if ((rc = scan_exclusive(c->wave_counts.p, c->wave_counts.p, nw, c->scan_tmp.p, n_vis_dev, s))) return rc;
-    } else {
-        GSR_HIP_CHECK(hipMemsetAsync(n_vis_dev, 0, sizeof(uint32_t), s));
+        if ((rc = scan_exclusive(c->wave_counts.p, c->wave_counts.p, nw, c->scan_tmp.p, counters + 0, s))) return rc;
     }
     if ((rc = prof_record(c, slot, EV_CULL, s))) return rc;
-    if (n > 0 && (rc = launch_preprocess(sc->d, u, c->vis_mask.p, c->wave_counts.p, n_vis_dev, c->recs.p,
-                                         c->keys_a.p, radii, s)))
+    if (n > 0 && (rc = launch_preprocess(sc->d, u, c->vis_mask.p, c->wave_counts.p, counters + 0, c->recs.p,
+                                         c->keys_a.p, c->trect.p, counters + 1, radii, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_PRE, s))) return rc;
-    // V sizes the depth-sort grid: one 4-byte read-back.
-    GSR_HIP_CHECK(hipMemcpyAsync(c->host_counters, n_vis_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    GSR_HIP_CHECK(hipStreamSynchronize(s));
-    n_vis = c->host_counters[0];
-    if (c->prof_on) prof_accumulate(c, slot ^ 1, false);  // previous frame finished before this sync
+    GSR_HIP_CHECK(hipMemcpyAsync(c->host_counters, counters, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    GSR_HIP_CHECK(hipEventRecord(c->counts_ready, s));
     if ((rc = prof_record(c, slot, EV_AFTER_SYNC1, s))) return rc;
 
+    // depth sort over the upper bound N; the device count V bounds the work
     uint32_t *ka = c->keys_a.p, *kb = c->keys_b.p, *va = c->vals_a.p, *vb = c->vals_b.p;
-    if (n_vis > 0) {
-        if ((rc = radix_sort_pairs(&ka, &va, &kb, &vb, true, n_vis, 0, 32, c->radix_tmp.p, s))) return rc;
-        c->last_depth_order = va;
-    }
+    if (n > 0 && (rc = radix_sort_pairs(&ka, &va, &kb, &vb, true, n, counters + 0, 0, 32, c->radix_tmp.p,
+                                        c->zero.p + zl.totals_depth, s)))
+        return rc;
     if ((rc = prof_record(c, slot, EV_DSORT, s))) return rc;
-    if (n_vis > 0) {
-        if ((rc = launch_dup_count(va, c->recs.p, n_vis, c->dup_off.p, s))) return rc;
-        if ((rc = scan_exclusive(c->dup_off.p, c->dup_off.p, n_vis, c->scan_tmp.p, n_dup_dev, s))) return rc;
-        if ((rc = prof_record(c, slot, EV_COUNTS, s))) return rc;
-        GSR_HIP_CHECK(hipMemcpyAsync(c->host_counters + 1, n_dup_dev, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        GSR_HIP_CHECK(hipStreamSynchronize(s));
-        n_dup = c->host_counters[1];
-    } else {
-        if ((rc = prof_record(c, slot, EV_COUNTS, s))) return rc;
-    }
-    if ((rc = prof_record(c, slot, EV_AFTER_SYNC2, s))) return rc;
+
+    // host: V and D (the GPU is busy with the depth sort meanwhile)
+    GSR_HIP_CHECK(hipEventSynchronize(c->counts_ready));
+    const uint32_t n_vis = n > 0 ? c->host_counters[0] : 0u;
+    const uint32_t n_dup = n > 0 ? c->host_counters[1] : 0u;
+    if (c->prof_on) prof_accumulate(c, slot ^ 1, false);
+    if (n_vis > 0) c->last_depth_order = va;
 
     uint32_t* tile_list = c->tvals_a.p;
     if (n_dup > 0) {
@@ -410,35 +420,37 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
         if ((rc = c->tvals_b.ensure(n_dup, "tile_vals"))) return rc;
         if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(n_dup), radix_tmp_elems(n)), "radix_tmp")))
             return rc;
-        if ((rc = launch_dup_write(va, c->recs.p, n_vis, c->dup_off.p, u.tiles_x, c->tkeys_a.p, c->tvals_a.p, s)))
+        if ((rc = launch_binning(va, c->trect.p, n_vis, u.tiles_x, c->bin_tmp.p, c->tkeys_a.p, c->tvals_a.p, s)))
             return rc;
     }
+    if ((rc = prof_record(c, slot, EV_COUNTS, s))) return rc;
+    if ((rc = prof_record(c, slot, EV_AFTER_SYNC2, s))) return rc;
     if ((rc = prof_record(c, slot, EV_DUPW, s))) return rc;
     uint32_t *tka = c->tkeys_a.p, *tkb = c->tkeys_b.p, *tva = c->tvals_a.p, *tvb = c->tvals_b.p;
     if (n_dup > 0) {
         const int tbits = bits_for((uint32_t)num_tiles);
-        if (tbits > 0 && (rc = radix_sort_pairs(&tka, &tva, &tkb, &tvb, false, n_dup, 0, tbits, c->radix_tmp.p, s)))
+        if (tbits > 0 && (rc = radix_sort_pairs(&tka, &tva, &tkb, &tvb, false, n_dup, nullptr, 0, tbits,
+                                                c->radix_tmp.p, c->zero.p + zl.totals_tile, s)))
             return rc;
         tile_list = tva;
         c->last_tile_list = tva;
     }
     if ((rc = prof_record(c, slot, EV_TSORT, s))) return rc;
-    if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, c->ranges.p, s))) return rc;
+    if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, ranges, s))) return rc;
+
     // compositing chunks: at most one per tile plus one per `chunk` instances
     const size_t max_chunks = (size_t)num_tiles + n_dup / c->chunk + 1;
     if ((rc = c->chunk_cnt.ensure((size_t)num_tiles, "chunk_cnt"))) return rc;
-    if ((rc = c->chunk_off.ensure((size_t)num_tiles, "chunk_off"))) return rc;
+    if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
     if ((rc = c->chunk_desc.ensure(max_chunks, "chunk_desc"))) return rc;
     if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
-    if ((rc = c->scan_tmp.ensure(std::max(scan_tmp_elems((size_t)num_tiles), scan_tmp_elems(n)), "scan_tmp")))
-        return rc;
-    if ((rc = launch_chunks(c->ranges.p, num_tiles, c->chunk, c->chunk_cnt.p, c->chunk_off.p, c->scan_tmp.p,
-                            c->counters.p + 2, c->chunk_desc.p, s)))
+    if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
+                            c->chunk_desc.p, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
-    if ((rc = launch_composite(c->chunk_desc.p, c->counters.p + 2, (uint32_t)max_chunks, c->chunk_off.p,
-                               c->chunk_cnt.p, tile_list, c->recs.p, u, frag_class_of(u.render_mod), st->t_min,
-                               st->bg, st->out_layout, out, c->partial.p, s)))
+    if ((rc = launch_composite(c->chunk_desc.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
+                               sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), st->t_min, st->bg,
+                               st->out_layout, out, c->partial.p, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_COUNT, s))) return rc;
     if (c->prof_on) c->ev_pending[slot] = true;
@@ -476,7 +488,7 @@ int64_t gsr_debug_copy(const gsr_context* c, int32_t what, void* dst, int64_t ma
     switch (what) {
         case GSR_DEBUG_RECORDS: src = c->recs.p; bytes = c->stats.n_visible * (int64_t)sizeof(SplatRec); break;
         case GSR_DEBUG_DEPTH_ORDER: src = c->last_depth_order; bytes = c->stats.n_visible * 4; break;
-        case GSR_DEBUG_TILE_RANGES: src = c->ranges.p; bytes = c->last_tiles * 8; break;
+        case GSR_DEBUG_TILE_RANGES: src = c->last_ranges; bytes = c->last_tiles * 8; break;
         case GSR_DEBUG_TILE_LIST: src = c->last_tile_list; bytes = c->stats.n_instances * 4; break;
         default: return set_error(GSR_ERR_INVALID, "unknown debug array");
     }
@@ -493,9 +505,13 @@ int gsr_sort_depth(gsr_context* c, const gsr_scene* sc, const float view[16], in
     if (n == 0) return GSR_OK;
     int rc = ensure_scene_buffers(c, n);
     if (rc) return rc;
+    if ((rc = c->zero.ensure(ZeroLayout(0).total, "zero block"))) return rc;
+    GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * ZeroLayout(0).total, s));
     if ((rc = launch_depth_keys_all(sc->d, view, c->keys_a.p, s))) return rc;
     uint32_t *ka = c->keys_a.p, *kb = c->keys_b.p, *va = c->vals_a.p, *vb = c->vals_b.p;
-    if ((rc = radix_sort_pairs(&ka, &va, &kb, &vb, true, n, 0, 32, c->radix_tmp.p, s))) return rc;
+    if ((rc = radix_sort_pairs(&ka, &va, &kb, &vb, true, n, nullptr, 0, 32, c->radix_tmp.p,
+                               c->zero.p + ZeroLayout(0).totals_depth, s)))
+        return rc;
     GSR_HIP_CHECK(hipMemcpyAsync(index_dev, va, n * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     return GSR_OK;
 }

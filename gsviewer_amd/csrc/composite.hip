@@ -9,7 +9,7 @@
 //
 // Compositing (the fragment stage gau_frag.glsl:14-53 + GL SRC_ALPHA /
 // ONE_MINUS_SRC_ALPHA blending, evaluated front-to-back with transmittance):
-// one wave64 per chunk of a tile's list (see k_chunk_count), 4 pixels per lane
+// one wave64 per chunk of a tile's list (see k_build_chunks), 4 pixels per lane
 // (four horizontal 16x4 slices), records staged per wave through LDS, no
 // workgroup barriers; a wave retires as soon as all its 256 pixels are
 // saturated (transmittance < t_min).  Slices a splat's row span misses are
@@ -21,38 +21,74 @@ namespace {
 
 constexpr int kThreads = 256;
 
-__global__ __launch_bounds__(kThreads) void k_dup_count(const uint32_t* __restrict__ sorted_ids,
-                                                        const SplatRec* __restrict__ recs, uint32_t n_vis,
-                                                        uint32_t* __restrict__ counts) {
-    const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
-    if (r >= n_vis) return;
-    const int4 q = reinterpret_cast<const int4*>(recs + sorted_ids[r])[2];
-    const int4 t = reinterpret_cast<const int4*>(recs + sorted_ids[r])[3];
-    const int x0 = q.w, x1 = t.x, r0 = t.y, r1 = t.z;
-    uint32_t c = 0;
-    if (x0 <= x1 && r0 <= r1) c = (uint32_t)(((x1 >> 4) - (x0 >> 4) + 1) * ((r1 >> 4) - (r0 >> 4) + 1));
-    counts[r] = c;
+// Binning: tile instances of the depth-sorted splats.  Each 256-thread block
+// owns 1024 consecutive sorted splats (4 per thread); the tile rectangle of a
+// splat comes from the compact 8-B trect written by the preprocess.
+constexpr int kBinItems = 4;
+constexpr int kBinBlock = kThreads * kBinItems;  // 1024
+
+__device__ __forceinline__ uint32_t rect_tiles(uint2 tr) {
+    const uint32_t tx0 = tr.x & 0xffffu, tx1 = tr.x >> 16, ty0 = tr.y & 0xffffu, ty1 = tr.y >> 16;
+    return (tx0 <= tx1) ? (tx1 - tx0 + 1) * (ty1 - ty0 + 1) : 0u;
 }
 
-__global__ __launch_bounds__(kThreads) void k_dup_write(const uint32_t* __restrict__ sorted_ids,
-                                                        const SplatRec* __restrict__ recs, uint32_t n_vis,
-                                                        const uint32_t* __restrict__ offsets, int tiles_x,
+__global__ __launch_bounds__(kThreads) void k_bin_reduce(const uint32_t* __restrict__ sorted_ids,
+                                                         const uint2* __restrict__ trect, uint32_t n_vis,
+                                                         uint32_t* __restrict__ block_sums) {
+    __shared__ uint32_t lds[kThreads / 64];
+    const uint32_t base = blockIdx.x * kBinBlock + threadIdx.x;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kBinItems; ++k) {
+        const uint32_t r = base + k * kThreads;
+        if (r < n_vis) s += rect_tiles(trect[sorted_ids[r]]);
+    }
+    s = wave_reduce_sum(s);
+    if (__lane_id() == 0) lds[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = lds[0] + lds[1] + lds[2] + lds[3];
+}
+
+// Exclusive offsets of the block's splats (block prefix + in-block scan), then
+// one (tile key, record slot) instance per covered tile, row-major.
+__global__ __launch_bounds__(kThreads) void k_bin_write(const uint32_t* __restrict__ sorted_ids,
+                                                        const uint2* __restrict__ trect, uint32_t n_vis,
+                                                        const uint32_t* __restrict__ block_off, int tiles_x,
                                                         uint32_t* __restrict__ tile_keys,
                                                         uint32_t* __restrict__ tile_vals) {
-    const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
-    if (r >= n_vis) return;
-    const uint32_t id = sorted_ids[r];
-    const int4 q = reinterpret_cast<const int4*>(recs + id)[2];
-    const int4 t = reinterpret_cast<const int4*>(recs + id)[3];
-    const int x0 = q.w, x1 = t.x, r0 = t.y, r1 = t.z;
-    if (x0 > x1 || r0 > r1) return;
-    uint32_t o = offsets[r];
-    for (int ty = r0 >> 4; ty <= (r1 >> 4); ++ty)
-        for (int tx = x0 >> 4; tx <= (x1 >> 4); ++tx) {
-            tile_keys[o] = (uint32_t)(ty * tiles_x + tx);
-            tile_vals[o] = id;
-            ++o;
-        }
+    __shared__ uint32_t lds[kThreads / 64];
+    const uint32_t base = blockIdx.x * kBinBlock + threadIdx.x * kBinItems;  // 4 consecutive per thread
+    uint32_t id[kBinItems];
+    uint2 tr[kBinItems];
+#pragma unroll
+    for (int k = 0; k < kBinItems; ++k) {
+        const uint32_t r = base + k;
+        id[k] = r < n_vis ? sorted_ids[r] : 0u;
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kBinItems; ++k) {
+        tr[k] = (base + k < n_vis) ? trect[id[k]] : make_uint2(0xffffu, 0u);
+        s += rect_tiles(tr[k]);
+    }
+    const int w = threadIdx.x >> 6;
+    const uint32_t inc = wave_inclusive_scan(s);
+    if (__lane_id() == 63) lds[w] = inc;
+    __syncthreads();
+    uint32_t o = block_off[blockIdx.x] + inc - s;
+#pragma unroll
+    for (int k = 0; k < kThreads / 64; ++k) o += (k < w) ? lds[k] : 0u;
+#pragma unroll
+    for (int k = 0; k < kBinItems; ++k) {
+        const uint32_t tx0 = tr[k].x & 0xffffu, tx1 = tr[k].x >> 16, ty0 = tr[k].y & 0xffffu, ty1 = tr[k].y >> 16;
+        if (tx0 > tx1) continue;
+        for (uint32_t ty = ty0; ty <= ty1; ++ty)
+            for (uint32_t tx = tx0; tx <= tx1; ++tx) {
+                tile_keys[o] = ty * (uint32_t)tiles_x + tx;
+                tile_vals[o] = id[k];
+                ++o;
+            }
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void k_tile_ranges(const uint32_t* __restrict__ keys, uint32_t n,
@@ -81,29 +117,43 @@ constexpr int kBatch = 64;  // records staged per wave per LDS batch
 // folded in depth order afterwards (k_merge).  This bounds the work of one
 // wave, which is what the heavy tiles of a real scene (horizon lines,
 // dense cores) need.
-__global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restrict__ ranges, int num_tiles,
-                                                          uint32_t chunk, uint32_t* __restrict__ counts) {
-    const int t = blockIdx.x * kThreads + threadIdx.x;
-    if (t >= num_tiles) return;
-    const uint2 r = ranges[t];
+//
+// Chunk slots: slot t (< num_tiles) is chunk 0 of tile t, so every tile's
+// front chunk is dispatched first; chunks k >= 1 of tile t follow at
+// num_tiles + extra_off[t] + k - 1.  Built by ONE workgroup (num_tiles is at
+// most a few tens of thousands).
+__device__ __forceinline__ uint32_t chunks_of(uint2 r, uint32_t chunk) {
     const uint32_t len = r.y - r.x;
-    counts[t] = len == 0 ? 1u : (len + chunk - 1) / chunk;
+    return len == 0 ? 1u : (len + chunk - 1) / chunk;
 }
 
+__global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restrict__ ranges, int num_tiles,
+                                                          uint32_t chunk, uint32_t* __restrict__ extra) {
+    const int t = blockIdx.x * kThreads + threadIdx.x;
+    if (t < num_tiles) extra[t] = chunks_of(ranges[t], chunk) - 1u;
+}
+
+// extra_off = exclusive scan of extra (chunks beyond the first), in place.
 __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restrict__ ranges, int num_tiles,
-                                                          uint32_t chunk, const uint32_t* __restrict__ offsets,
+                                                          uint32_t chunk, uint32_t* __restrict__ chunk_cnt,
+                                                          uint32_t* __restrict__ chunk_base,
                                                           uint4* __restrict__ desc) {
     const int t = blockIdx.x * kThreads + threadIdx.x;
     if (t >= num_tiles) return;
     const uint2 r = ranges[t];
-    const uint32_t len = r.y - r.x;
-    const uint32_t cnt = len == 0 ? 1u : (len + chunk - 1) / chunk;
-    const uint32_t o = offsets[t];
+    const uint32_t cnt = chunks_of(r, chunk);
+    const uint32_t base = (uint32_t)num_tiles + chunk_base[t];  // chunk_base holds extra_off on entry
+    chunk_cnt[t] = cnt;
+    chunk_base[t] = base;
     for (uint32_t k = 0; k < cnt; ++k) {
         const uint32_t b = r.x + k * chunk;
         const uint32_t e = min(r.y, b + chunk);
-        desc[o + k] = make_uint4((uint32_t)t, b, e, (cnt << 16) | k);
+        desc[k == 0 ? (uint32_t)t : base + k - 1] = make_uint4((uint32_t)t, b, e, (cnt << 16) | k);
     }
+}
+
+__device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One wave per chunk, 4 pixels per lane (four 16x4 slices of the 16x16 tile).
@@ -111,20 +161,31 @@ __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restric
 // prefetched one batch ahead in registers) into a wave-private LDS buffer and
 // then read back with wave-uniform (broadcast) ds_read_b128.  No workgroup
 // barriers: the four waves of a block are independent chunks.
+//
+// Saturation words (multi-chunk tiles only): sat[tile*4 + slice] holds
+// ~(smallest chunk index) (atomicMax of the complement, so a zeroed word means
+// "none") of the first chunk whose 64 pixels of that slice all reached a LOCAL
+// transmittance < t_min; the absolute transmittance after that chunk is then
+// < t_min too, so everything behind it contributes less than t_min (the same
+// bound as sequential early termination).  Later chunks stop compositing such
+// slices and k_merge folds each slice only up to that chunk.  The words are
+// read relaxed at agent scope; a stale read only costs work, never accuracy.
 template <int FRAG>
 __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict__ desc,
                                                         const uint32_t* __restrict__ n_chunks_dev,
                                                         const uint32_t* __restrict__ list,
                                                         const SplatRec* __restrict__ recs, CompositeArgs a,
-                                                        float* __restrict__ out, float4* __restrict__ partial) {
+                                                        float* __restrict__ out, float4* __restrict__ partial,
+                                                        uint32_t* __restrict__ sat) {
     __shared__ float4 lds[kThreads / 64][kBatch * 4];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t chunk_id = blockIdx.x * (kThreads / 64) + wave;
-    if (chunk_id >= n_chunks_dev[0]) return;
-    const uint4 d = desc[chunk_id];
+    const uint32_t slot = blockIdx.x * (kThreads / 64) + wave;
+    if (slot >= (uint32_t)a.num_tiles + n_chunks_dev[0]) return;  // device count of extra chunks
+    const uint4 d = desc[slot];
     const int tile = (int)d.x;
     const uint32_t begin = d.y, end = d.z;
     const uint32_t nchunks = d.w >> 16;
+    const uint32_t kk = d.w & 0xffffu;
     const int lane = __lane_id();
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
     const int x = tx * kTile + (lane & 15);
@@ -142,18 +203,27 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
         cr[k] = cg[k] = cb[k] = 0.f;
     }
     const float t_min = a.t_min;
+    const bool track = (nchunks > 1) && (t_min > 0.f);
+    uint32_t* my_sat = sat + (size_t)tile * 4;
+    // live slices (bit k): not yet saturated locally nor by an earlier chunk
+    uint32_t live = 0xfu;
+    if (track && kk > 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (0xffffffffu - ld_relaxed(my_sat + k) < kk) live &= ~(1u << k);
+        live = __builtin_amdgcn_readfirstlane(live);
+    }
     float4* my = lds[wave];
 
-    // prefetch first batch
     float4 f0, f1, f2, f3;
     {
         const uint32_t i = begin + lane;
-        if (i < end) {
+        if (i < end && live) {
             const float4* r = reinterpret_cast<const float4*>(recs + list[i]);
             f0 = r[0]; f1 = r[1]; f2 = r[2]; f3 = r[3];
         }
     }
-    for (uint32_t b = begin; b < end; b += kBatch) {
+    for (uint32_t b = begin; b < end && live; b += kBatch) {
         __builtin_amdgcn_wave_barrier();
         my[lane * 4 + 0] = f0;
         my[lane * 4 + 1] = f1;
@@ -181,7 +251,8 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int srow0 = row_base + 4 * k;
-                if (srow0 > sr1 || srow0 + 3 < sr0) continue;  // scalar: slice misses the splat
+                // scalar: slice saturated, or the splat's rows miss the slice
+                if (!(live & (1u << k)) || srow0 > sr1 || srow0 + 3 < sr0) continue;
                 const int row = srow0 + lrow;
                 const bool in = inx & (row >= sr0) & (row <= sr1) & (T[k] >= t_min);
                 float alpha, fr = q2.x, fg = q2.y, fb = q2.z;
@@ -212,15 +283,33 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
             }
         }
         if (t_min > 0.f) {
-            // a pixel whose chunk-local T is below t_min has absolute T below it too
-            const bool live = (T[0] >= t_min) | (T[1] >= t_min) | (T[2] >= t_min) | (T[3] >= t_min);
-            if (!__any(live)) break;
+            // a slice whose chunk-local T is below t_min everywhere is done
+            uint32_t still = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (__any(T[k] >= t_min)) still |= (1u << k);
+            const uint32_t newly = live & ~still;
+            if (track && newly) {
+                if (lane == 0) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (newly & (1u << k)) atomicMax(my_sat + k, 0xffffffffu - kk);
+                }
+            }
+            live &= still;
+            if (track && kk > 0 && live) {
+                uint32_t dead = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (0xffffffffu - ld_relaxed(my_sat + k) < kk) dead |= (1u << k);
+                live &= ~__builtin_amdgcn_readfirstlane(dead);
+            }
         }
     }
 
     if (nchunks > 1) {
-        // partial (C, T) per pixel, folded by k_merge; layout [chunk][k][lane]
-        float4* p = partial + (size_t)chunk_id * 256;
+        // partial (C, T) per pixel, folded by k_merge; layout [slot][k][lane]
+        float4* p = partial + (size_t)slot * 256;
 #pragma unroll
         for (int k = 0; k < 4; ++k) p[k * 64 + lane] = make_float4(cr[k], cg[k], cb[k], T[k]);
         return;
@@ -247,66 +336,76 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
     }
 }
 
-// Fold the partial results of multi-chunk tiles in depth order; one wave per tile.
-__global__ __launch_bounds__(kThreads) void k_merge(const uint32_t* __restrict__ chunk_off,
-                                                    const uint32_t* __restrict__ chunk_cnt,
-                                                    const float4* __restrict__ partial, CompositeArgs a,
+// Fold the partial results of multi-chunk tiles in depth order: one block per
+// tile, wave k folds slice k up to its saturating chunk (if any).
+__global__ __launch_bounds__(kThreads) void k_merge(const uint32_t* __restrict__ chunk_cnt,
+                                                    const uint32_t* __restrict__ chunk_base,
+                                                    const float4* __restrict__ partial,
+                                                    const uint32_t* __restrict__ sat, CompositeArgs a,
                                                     float* __restrict__ out) {
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int tile = blockIdx.x * (kThreads / 64) + wave;
-    if (tile >= a.num_tiles) return;
+    const int tile = blockIdx.x;
     const uint32_t cnt = chunk_cnt[tile];
     if (cnt <= 1) return;
-    const uint32_t c0 = chunk_off[tile];
+    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = __lane_id();
+    const uint32_t last = min(cnt - 1, 0xffffffffu - sat[tile * 4 + k]);
+    const uint32_t base = chunk_base[tile];
+    float r = 0.f, g = 0.f, b = 0.f, T = 1.f;
+    constexpr int kDepth = 8;
+    for (uint32_t c0 = 0; c0 <= last; c0 += kDepth) {
+        float4 q[kDepth];
+#pragma unroll
+        for (int j = 0; j < kDepth; ++j) {
+            const uint32_t c = c0 + j;
+            if (c <= last) {
+                const uint32_t slot = c == 0 ? (uint32_t)tile : base + c - 1;
+                q[j] = partial[(size_t)slot * 256 + k * 64 + lane];
+            } else {
+                q[j] = make_float4(0.f, 0.f, 0.f, 1.f);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kDepth; ++j) {
+            r += T * q[j].x;
+            g += T * q[j].y;
+            b += T * q[j].z;
+            T *= q[j].w;
+        }
+    }
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
     const int x = tx * kTile + (lane & 15);
-    if (x >= a.width) return;
+    const int row = ty * kTile + 4 * k + (lane >> 4);
+    if (x >= a.width || row >= a.height) return;
+    r += T * a.bg[0];
+    g += T * a.bg[1];
+    b += T * a.bg[2];
     const size_t plane = (size_t)a.width * a.height;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int row = ty * kTile + 4 * k + (lane >> 4);
-        float r = 0.f, g = 0.f, b = 0.f, T = 1.f;
-        for (uint32_t c = 0; c < cnt; ++c) {
-            const float4 q = partial[(size_t)(c0 + c) * 256 + k * 64 + lane];
-            r += T * q.x;
-            g += T * q.y;
-            b += T * q.z;
-            T *= q.w;
-        }
-        if (row >= a.height) continue;
-        r += T * a.bg[0];
-        g += T * a.bg[1];
-        b += T * a.bg[2];
-        const size_t pidx = (size_t)row * a.width + x;
-        if (a.out_layout == 0) {
-            out[pidx] = r;
-            out[plane + pidx] = g;
-            out[2 * plane + pidx] = b;
-        } else {
-            out[3 * pidx] = r;
-            out[3 * pidx + 1] = g;
-            out[3 * pidx + 2] = b;
-        }
+    const size_t pidx = (size_t)row * a.width + x;
+    if (a.out_layout == 0) {
+        out[pidx] = r;
+        out[plane + pidx] = g;
+        out[2 * plane + pidx] = b;
+    } else {
+        out[3 * pidx] = r;
+        out[3 * pidx + 1] = g;
+        out[3 * pidx + 2] = b;
     }
 }
 
 }  // namespace
 
-int launch_dup_count(const uint32_t* sorted_ids, const SplatRec* recs, uint32_t n_vis, uint32_t* counts,
-                     hipStream_t s) {
-    if (n_vis == 0) return GSR_OK;
-    k_dup_count<<<(n_vis + kThreads - 1) / kThreads, kThreads, 0, s>>>(sorted_ids, recs, n_vis, counts);
-    GSR_LAUNCH_CHECK("dup_count");
-    return GSR_OK;
-}
+size_t bin_tmp_elems(size_t n_vis) { return (n_vis + kBinBlock - 1) / kBinBlock + 1; }
 
-int launch_dup_write(const uint32_t* sorted_ids, const SplatRec* recs, uint32_t n_vis, const uint32_t* offsets,
-                     int tiles_x, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s) {
+int launch_binning(const uint32_t* sorted_ids, const uint2* trect, uint32_t n_vis, int tiles_x, uint32_t* tmp,
+                   uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s) {
     if (n_vis == 0) return GSR_OK;
-    k_dup_write<<<(n_vis + kThreads - 1) / kThreads, kThreads, 0, s>>>(sorted_ids, recs, n_vis, offsets, tiles_x,
-                                                                       tile_keys, tile_vals);
-    GSR_LAUNCH_CHECK("dup_write");
+    const uint32_t nb = (n_vis + kBinBlock - 1) / kBinBlock;
+    k_bin_reduce<<<nb, kThreads, 0, s>>>(sorted_ids, trect, n_vis, tmp);
+    GSR_LAUNCH_CHECK("bin_reduce");
+    int rc = scan_exclusive(tmp, tmp, nb, nullptr, nullptr, s);
+    if (rc) return rc;
+    k_bin_write<<<nb, kThreads, 0, s>>>(sorted_ids, trect, n_vis, tmp, tiles_x, tile_keys, tile_vals);
+    GSR_LAUNCH_CHECK("bin_write");
     return GSR_OK;
 }
 
@@ -331,40 +430,43 @@ static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float*
     return a;
 }
 
-int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t* chunk_cnt, uint32_t* chunk_off,
-                  uint32_t* scan_tmp, uint32_t* n_chunks_dev, uint4* desc, hipStream_t s) {
+int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t* chunk_cnt, uint32_t* chunk_base,
+                  uint32_t* n_extra_dev, uint4* desc, hipStream_t s) {
     const unsigned g = (unsigned)((num_tiles + kThreads - 1) / kThreads);
-    k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_cnt);
+    k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_base);
     GSR_LAUNCH_CHECK("chunk_count");
-    int rc = scan_exclusive(chunk_cnt, chunk_off, (size_t)num_tiles, scan_tmp, n_chunks_dev, s);
+    int rc = scan_exclusive(chunk_base, chunk_base, (size_t)num_tiles, nullptr, n_extra_dev, s);
     if (rc) return rc;
-    k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_off, desc);
+    k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_cnt, chunk_base, desc);
     GSR_LAUNCH_CHECK("chunk_write");
     return GSR_OK;
 }
 
-int launch_composite(const uint4* desc, const uint32_t* n_chunks_dev, uint32_t max_chunks, const uint32_t* chunk_off,
-                     const uint32_t* chunk_cnt, const uint32_t* tile_vals, const SplatRec* recs,
-                     const FrameUniforms& u, int frag_class, float t_min, const float* bg, int out_layout,
-                     float* out, float4* partial, hipStream_t s) {
+int launch_composite(const uint4* desc, const uint32_t* n_chunks_dev, uint32_t max_chunks, const uint32_t* chunk_cnt,
+                     const uint32_t* chunk_base, uint32_t* sat, const uint32_t* tile_vals, const SplatRec* recs,
+                     const FrameUniforms& u, int frag_class, float t_min, const float* bg, int out_layout, float* out,
+                     float4* partial, hipStream_t s) {
     const CompositeArgs a = make_args(u, t_min, bg, out_layout);
     const unsigned grid = (unsigned)((max_chunks + 3) / 4);
     switch (frag_class) {
         case kFragGauss:
-            k_composite<kFragGauss><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial);
+            k_composite<kFragGauss><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial, sat);
             break;
         case kFragBillboard:
-            k_composite<kFragBillboard><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial);
+            k_composite<kFragBillboard><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial,
+                                                                  sat);
             break;
         case kFragFlatBall:
-            k_composite<kFragFlatBall><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial);
+            k_composite<kFragFlatBall><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial,
+                                                                 sat);
             break;
         default:
-            k_composite<kFragGaussBall><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial);
+            k_composite<kFragGaussBall><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial,
+                                                                  sat);
             break;
     }
     GSR_LAUNCH_CHECK("composite");
-    k_merge<<<(unsigned)((a.num_tiles + 3) / 4), kThreads, 0, s>>>(chunk_off, chunk_cnt, partial, a, out);
+    k_merge<<<(unsigned)a.num_tiles, kThreads, 0, s>>>(chunk_cnt, chunk_base, partial, sat, a, out);
     GSR_LAUNCH_CHECK("merge");
     return GSR_OK;
 }

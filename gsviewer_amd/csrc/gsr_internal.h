@@ -130,10 +130,13 @@ int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
 // radix_sort.hip: stable LSD sort of (key, val) by bits [begin_bit, end_bit).
 // Buffers are ping-ponged; the sorted result ends in (*keys_io, *vals_io)
 // (pointers swapped as needed). vals_in == nullptr means vals = 0..n-1.
+// n_dev (nullable): device-side element count <= n (grids are sized by n).
+// totals: radix_totals_elems() uint32 of scratch.
 size_t radix_tmp_elems(size_t n);
+size_t radix_totals_elems();
 int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt,
-                     uint32_t** vals_alt, bool identity_vals, size_t n, int begin_bit,
-                     int end_bit, uint32_t* tmp, hipStream_t s);
+                     uint32_t** vals_alt, bool identity_vals, size_t n, const uint32_t* n_dev,
+                     int begin_bit, int end_bit, uint32_t* tmp, uint32_t* totals, hipStream_t s);
 
 // scene.hip
 int scene_repack_from_fields(SceneData& sd, const float* xyz, const float* rot,
@@ -146,24 +149,23 @@ int launch_cull(const SceneData& sd, const FrameUniforms& u, uint64_t* vis_mask,
                 uint32_t* wave_counts, hipStream_t s);
 int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_t* vis_mask,
                       const uint32_t* wave_off, const uint32_t* n_vis_dev, SplatRec* recs,
-                      uint32_t* depth_keys, int32_t* radii, hipStream_t s);
+                      uint32_t* depth_keys, uint2* trect, uint32_t* n_dup_dev, int32_t* radii,
+                      hipStream_t s);
 int launch_depth_keys_all(const SceneData& sd, const float* V, uint32_t* keys, hipStream_t s);
 
 // composite.hip
-int launch_dup_count(const uint32_t* sorted_ids, const SplatRec* recs, uint32_t n_vis,
-                     uint32_t* counts, hipStream_t s);
-int launch_dup_write(const uint32_t* sorted_ids, const SplatRec* recs, uint32_t n_vis,
-                     const uint32_t* offsets, int tiles_x, uint32_t* tile_keys,
-                     uint32_t* tile_vals, hipStream_t s);
+size_t bin_tmp_elems(size_t n_vis);
+int launch_binning(const uint32_t* sorted_ids, const uint2* trect, uint32_t n_vis, int tiles_x,
+                   uint32_t* tmp, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s);
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
                        hipStream_t s);
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t* chunk_cnt,
-                  uint32_t* chunk_off, uint32_t* scan_tmp, uint32_t* n_chunks_dev, uint4* desc,
-                  hipStream_t s);
+                  uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, hipStream_t s);
 int launch_composite(const uint4* desc, const uint32_t* n_chunks_dev, uint32_t max_chunks,
-                     const uint32_t* chunk_off, const uint32_t* chunk_cnt, const uint32_t* tile_vals,
-                     const SplatRec* recs, const FrameUniforms& u, int frag_class, float t_min,
-                     const float* bg, int out_layout, float* out, float4* partial, hipStream_t s);
+                     const uint32_t* chunk_cnt, const uint32_t* chunk_base, uint32_t* sat,
+                     const uint32_t* tile_vals, const SplatRec* recs, const FrameUniforms& u,
+                     int frag_class, float t_min, const float* bg, int out_layout, float* out,
+                     float4* partial, hipStream_t s);
 
 }  // namespace gsr
 

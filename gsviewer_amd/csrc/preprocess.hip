@@ -227,22 +227,15 @@ __device__ __forceinline__ V3 sh_color(const float4* __restrict__ sh, int64_t n,
 
 __device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
 
-__global__ __launch_bounds__(kThreads) void k_preprocess(const float4* __restrict__ pos_op, const float4* __restrict__ rot,
-                                                         const float4* __restrict__ scale, const float4* __restrict__ sh,
-                                                         int64_t n, FrameUniforms u,
-                                                         const uint64_t* __restrict__ vis_mask,
-                                                         const uint32_t* __restrict__ wave_off,
-                                                         const uint32_t* __restrict__ n_vis_dev,
-                                                         SplatRec* __restrict__ recs, uint32_t* __restrict__ depth_keys,
-                                                         int32_t* __restrict__ radii) {
-    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t m = vis_mask[i >> 6];
-    const bool vis = (m >> __lane_id()) & 1ull;
-    if (!vis) {
-        if (radii) radii[i] = 0;
-        return;
-    }
+// Per-Gaussian body of k_preprocess for a visible lane; returns the number of
+// 16x16 tiles its covered pixel rectangle touches.
+__device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ pos_op, const float4* __restrict__ rot,
+                                                  const float4* __restrict__ scale, const float4* __restrict__ sh,
+                                                  int64_t n, const FrameUniforms& u, uint64_t m, int64_t i,
+                                                  const uint32_t* __restrict__ wave_off,
+                                                  const uint32_t* __restrict__ n_vis_dev, SplatRec* __restrict__ recs,
+                                                  uint32_t* __restrict__ depth_keys, uint2* __restrict__ trect,
+                                                  int32_t* __restrict__ radii) {
     const uint32_t slot = n_vis_dev[0] - 1u - (wave_off[i >> 6] + (uint32_t)__popcll(m & lanemask_lt()));
 
     const float4 po = pos_op[i];
@@ -386,7 +379,44 @@ __global__ __launch_bounds__(kThreads) void k_preprocess(const float4* __restric
         const float rr = ceilf(fmaxf(qs[0], qs[1]));
         radii[i] = (rr >= 0.f && rr < 2147483520.f) ? (int32_t)rr : 0;
     }
+    uint32_t tiles = 0;
+    uint2 tr = make_uint2(0xffffu, 0u);  // empty: tx0 > tx1
+    if (rec.x0 <= rec.x1 && rec.r0 <= rec.r1) {
+        const uint32_t tx0 = rec.x0 >> 4, tx1 = rec.x1 >> 4, ty0 = rec.r0 >> 4, ty1 = rec.r1 >> 4;
+        tr = make_uint2(tx0 | (tx1 << 16), ty0 | (ty1 << 16));
+        tiles = (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+    }
+    trect[slot] = tr;
+    return tiles;
 }
+
+__global__ __launch_bounds__(kThreads) void k_preprocess(const float4* __restrict__ pos_op, const float4* __restrict__ rot,
+                                                         const float4* __restrict__ scale, const float4* __restrict__ sh,
+                                                         int64_t n, FrameUniforms u,
+                                                         const uint64_t* __restrict__ vis_mask,
+                                                         const uint32_t* __restrict__ wave_off,
+                                                         const uint32_t* __restrict__ n_vis_dev,
+                                                         SplatRec* __restrict__ recs, uint32_t* __restrict__ depth_keys,
+                                                         uint2* __restrict__ trect, uint32_t* __restrict__ n_dup_dev,
+                                                         int32_t* __restrict__ radii) {
+    __shared__ uint32_t s_cnt[kThreads / 64];
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const uint64_t m = (i < n) ? vis_mask[i >> 6] : 0ull;
+    const bool vis = (m >> __lane_id()) & 1ull;
+    uint32_t tiles = 0;
+    if (vis) tiles = preprocess_one(pos_op, rot, scale, sh, n, u, m, i, wave_off, n_vis_dev, recs, depth_keys, trect,
+                                    radii);
+    else if (i < n && radii) radii[i] = 0;
+    // instance total for the frame (sizes the tile sort without waiting for it)
+    const uint32_t ws = wave_reduce_sum(tiles);
+    if (__lane_id() == 0) s_cnt[threadIdx.x >> 6] = ws;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t b = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        if (b) atomicAdd(n_dup_dev, b);
+    }
+}
+
 
 __global__ __launch_bounds__(kThreads) void k_depth_keys_all(const float4* __restrict__ pos_op, int64_t n, float v8,
                                                              float v9, float v10, float v11, uint32_t* __restrict__ keys) {
@@ -408,10 +438,10 @@ int launch_cull(const SceneData& sd, const FrameUniforms& u, uint64_t* vis_mask,
 
 int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_t* vis_mask,
                       const uint32_t* wave_off, const uint32_t* n_vis_dev, SplatRec* recs, uint32_t* depth_keys,
-                      int32_t* radii, hipStream_t s) {
+                      uint2* trect, uint32_t* n_dup_dev, int32_t* radii, hipStream_t s) {
     const unsigned grid = (unsigned)((sd.n + kThreads - 1) / kThreads);
     k_preprocess<<<grid, kThreads, 0, s>>>(sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, u, vis_mask, wave_off, n_vis_dev,
-                                           recs, depth_keys, radii);
+                                           recs, depth_keys, trect, n_dup_dev, radii);
     GSR_LAUNCH_CHECK("preprocess");
     return GSR_OK;
 }

@@ -12,6 +12,7 @@ constexpr int kThreads = 256;
 constexpr int kItems = 16;
 constexpr int kTileItems = kThreads * kItems;  // 4096
 constexpr int kPartialThreads = 1024;
+constexpr size_t kSingleMax = 131072;  // single-workgroup scan up to this many elements
 
 // Exclusive scan of one value per thread across a block of NT threads.
 template <int NT>
@@ -115,6 +116,53 @@ __global__ __launch_bounds__(kThreads) void k_scan_final(const uint32_t* __restr
     }
 }
 
+// One workgroup scans everything (n up to ~1e5): one launch instead of three
+// for the small arrays of a frame (wave counts, tiles, block sums).  The array
+// is walked in 4096-element chunks: coalesced dwordx4 loads (next chunk
+// prefetched), a block scan per chunk, a running carry.
+__global__ __launch_bounds__(kPartialThreads) void k_scan_single(const uint32_t* __restrict__ in,
+                                                                 uint32_t* __restrict__ out, size_t n,
+                                                                 uint32_t* __restrict__ total_dev) {
+    __shared__ uint32_t lds[2][kPartialThreads / 64];
+    constexpr size_t kChunk = 4 * kPartialThreads;
+    const bool aligned = (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
+    auto load4 = [&](size_t c, uint32_t (&v)[4]) {
+        const size_t i = c * kChunk + 4 * (size_t)threadIdx.x;
+        if (aligned && i + 4 <= n) {
+            const uint4 t = *reinterpret_cast<const uint4*>(in + i);
+            v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+            for (int k = 0; k < 4; ++k) v[k] = (i + k < n) ? in[i + k] : 0u;
+        }
+    };
+    const size_t nchunks = (n + kChunk - 1) / kChunk;
+    uint32_t carry = 0;
+    uint32_t cur[4];
+    load4(0, cur);
+    for (size_t c = 0; c < nchunks; ++c) {
+        uint32_t nxt[4] = {0u, 0u, 0u, 0u};
+        if (c + 1 < nchunks) load4(c + 1, nxt);
+        const uint32_t s = cur[0] + cur[1] + cur[2] + cur[3];
+        uint32_t total;
+        uint32_t run = carry + block_exclusive<kPartialThreads>(s, lds[c & 1], total);
+        const size_t i = c * kChunk + 4 * (size_t)threadIdx.x;
+        uint32_t o[4];
+        for (int k = 0; k < 4; ++k) {
+            o[k] = run;
+            run += cur[k];
+        }
+        if (aligned && i + 4 <= n) {
+            *reinterpret_cast<uint4*>(out + i) = make_uint4(o[0], o[1], o[2], o[3]);
+        } else {
+            for (int k = 0; k < 4; ++k)
+                if (i + k < n) out[i + k] = o[k];
+        }
+        carry += total;
+        for (int k = 0; k < 4; ++k) cur[k] = nxt[k];
+    }
+    if (threadIdx.x == 0 && total_dev) *total_dev = carry;
+}
+
 }  // namespace
 
 size_t scan_tmp_elems(size_t n) {
@@ -128,6 +176,12 @@ int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
         if (total_dev) GSR_HIP_CHECK(hipMemsetAsync(total_dev, 0, sizeof(uint32_t), s));
         return GSR_OK;
     }
+    if (n <= kSingleMax) {
+        k_scan_single<<<1, kPartialThreads, 0, s>>>(in, out, n, total_dev);
+        GSR_LAUNCH_CHECK("scan_single");
+        return GSR_OK;
+    }
+    if (!tmp) return set_error(GSR_ERR_INVALID, "scan: temporary buffer required for large n");
     const size_t nb = (n + kTileItems - 1) / kTileItems;
     k_scan_reduce<<<dim3((unsigned)nb), dim3(kThreads), 0, s>>>(in, n, tmp);
     GSR_LAUNCH_CHECK("scan_reduce");
