@@ -75,7 +75,7 @@ struct gsr_context {
     gsr::DevBuf<uint32_t> chunk_cnt, chunk_base;  // per tile
     gsr::DevBuf<uint4> chunk_desc;                // per chunk
     gsr::DevBuf<float4> partial;                  // per chunk x 256 px (multi-chunk tiles)
-    uint32_t chunk = 256;                         // instances per compositing chunk
+    uint32_t chunk = 192;                         // instances per compositing chunk (swept: 128-192 best)
     uint32_t* host_counters = nullptr;  // pinned
     hipEvent_t counts_ready = nullptr;
     gsr_frame_stats stats{};

@@ -238,6 +238,7 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
             }
         }
         const int nb = (int)min((uint32_t)kBatch, end - b);
+#pragma unroll 2
         for (int j = 0; j < nb; ++j) {
             const float4 q0 = my[j * 4 + 0];  // cx cy sx sy
             const float4 q1 = my[j * 4 + 1];  // A B C opacity
@@ -246,26 +247,34 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
             const int sx0 = __float_as_int(q2.w), sx1 = __float_as_int(q3.x);
             const int sr0 = __builtin_amdgcn_readfirstlane(__float_as_int(q3.y));
             const int sr1 = __builtin_amdgcn_readfirstlane(__float_as_int(q3.z));
-            const bool inx = (x >= sx0) & (x <= sx1);
+            // coverage as a 0/1 multiplier: no exec-mask branches in the pixel math
+            const float mx = ((uint32_t)(x - sx0) <= (uint32_t)(sx1 - sx0)) ? 1.0f : 0.0f;
+            const float opx = q1.w * mx;
             const float dx = (px - q0.x) * q0.z;
+            // power*log2(e) = (c2*dy + p1)*dy + p0 with
+            // power = -0.5*(A dx dx + C dy dy) - B dx dy  (gau_frag.glsl:37)
+            constexpr float kLog2e = 1.4426950408889634f;
+            const float p0 = (-0.5f * kLog2e) * q1.x * dx * dx;
+            const float p1 = (-kLog2e) * q1.y * dx;
+            const float c2 = (-0.5f * kLog2e) * q1.z;
+            // scalar 4-bit mask of the 16x4 slices the splat's rows touch (and still live)
+            const int slo = max(sr0 - row_base, 0) >> 2, shi = min(sr1 - row_base, 15) >> 2;
+            const uint32_t smask = (shi >= slo ? ((2u << shi) - (1u << slo)) : 0u) & live;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int srow0 = row_base + 4 * k;
-                // scalar: slice saturated, or the splat's rows miss the slice
-                if (!(live & (1u << k)) || srow0 > sr1 || srow0 + 3 < sr0) continue;
-                const int row = srow0 + lrow;
-                const bool in = inx & (row >= sr0) & (row <= sr1) & (T[k] >= t_min);
+                if (!(smask & (1u << k))) continue;
+                const bool inrow = (uint32_t)(lrow - (sr0 - srow0)) <= (uint32_t)(sr1 - sr0);
                 float alpha, fr = q2.x, fg = q2.y, fb = q2.z;
-                bool keep;
                 if (FRAG == kFragBillboard) {
-                    alpha = 1.0f;
-                    keep = in;
+                    alpha = inrow ? mx : 0.0f;
                 } else {
                     const float dy = (pyw[k] - q0.y) * q0.w;
-                    const float power = -0.5f * (q1.x * dx * dx + q1.z * dy * dy) - q1.y * dx * dy;
-                    const float e = __expf(power);
-                    alpha = fminf(0.99f, q1.w * e);
-                    keep = in & !(power > 0.0f) & !(alpha < (1.0f / 255.0f));
+                    const float pw = (c2 * dy + p1) * dy + p0;  // power * log2(e)
+                    const float e = __builtin_amdgcn_exp2f(pw);  // exp(power)
+                    alpha = fminf(0.99f, (inrow ? opx : 0.0f) * e);
+                    // discards: power > 0, alpha < 1/255
+                    alpha = ((pw > 0.0f) | (alpha < (1.0f / 255.0f))) ? 0.0f : alpha;
                     if (FRAG == kFragFlatBall || FRAG == kFragGaussBall) alpha = (alpha > 0.22f) ? 1.0f : 0.0f;
                     if (FRAG == kFragGaussBall) {
                         fr = fminf(fmaxf(fr * e, 0.f), 1.f);
@@ -273,13 +282,12 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
                         fb = fminf(fmaxf(fb * e, 0.f), 1.f);
                     }
                 }
-                if (keep) {
-                    const float w = alpha * T[k];
-                    cr[k] += fr * w;
-                    cg[k] += fg * w;
-                    cb[k] += fb * w;
-                    T[k] = T[k] * (1.0f - alpha);
-                }
+                // alpha == 0 leaves (C, T) bit-identical: a discarded fragment
+                const float w = alpha * T[k];
+                cr[k] += fr * w;
+                cg[k] += fg * w;
+                cb[k] += fb * w;
+                T[k] = T[k] - w;
             }
         }
         if (t_min > 0.f) {

@@ -137,9 +137,17 @@ __device__ __forceinline__ float4 load_plane(const float4* __restrict__ sh, int6
     return sh[(int64_t)p * n + i];
 }
 
-// Colour varying, gau_vert.glsl:251-330 (modes other than -3 / -2).
-__device__ __forceinline__ V3 sh_color(const float4* __restrict__ sh, int64_t n, int64_t i, float x, float y, float z,
-                                       const FrameUniforms& u) {
+// SH floats needed at effective degree DEG (gau_vert.glsl:289-327 gates).
+template <int DEG>
+constexpr int sh_planes_for() {
+    return DEG < 0 ? 0 : DEG == 0 ? 1 : DEG == 1 ? 3 : DEG == 2 ? 7 : 12;
+}
+
+// Colour varying, gau_vert.glsl:274-330, evaluated at effective degree DEG
+// (the host picks DEG = what `sh_dim > 3/12/27 && render_mod >= 1/2/3`
+// enables).  f[] holds the preloaded SH floats of this Gaussian.
+template <int DEG>
+__device__ __forceinline__ V3 sh_color(const float (&f)[48], float x, float y, float z, const FrameUniforms& u) {
     // dir = normalize(g_pos.xyz - cam_pos), rotateLightDirection
     V3 d = normalize3(x - u.campos[0], y - u.campos[1], z - u.campos[2]);
     float dx = d.x, dy = d.y, dz = d.z;
@@ -161,36 +169,18 @@ __device__ __forceinline__ V3 sh_color(const float4* __restrict__ sh, int64_t n,
         dx = rx;
         dy = ry;
     }
-    const int sh_dim = u.sh_dim;
-    const int mode = u.render_mod;
-    // Load the SH floats needed at this degree: g[k] = coefficient k RGB.
-    float f[48];
-    const int need = (sh_dim > 27 && mode >= 3) ? 48 : (sh_dim > 12 && mode >= 2) ? 27 : (sh_dim > 3 && mode >= 1) ? 12 : 3;
-    const int planes = (need + 3) >> 2;
-#pragma unroll
-    for (int p = 0; p < 12; ++p) {
-        if (p < planes) {
-            const float4 t = load_plane(sh, n, p, i);
-            f[4 * p + 0] = t.x;
-            f[4 * p + 1] = t.y;
-            f[4 * p + 2] = t.z;
-            f[4 * p + 3] = t.w;
-        } else {
-            f[4 * p + 0] = f[4 * p + 1] = f[4 * p + 2] = f[4 * p + 3] = 0.f;
-        }
-    }
 #define G(k, c) f[3 * (k) + (c)]
     float col[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) col[c] = SH_C0 * G(0, c);
-    if (sh_dim > 3 && mode >= 1) {
+    if (DEG >= 1) {
         const float X = dx, Y = dy, Z = dz;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             col[c] = ((col[c] - (SH_C1 * Y) * G(1, c)) + (SH_C1 * Z) * G(2, c)) - (SH_C1 * X) * G(3, c);
             col[c] = col[c] * u.dc_factor;
         }
-        if (sh_dim > 12 && mode >= 2) {
+        if (DEG >= 2) {
             const float xx = X * X, yy = Y * Y, zz = Z * Z;
             const float xy = X * Y, yz = Y * Z, xz = X * Z;
             const float k4 = SH_C2_0 * xy, k5 = SH_C2_1 * yz, k6 = SH_C2_2 * ((2.0f * zz - xx) - yy);
@@ -198,7 +188,7 @@ __device__ __forceinline__ V3 sh_color(const float4* __restrict__ sh, int64_t n,
 #pragma unroll
             for (int c = 0; c < 3; ++c)
                 col[c] = ((((col[c] + k4 * G(4, c)) + k5 * G(5, c)) + k6 * G(6, c)) + k7 * G(7, c)) + k8 * G(8, c);
-            if (sh_dim > 27 && mode >= 3) {
+            if (DEG >= 3) {
                 const float k9 = (SH_C3_0 * Y) * (3.0f * xx - yy);
                 const float k10 = (SH_C3_1 * xy) * Z;
                 const float k11 = (SH_C3_2 * Y) * ((4.0f * zz - xx) - yy);
@@ -229,6 +219,7 @@ __device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.f), 
 
 // Per-Gaussian body of k_preprocess for a visible lane; returns the number of
 // 16x16 tiles its covered pixel rectangle touches.
+template <int DEG>
 __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ pos_op, const float4* __restrict__ rot,
                                                   const float4* __restrict__ scale, const float4* __restrict__ sh,
                                                   int64_t n, const FrameUniforms& u, uint64_t m, int64_t i,
@@ -238,12 +229,27 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
                                                   int32_t* __restrict__ radii) {
     const uint32_t slot = n_vis_dev[0] - 1u - (wave_off[i >> 6] + (uint32_t)__popcll(m & lanemask_lt()));
 
+    // issue every load of this Gaussian up front (all unconditional at this DEG)
     const float4 po = pos_op[i];
+    const float4 q1 = rot[i];
+    const float4 sc4 = scale[i];
+    float f[48];
+#pragma unroll
+    for (int p = 0; p < 12; ++p) {
+        if (p < sh_planes_for<DEG>()) {
+            const float4 t = load_plane(sh, n, p, i);
+            f[4 * p + 0] = t.x;
+            f[4 * p + 1] = t.y;
+            f[4 * p + 2] = t.z;
+            f[4 * p + 3] = t.w;
+        } else {
+            f[4 * p + 0] = f[4 * p + 1] = f[4 * p + 2] = f[4 * p + 3] = 0.f;
+        }
+    }
     const float x = po.x, y = po.y, z = po.z;
     const Projected pr = project(x, y, z, u);
 
     // quatMultiply(g_rot, rot_modifier) (gau_vert.glsl:134-141, :224)
-    const float4 q1 = rot[i];
     const float q1x = q1.x, q1y = q1.y, q1z = q1.z, q1w = q1.w;
     const float q2x = u.rotmod[0], q2y = u.rotmod[1], q2z = u.rotmod[2], q2w = u.rotmod[3];
     const float qx = ((q1w * q2x + q1x * q2w) + q1y * q2z) - q1z * q2y;
@@ -252,7 +258,6 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     const float qw = ((q1w * q2w - q1x * q2x) - q1y * q2y) - q1z * q2z;
 
     // computeCov3D (gau_vert.glsl:75-95): (r,x,y,z) = q.xyzw
-    const float4 sc4 = scale[i];
     const float s[3] = {sc4.x * u.gsf, sc4.y * u.gsf, sc4.z * u.gsf};
     const float r = qx, qx_ = qy, qy_ = qz, qz_ = qw;
     const float R[3][3] = {
@@ -358,7 +363,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
         if (mode == -1) nrm = normalize3(nrm.x, nrm.y, nrm.z);
         col = V3{0.5f * (nrm.x + 1.0f), 0.5f * (nrm.y + 1.0f), 0.5f * (nrm.z + 1.0f)};
     } else {
-        col = sh_color(sh, n, i, x, y, z, u);
+        col = sh_color<DEG < 0 ? 0 : DEG>(f, x, y, z, u);
     }
     if (mode != -6) {  // unorm target clamps the fragment colour
         col.x = clamp01(col.x);
@@ -390,6 +395,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     return tiles;
 }
 
+template <int DEG>
 __global__ __launch_bounds__(kThreads) void k_preprocess(const float4* __restrict__ pos_op, const float4* __restrict__ rot,
                                                          const float4* __restrict__ scale, const float4* __restrict__ sh,
                                                          int64_t n, FrameUniforms u,
@@ -404,7 +410,7 @@ __global__ __launch_bounds__(kThreads) void k_preprocess(const float4* __restric
     const uint64_t m = (i < n) ? vis_mask[i >> 6] : 0ull;
     const bool vis = (m >> __lane_id()) & 1ull;
     uint32_t tiles = 0;
-    if (vis) tiles = preprocess_one(pos_op, rot, scale, sh, n, u, m, i, wave_off, n_vis_dev, recs, depth_keys, trect,
+    if (vis) tiles = preprocess_one<DEG>(pos_op, rot, scale, sh, n, u, m, i, wave_off, n_vis_dev, recs, depth_keys, trect,
                                     radii);
     else if (i < n && radii) radii[i] = 0;
     // instance total for the frame (sizes the tile sort without waiting for it)
@@ -440,8 +446,21 @@ int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_
                       const uint32_t* wave_off, const uint32_t* n_vis_dev, SplatRec* recs, uint32_t* depth_keys,
                       uint2* trect, uint32_t* n_dup_dev, int32_t* radii, hipStream_t s) {
     const unsigned grid = (unsigned)((sd.n + kThreads - 1) / kThreads);
-    k_preprocess<<<grid, kThreads, 0, s>>>(sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, u, vis_mask, wave_off, n_vis_dev,
-                                           recs, depth_keys, trect, n_dup_dev, radii);
+    // effective SH degree: the gates of gau_vert.glsl:289-313; -1 = colour not from SH
+    const int m = u.render_mod;
+    int deg = (u.sh_dim > 27 && m >= 3) ? 3 : (u.sh_dim > 12 && m >= 2) ? 2 : (u.sh_dim > 3 && m >= 1) ? 1 : 0;
+    if (m == -3 || m == -2 || m == -1) deg = -1;
+#define GSR_PRE(D)                                                                                                  \
+    k_preprocess<D><<<grid, kThreads, 0, s>>>(sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, u, vis_mask, wave_off,    \
+                                              n_vis_dev, recs, depth_keys, trect, n_dup_dev, radii)
+    switch (deg) {
+        case -1: GSR_PRE(-1); break;
+        case 0: GSR_PRE(0); break;
+        case 1: GSR_PRE(1); break;
+        case 2: GSR_PRE(2); break;
+        default: GSR_PRE(3); break;
+    }
+#undef GSR_PRE
     GSR_LAUNCH_CHECK("preprocess");
     return GSR_OK;
 }
