@@ -203,8 +203,8 @@ def main():
         nvis = stats["n_visible"]
         # algorithmic bytes per launch of each stage (DESIGN.md "Roofline")
         alg = {
-            "composite": inst * (64 + 4) + ntiles * 8 + W * H * 12,
-            "preprocess": n * 8 + nvis * (rec_bytes - 16 + 64 + 4),  # masks + visible attrs in, record+key out
+            "composite": inst * (48 + 4) + ntiles * 8 + W * H * 12,
+            "preprocess": n * 8 + nvis * (rec_bytes - 16 + 48 + 4),  # masks + visible attrs in, record+key out
             "cull": n * 16 + (n // 64) * 12,
             "depth_sort": nvis * 4 * 8 * 2 + nvis * 4 * 4,
             "tile_sort": inst * 8 * 2 * 2 + inst * 4 * 2,

@@ -10,7 +10,8 @@ import os
 import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libgsr.so")
+# GSR_LIB_PATH selects an alternative build (A/B experiments); default: in-tree.
+LIB_PATH = os.environ.get("GSR_LIB_PATH") or os.path.join(_PKG, "libgsr.so")
 
 
 class GsrCamera(ctypes.Structure):

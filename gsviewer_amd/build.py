@@ -33,8 +33,8 @@ def hipcc():
     raise RuntimeError("hipcc not found (set HIPCC)")
 
 
-def _compile(src, debug):
-    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+def _compile(src, debug, bdir=BUILD, defines=()):
+    obj = os.path.join(bdir, os.path.basename(src) + ".o")
     deps = [os.path.join(CSRC, src), os.path.join(CSRC, "gsr_internal.h"), os.path.join(INCLUDE, "gsr.h")]
     if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj
@@ -43,6 +43,7 @@ def _compile(src, debug):
            "-I", INCLUDE, "-I", CSRC, os.path.join(CSRC, src), "-o", obj]
     cmd += ["-O0", "-g"] if debug else ["-O3"]
     cmd += EXTRA_FLAGS.get(src, [])
+    cmd += ["-D" + d for d in defines]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
@@ -51,26 +52,33 @@ def _compile(src, debug):
     return obj
 
 
-def build(jobs=None, debug=False, verbose=True):
-    os.makedirs(BUILD, exist_ok=True)
+def build(jobs=None, debug=False, verbose=True, defines=(), out=None):
+    """Compile and link libgsr.so.  `defines`/`out` build an experiment
+    variant (extra -D flags) into a separate .so; the default build is the
+    product library."""
+    out = out or LIB
+    bdir = BUILD if not defines else BUILD + "_" + "_".join(d.replace("=", "") for d in defines)
+    os.makedirs(bdir, exist_ok=True)
     jobs = jobs or min(len(SOURCES), os.cpu_count() or 4, 8)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, debug), SOURCES))
-    if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(o) for o in objs):
-        return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
+        objs = list(ex.map(lambda s: _compile(s, debug, bdir, defines), SOURCES))
+    if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(o) for o in objs):
+        return out
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(out + ".tmp", out)
     if verbose:
-        print("built", LIB)
-    return LIB
+        print("built", out)
+    return out
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--debug", action="store_true")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="experiment define (variant build)")
+    ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    build(a.jobs, a.debug)
+    build(a.jobs, a.debug, defines=a.defines, out=a.out)

@@ -157,7 +157,7 @@ __device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
 }
 
 // One wave per chunk, 4 pixels per lane (four 16x4 slices of the 16x16 tile).
-// Records of the chunk are gathered 64 at a time (one 64-B record per lane,
+// Records of the chunk are gathered 64 at a time (one 48-B record per lane,
 // prefetched one batch ahead in registers) into a wave-private LDS buffer and
 // then read back with wave-uniform (broadcast) ds_read_b128.  No workgroup
 // barriers: the four waves of a block are independent chunks.
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
                                                         const SplatRec* __restrict__ recs, CompositeArgs a,
                                                         float* __restrict__ out, float4* __restrict__ partial,
                                                         uint32_t* __restrict__ sat) {
-    __shared__ float4 lds[kThreads / 64][kBatch * 4];
+    __shared__ float4 lds[kThreads / 64][kBatch * 3];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t slot = blockIdx.x * (kThreads / 64) + wave;
     if (slot >= (uint32_t)a.num_tiles + n_chunks_dev[0]) return;  // device count of extra chunks
@@ -215,61 +215,61 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
     }
     float4* my = lds[wave];
 
-    float4 f0, f1, f2, f3;
+    float4 f0, f1, f2;
     {
         const uint32_t i = begin + lane;
         if (i < end && live) {
             const float4* r = reinterpret_cast<const float4*>(recs + list[i]);
-            f0 = r[0]; f1 = r[1]; f2 = r[2]; f3 = r[3];
+            f0 = r[0]; f1 = r[1]; f2 = r[2];
         }
     }
     for (uint32_t b = begin; b < end && live; b += kBatch) {
         __builtin_amdgcn_wave_barrier();
-        my[lane * 4 + 0] = f0;
-        my[lane * 4 + 1] = f1;
-        my[lane * 4 + 2] = f2;
-        my[lane * 4 + 3] = f3;
+        my[lane * 3 + 0] = f0;
+        my[lane * 3 + 1] = f1;
+        my[lane * 3 + 2] = f2;
         __builtin_amdgcn_wave_barrier();
         {  // prefetch next batch while this one is composited
             const uint32_t i = b + kBatch + lane;
             if (i < end) {
                 const float4* r = reinterpret_cast<const float4*>(recs + list[i]);
-                f0 = r[0]; f1 = r[1]; f2 = r[2]; f3 = r[3];
+                f0 = r[0]; f1 = r[1]; f2 = r[2];
             }
         }
         const int nb = (int)min((uint32_t)kBatch, end - b);
 #pragma unroll 2
         for (int j = 0; j < nb; ++j) {
-            const float4 q0 = my[j * 4 + 0];  // cx cy sx sy
-            const float4 q1 = my[j * 4 + 1];  // A B C opacity
-            const float4 q2 = my[j * 4 + 2];  // r g b x0
-            const float4 q3 = my[j * 4 + 3];  // x1 r0 r1 -
-            const int sx0 = __float_as_int(q2.w), sx1 = __float_as_int(q3.x);
-            const int sr0 = __builtin_amdgcn_readfirstlane(__float_as_int(q3.y));
-            const int sr1 = __builtin_amdgcn_readfirstlane(__float_as_int(q3.z));
+            const float4 q0 = my[j * 3 + 0];  // cx cy opacity xspan
+            const float4 q1 = my[j * 3 + 1];  // qa qb qc yspan
+            const float4 q2 = my[j * 3 + 2];  // r g b -
+            const uint32_t xs = __float_as_uint(q0.w);
+            const int sx0 = (int)(xs & 0xffffu), sx1 = (int)(xs >> 16);
+            const uint32_t ys = __builtin_amdgcn_readfirstlane(__float_as_uint(q1.w));
+            const int sr0 = (int)(ys & 0xffffu), sr1 = (int)(ys >> 16);
             // coverage as a 0/1 multiplier: no exec-mask branches in the pixel math
             const float mx = ((uint32_t)(x - sx0) <= (uint32_t)(sx1 - sx0)) ? 1.0f : 0.0f;
-            const float opx = q1.w * mx;
-            const float dx = (px - q0.x) * q0.z;
-            // power*log2(e) = (c2*dy + p1)*dy + p0 with
-            // power = -0.5*(A dx dx + C dy dy) - B dx dy  (gau_frag.glsl:37)
-            constexpr float kLog2e = 1.4426950408889634f;
-            const float p0 = (-0.5f * kLog2e) * q1.x * dx * dx;
-            const float p1 = (-kLog2e) * q1.y * dx;
-            const float c2 = (-0.5f * kLog2e) * q1.z;
+            const float opx = q0.z * mx;
+            // power*log2(e) = qa dx^2 + qb dx dy + qc dy^2 in pixel units
+            // (gau_frag.glsl:37 with coordxy's scale folded in by the preprocess)
+            const float dx = px - q0.x;
+            const float p0 = q1.x * dx * dx;
+            const float p1 = q1.y * dx;
+            const float c2 = q1.z;
             // scalar 4-bit mask of the 16x4 slices the splat's rows touch (and still live)
             const int slo = max(sr0 - row_base, 0) >> 2, shi = min(sr1 - row_base, 15) >> 2;
             const uint32_t smask = (shi >= slo ? ((2u << shi) - (1u << slo)) : 0u) & live;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int srow0 = row_base + 4 * k;
+#ifndef GSR_COMP_NOSKIP
                 if (!(smask & (1u << k))) continue;
+#endif
                 const bool inrow = (uint32_t)(lrow - (sr0 - srow0)) <= (uint32_t)(sr1 - sr0);
                 float alpha, fr = q2.x, fg = q2.y, fb = q2.z;
                 if (FRAG == kFragBillboard) {
                     alpha = inrow ? mx : 0.0f;
                 } else {
-                    const float dy = (pyw[k] - q0.y) * q0.w;
+                    const float dy = pyw[k] - q0.y;
                     const float pw = (c2 * dy + p1) * dy + p0;  // power * log2(e)
                     const float e = __builtin_amdgcn_exp2f(pw);  // exp(power)
                     alpha = fminf(0.99f, (inrow ? opx : 0.0f) * e);
@@ -282,6 +282,9 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
                         fb = fminf(fmaxf(fb * e, 0.f), 1.f);
                     }
                 }
+#ifdef GSR_COMP_NOSKIP
+                alpha = (smask & (1u << k)) ? alpha : 0.0f;
+#endif
                 // alpha == 0 leaves (C, T) bit-identical: a discarded fragment
                 const float w = alpha * T[k];
                 cr[k] += fr * w;

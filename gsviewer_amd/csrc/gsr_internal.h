@@ -14,19 +14,23 @@ namespace gsr {
 constexpr int kTile = 16;              // composite tile edge (pixels)
 constexpr int kWave = 64;              // CDNA wavefront
 
-// One visible splat after preprocess: 64 bytes, read wave-uniformly by the
-// compositor (scalar loads), so it is kept a single 64-B line.
+// One visible splat after preprocess: 48 bytes = exactly three float4, so the
+// compositor reads a record with three broadcast ds_read_b128 (12 LDS cycles).
+// The fragment falloff is stored as the quadratic form of power*log2(e) in
+// PIXEL offsets (gau_frag.glsl:37 with coordxy = (pixel - centre) * s):
+//   power*log2e = qa*dx^2 + qb*dx*dy + qc*dy^2,  dx = px - cx, dy = pyw - cy
+//   qa = -0.5*log2e*A*sx*sx,  qb = -log2e*B*sx*sy,  qc = -0.5*log2e*C*sy*sy
 struct alignas(16) SplatRec {
     float cx, cy;       // quad centre, window coords (origin bottom-left)
-    float sx, sy;       // coordxy = (pixel - centre) * s  (affine varying)
-    float A, B, C;      // conic (gau_vert.glsl:240)
     float opacity;      // alpha varying
+    uint32_t xspan;     // covered pixel columns x0 | x1 << 16, inclusive (image coords)
+    float qa, qb, qc;   // falloff quadratic form (see above)
+    uint32_t yspan;     // covered pixel rows r0 | r1 << 16, inclusive (image coords, row 0 = top)
     float r, g, b;      // colour varying (clamped to [0,1] unless mode -6)
-    int32_t x0, x1;     // covered pixel columns, inclusive (image coords)
-    int32_t r0, r1;     // covered pixel rows, inclusive (image coords, row 0 = top)
-    int32_t pad;
+    float pad;
 };
-static_assert(sizeof(SplatRec) == 64, "SplatRec must be 64 bytes");
+static_assert(sizeof(SplatRec) == 48, "SplatRec must be 48 bytes");
+constexpr float kLog2e = 1.4426950408889634f;
 
 // Render-mode classes of the fragment stage (gau_frag.glsl:16-52).
 enum FragClass : int { kFragGauss = 0, kFragBillboard = 1, kFragFlatBall = 2, kFragGaussBall = 3 };

@@ -10,7 +10,7 @@
 //                 ballot + count per wave;  -> scan of the wave counts
 //   k_preprocess  recomputes the cull for its lane, and for visible lanes
 //                 loads rot/scale/SH planes (coalesced float4), writes the
-//                 64-B SplatRec and the depth key at its compacted slot.
+//                 48-B SplatRec and the depth key at its compacted slot.
 // Compaction slot = n_vis-1-(rank in Gaussian-index order), so a stable
 // ascending depth sort resolves exact depth ties in DESCENDING index order:
 // the exact reverse of the GL draw order (renderer_ogl.py:24, ascending z,
@@ -312,9 +312,9 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     const float det = ca * cc - cb * cb;
     const float det_inv = 1.0f / det;
     SplatRec rec;
-    rec.A = cc * det_inv;
-    rec.B = -cb * det_inv;
-    rec.C = ca * det_inv;
+    const float cA = cc * det_inv;
+    const float cB = -cb * det_inv;
+    const float cC = ca * det_inv;
     rec.opacity = po.w;
 
     // quad (gau_vert.glsl:225, 242-245) + viewport transform
@@ -333,8 +333,9 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     }
     rec.cx = cw[0];
     rec.cy = cw[1];
-    rec.sx = sc[0];
-    rec.sy = sc[1];
+    rec.qa = (((-0.5f * kLog2e) * cA) * sc[0]) * sc[0];
+    rec.qb = (((-kLog2e) * cB) * sc[0]) * sc[1];
+    rec.qc = (((-0.5f * kLog2e) * cC) * sc[1]) * sc[1];
     int x0, x1, j0i, j1i;
     pixel_span(lo[0], hi[0], u.width, x0, x1);
     pixel_span(lo[1], hi[1], u.height, j0i, j1i);
@@ -342,11 +343,11 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     x1 = min(x1, u.width - 1);
     j0i = max(j0i, 0);
     j1i = min(j1i, u.height - 1);
-    rec.x0 = x0;
-    rec.x1 = x1;
-    rec.r0 = (u.height - 1) - j1i;
-    rec.r1 = (u.height - 1) - j0i;
-    rec.pad = 0;
+    const int r0 = (u.height - 1) - j1i, r1 = (u.height - 1) - j0i;
+    const bool nonempty = (x0 <= x1) && (r0 <= r1);
+    rec.xspan = nonempty ? ((uint32_t)x0 | ((uint32_t)x1 << 16)) : 0xffffu;  // empty: x0 > x1
+    rec.yspan = nonempty ? ((uint32_t)r0 | ((uint32_t)r1 << 16)) : 0xffffu;
+    rec.pad = 0.f;
 
     // colour varying
     const int mode = u.render_mod;
@@ -375,10 +376,9 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     rec.b = col.z;
 
     float4* dst = reinterpret_cast<float4*>(recs + slot);
-    dst[0] = make_float4(rec.cx, rec.cy, rec.sx, rec.sy);
-    dst[1] = make_float4(rec.A, rec.B, rec.C, rec.opacity);
-    dst[2] = make_float4(rec.r, rec.g, rec.b, __int_as_float(rec.x0));
-    dst[3] = make_float4(__int_as_float(rec.x1), __int_as_float(rec.r0), __int_as_float(rec.r1), 0.f);
+    dst[0] = make_float4(rec.cx, rec.cy, rec.opacity, __uint_as_float(rec.xspan));
+    dst[1] = make_float4(rec.qa, rec.qb, rec.qc, __uint_as_float(rec.yspan));
+    dst[2] = make_float4(rec.r, rec.g, rec.b, 0.f);
     depth_keys[slot] = float_order_key(-pr.pv[2]);
     if (radii) {
         const float rr = ceilf(fmaxf(qs[0], qs[1]));
@@ -386,8 +386,8 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     }
     uint32_t tiles = 0;
     uint2 tr = make_uint2(0xffffu, 0u);  // empty: tx0 > tx1
-    if (rec.x0 <= rec.x1 && rec.r0 <= rec.r1) {
-        const uint32_t tx0 = rec.x0 >> 4, tx1 = rec.x1 >> 4, ty0 = rec.r0 >> 4, ty1 = rec.r1 >> 4;
+    if (nonempty) {
+        const uint32_t tx0 = x0 >> 4, tx1 = x1 >> 4, ty0 = r0 >> 4, ty1 = r1 >> 4;
         tr = make_uint2(tx0 | (tx1 << 16), ty0 | (ty1 << 16));
         tiles = (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
     }

@@ -159,7 +159,7 @@ int gsr_context_stage_times(gsr_context* ctx, double* ms_out /* [GSR_NUM_STAGES]
 /* Test hook: copy an internal array of the last gsr_render on `ctx` into
  * dst_dev (device memory, at most max_bytes). Returns the number of bytes
  * copied (>= 0) or a negative gsr_status.  what:
- *   GSR_DEBUG_RECORDS      64-B splat records in compacted slot order
+ *   GSR_DEBUG_RECORDS      48-B splat records in compacted slot order
  *                          (slot s = the s-th visible Gaussian in DESCENDING id order)
  *   GSR_DEBUG_DEPTH_ORDER  uint32 record slots, front-to-back
  *   GSR_DEBUG_TILE_RANGES  uint32 pairs [begin, end) per 16x16 tile (row-major tiles)

@@ -71,7 +71,7 @@ def gpu_frame(g, cam, settings, with_debug=False, radii=False):
             torch.cuda.synchronize()
             return buf.cpu().numpy().view(np.uint8)[:got].view(dtype)
 
-        res["records"] = grab(_lib.GSR_DEBUG_RECORDS, nv * 64, np.uint8).reshape(nv, 64)
+        res["records"] = grab(_lib.GSR_DEBUG_RECORDS, nv * 48, np.uint8).reshape(nv, 48)
         res["depth_order"] = grab(_lib.GSR_DEBUG_DEPTH_ORDER, nv * 4, np.uint32)
         res["ranges"] = grab(_lib.GSR_DEBUG_TILE_RANGES, nt * 8, np.uint32).reshape(nt, 2)
         res["tile_list"] = grab(_lib.GSR_DEBUG_TILE_LIST, nd * 4, np.uint32)
@@ -81,10 +81,25 @@ def gpu_frame(g, cam, settings, with_debug=False, radii=False):
 
 
 def decode_records(raw):
-    f = raw.view(np.float32).reshape(-1, 16)
-    i = raw.view(np.int32).reshape(-1, 16)
-    return dict(center=f[:, 0:2], coord_scale=f[:, 2:4], conic=f[:, 4:7], opacity=f[:, 7], color=f[:, 8:11],
-                x0=i[:, 11], x1=i[:, 12], r0=i[:, 13], r1=i[:, 14])
+    """48-B SplatRec (gsviewer_amd/csrc/gsr_internal.h)."""
+    f = raw.view(np.float32).reshape(-1, 12)
+    u = raw.view(np.uint32).reshape(-1, 12)
+    return dict(center=f[:, 0:2], opacity=f[:, 2], x0=(u[:, 3] & 0xFFFF).astype(np.int64),
+                x1=(u[:, 3] >> 16).astype(np.int64), qa=f[:, 4], qb=f[:, 5], qc=f[:, 6],
+                r0=(u[:, 7] & 0xFFFF).astype(np.int64), r1=(u[:, 7] >> 16).astype(np.int64), color=f[:, 8:11])
+
+
+def expected_quadratic(vs):
+    """qa, qb, qc of the record from the oracle's conic and coordxy scale, in
+    the kernel's float32 evaluation order (preprocess.hip)."""
+    F = np.float32
+    L = F(1.4426950408889634)
+    A, B, C = vs["conic"][:, 0], vs["conic"][:, 1], vs["conic"][:, 2]
+    sx, sy = vs["coord_scale"][:, 0], vs["coord_scale"][:, 1]
+    qa = (((F(-0.5) * L) * A) * sx) * sx
+    qb = (((-L) * B) * sx) * sy
+    qc = (((F(-0.5) * L) * C) * sy) * sy
+    return qa.astype(F), qb.astype(F), qc.astype(F)
 
 
 def compare_images(gpu, ref, tol=TOL_EXACT, frac=TOL_EXACT_FRAC, tol_max=TOL_MAX):

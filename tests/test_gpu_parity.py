@@ -6,7 +6,7 @@ import pytest
 from gsviewer_amd.camera import Camera, euler_to_rotation_matrix
 from gsviewer_amd.gaussian_data import garden_standin, naive_gaussian, random_scene
 from oracle import gl_oracle as O
-from helpers import TOL_TMIN, compare_images, decode_records, gpu_frame, uniforms_for
+from helpers import TOL_TMIN, compare_images, decode_records, expected_quadratic, gpu_frame, uniforms_for
 
 pytestmark = pytest.mark.gpu
 
@@ -51,13 +51,18 @@ def test_preprocess_records_bit_exact(gpu):
     rec = decode_records(res["records"])
     assert len(vis_desc) == len(rec["opacity"])
     np.testing.assert_array_equal(rec["center"], vs["center"][vis_desc])
-    np.testing.assert_array_equal(rec["coord_scale"], vs["coord_scale"][vis_desc])
-    np.testing.assert_array_equal(rec["conic"], vs["conic"][vis_desc])
+    qa, qb, qc = expected_quadratic(vs)
+    np.testing.assert_array_equal(rec["qa"], qa[vis_desc])
+    np.testing.assert_array_equal(rec["qb"], qb[vis_desc])
+    np.testing.assert_array_equal(rec["qc"], qc[vis_desc])
     np.testing.assert_array_equal(rec["opacity"], vs["opacity"][vis_desc])
     np.testing.assert_array_equal(rec["color"], np.clip(vs["color"][vis_desc], 0, 1))
     x0, x1, r0, r1 = O.splat_rects(vs, U)
+    nonempty = (x0 <= x1) & (r0 <= r1)
+    ne = nonempty[vis_desc]
     for a, b in [(rec["x0"], x0), (rec["x1"], x1), (rec["r0"], r0), (rec["r1"], r1)]:
-        np.testing.assert_array_equal(a, b[vis_desc])
+        np.testing.assert_array_equal(a[ne], b[vis_desc][ne])
+    assert np.all(rec["x0"][~ne] > rec["x1"][~ne])
 
 
 def test_depth_order_and_tile_lists_exact(gpu):
