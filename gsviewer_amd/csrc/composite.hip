@@ -152,6 +152,13 @@ __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restric
     }
 }
 
+// Bits [lo, hi] of a 16-bit mask, clamped to [0, 15]; 0 if the range is empty.
+__device__ __forceinline__ uint32_t span_bits16(int lo, int hi) {
+    lo = max(lo, 0);
+    hi = min(hi, 15);
+    return hi >= lo ? ((2u << hi) - (1u << lo)) : 0u;
+}
+
 __device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -188,7 +195,9 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
     const uint32_t kk = d.w & 0xffffu;
     const int lane = __lane_id();
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
-    const int x = tx * kTile + (lane & 15);
+    const int lcol = lane & 15;
+    const int col_base = tx * kTile;
+    const int x = col_base + lcol;
     const int row_base = ty * kTile;
     const int lrow = lane >> 4;
     const float px = (float)x + 0.5f;
@@ -215,64 +224,97 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
     }
     float4* my = lds[wave];
 
+    // Two-stage prefetch: the records of batch b+1 and the list indices of
+    // batch b+2 are in flight while batch b is composited, so neither the
+    // index load nor the dependent record gather is ever waited on directly.
     float4 f0, f1, f2;
-    {
+    uint32_t idx_next = 0;
+    if (live) {
         const uint32_t i = begin + lane;
-        if (i < end && live) {
+        if (i < end) {
             const float4* r = reinterpret_cast<const float4*>(recs + list[i]);
             f0 = r[0]; f1 = r[1]; f2 = r[2];
         }
+        const uint32_t i2 = begin + kBatch + lane;
+        if (i2 < end) idx_next = list[i2];
     }
     for (uint32_t b = begin; b < end && live; b += kBatch) {
         __builtin_amdgcn_wave_barrier();
-        my[lane * 3 + 0] = f0;
-        my[lane * 3 + 1] = f1;
-        my[lane * 3 + 2] = f2;
+        {
+            // Tile-relative coverage of this lane's record, computed once per
+            // record (not per pixel): .w of q0 = 16-bit column mask | 16-bit
+            // row mask << 16, .w of q1 = mask of the 16x4 slices it touches.
+            const uint32_t xs = __float_as_uint(f0.w), ys = __float_as_uint(f1.w);
+            const uint32_t covx = span_bits16((int)(xs & 0xffffu) - col_base, (int)(xs >> 16) - col_base);
+            const uint32_t covy = span_bits16((int)(ys & 0xffffu) - row_base, (int)(ys >> 16) - row_base);
+            const uint32_t sl = (uint32_t)((covy & 0x000fu) != 0) | ((uint32_t)((covy & 0x00f0u) != 0) << 1) |
+                                ((uint32_t)((covy & 0x0f00u) != 0) << 2) | ((uint32_t)((covy & 0xf000u) != 0) << 3);
+            my[lane * 3 + 0] = make_float4(f0.x, f0.y, f0.z, __uint_as_float(covx | (covy << 16)));
+            my[lane * 3 + 1] = make_float4(f1.x, f1.y, f1.z, __uint_as_float(sl));
+            my[lane * 3 + 2] = f2;
+        }
         __builtin_amdgcn_wave_barrier();
-        {  // prefetch next batch while this one is composited
+        // saturation words of the other chunks, consumed after this batch
+        uint32_t satw[4];
+        const bool poll = track && kk > 0;
+        if (poll) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) satw[k] = ld_relaxed(my_sat + k);
+        }
+        {  // prefetch: records of batch b+1, list indices of batch b+2
             const uint32_t i = b + kBatch + lane;
             if (i < end) {
-                const float4* r = reinterpret_cast<const float4*>(recs + list[i]);
+                const float4* r = reinterpret_cast<const float4*>(recs + idx_next);
                 f0 = r[0]; f1 = r[1]; f2 = r[2];
             }
+            const uint32_t i2 = b + 2 * kBatch + lane;
+            if (i2 < end) idx_next = list[i2];
         }
-        const int nb = (int)min((uint32_t)kBatch, end - b);
-#pragma unroll 2
+        const int nb = __builtin_amdgcn_readfirstlane((int)min((uint32_t)kBatch, end - b));
+#ifdef GSR_COMP_LDSPIPE
+        float4 n0 = my[0], n1 = my[1], n2 = my[2];
+#endif
         for (int j = 0; j < nb; ++j) {
+#ifdef GSR_COMP_LDSPIPE
+            const float4 q0 = n0, q1 = n1, q2 = n2;
+            {
+                const int jn = min(j + 1, kBatch - 1);
+                n0 = my[jn * 3 + 0];
+                n1 = my[jn * 3 + 1];
+                n2 = my[jn * 3 + 2];
+            }
+#else
             const float4 q0 = my[j * 3 + 0];  // cx cy opacity xspan
             const float4 q1 = my[j * 3 + 1];  // qa qb qc yspan
             const float4 q2 = my[j * 3 + 2];  // r g b -
-            const uint32_t xs = __float_as_uint(q0.w);
-            const int sx0 = (int)(xs & 0xffffu), sx1 = (int)(xs >> 16);
-            const uint32_t ys = __builtin_amdgcn_readfirstlane(__float_as_uint(q1.w));
-            const int sr0 = (int)(ys & 0xffffu), sr1 = (int)(ys >> 16);
-            // coverage as a 0/1 multiplier: no exec-mask branches in the pixel math
-            const float mx = ((uint32_t)(x - sx0) <= (uint32_t)(sx1 - sx0)) ? 1.0f : 0.0f;
-            const float opx = q0.z * mx;
+#endif
+            // scalar mask of the 16x4 slices the splat touches (and still live)
+            const uint32_t smask = __builtin_amdgcn_readfirstlane(__float_as_uint(q1.w)) & live;
+            // lane coverage: bit 4k = this lane's pixel of slice k is inside the splat's quad
+            // (all-zero when the column is not: bfe_i32 gives 0 or ~0)
+            const uint32_t cov = __float_as_uint(q0.w);
+            const uint32_t rb = (cov >> (16 + lrow)) & (uint32_t)__builtin_amdgcn_sbfe((int)cov, lcol, 1);
             // power*log2(e) = qa dx^2 + qb dx dy + qc dy^2 in pixel units
             // (gau_frag.glsl:37 with coordxy's scale folded in by the preprocess)
             const float dx = px - q0.x;
             const float p0 = q1.x * dx * dx;
             const float p1 = q1.y * dx;
             const float c2 = q1.z;
-            // scalar 4-bit mask of the 16x4 slices the splat's rows touch (and still live)
-            const int slo = max(sr0 - row_base, 0) >> 2, shi = min(sr1 - row_base, 15) >> 2;
-            const uint32_t smask = (shi >= slo ? ((2u << shi) - (1u << slo)) : 0u) & live;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int srow0 = row_base + 4 * k;
 #ifndef GSR_COMP_NOSKIP
-                if (!(smask & (1u << k))) continue;
+                if (!((smask >> k) & 1u)) continue;
 #endif
-                const bool inrow = (uint32_t)(lrow - (sr0 - srow0)) <= (uint32_t)(sr1 - sr0);
+                // opacity where the pixel is covered, +0 elsewhere (bit mask, no compare)
+                const uint32_t covk = (uint32_t)__builtin_amdgcn_sbfe((int)rb, 4 * k, 1);
                 float alpha, fr = q2.x, fg = q2.y, fb = q2.z;
                 if (FRAG == kFragBillboard) {
-                    alpha = inrow ? mx : 0.0f;
+                    alpha = __uint_as_float(covk & 0x3f800000u);  // 1.0 or 0.0
                 } else {
                     const float dy = pyw[k] - q0.y;
                     const float pw = (c2 * dy + p1) * dy + p0;  // power * log2(e)
                     const float e = __builtin_amdgcn_exp2f(pw);  // exp(power)
-                    alpha = fminf(0.99f, (inrow ? opx : 0.0f) * e);
+                    alpha = fminf(0.99f, __uint_as_float(covk & __float_as_uint(q0.z)) * e);
                     // discards: power > 0, alpha < 1/255
                     alpha = ((pw > 0.0f) | (alpha < (1.0f / 255.0f))) ? 0.0f : alpha;
                     if (FRAG == kFragFlatBall || FRAG == kFragGaussBall) alpha = (alpha > 0.22f) ? 1.0f : 0.0f;
@@ -308,11 +350,11 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
                 }
             }
             live &= still;
-            if (track && kk > 0 && live) {
+            if (poll && live) {
                 uint32_t dead = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    if (0xffffffffu - ld_relaxed(my_sat + k) < kk) dead |= (1u << k);
+                    if (0xffffffffu - satw[k] < kk) dead |= (1u << k);
                 live &= ~__builtin_amdgcn_readfirstlane(dead);
             }
         }
