@@ -75,6 +75,7 @@ struct gsr_context {
     gsr::DevBuf<uint32_t> chunk_cnt, chunk_base;  // per tile
     gsr::DevBuf<uint4> chunk_desc;                // per chunk
     gsr::DevBuf<float4> partial;                  // per chunk x 256 px (multi-chunk tiles)
+    gsr::DevBuf<float4> tmax;                     // per chunk: published slice maxima of local T
     uint32_t chunk = 192;                         // instances per compositing chunk (swept: 128-192 best)
     uint32_t* host_counters = nullptr;  // pinned
     hipEvent_t counts_ready = nullptr;
@@ -342,6 +343,7 @@ int gsr_context_destroy(gsr_context* c) {
     c->tvals_b.release(); c->radix_tmp.release(); c->zero.release();
     c->chunk_cnt.release(); c->chunk_base.release();
     if (c->counts_ready) (void)hipEventDestroy(c->counts_ready); c->chunk_desc.release(); c->partial.release();
+    c->tmax.release();
     if (c->host_counters) (void)hipHostFree(c->host_counters);
     for (auto& row : c->ev)
         for (auto& e : row)
@@ -444,13 +446,14 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
     if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
     if ((rc = c->chunk_desc.ensure(max_chunks, "chunk_desc"))) return rc;
     if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
+    if ((rc = c->tmax.ensure(max_chunks, "tmax"))) return rc;
     if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
-                            c->chunk_desc.p, s)))
+                            c->chunk_desc.p, c->tmax.p, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
     if ((rc = launch_composite(c->chunk_desc.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
                                sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), st->t_min, st->bg,
-                               st->out_layout, out, c->partial.p, s)))
+                               st->out_layout, out, c->partial.p, c->tmax.p, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_COUNT, s))) return rc;
     if (c->prof_on) c->ev_pending[slot] = true;

@@ -108,6 +108,9 @@ struct CompositeArgs {
 };
 
 constexpr int kBatch = 64;  // records staged per wave per LDS batch
+#ifdef GSR_COMP_TRACE
+constexpr uint32_t kTraceMax = 1u << 16;  // waves traced per launch
+#endif
 
 // Chunks: every tile's instance list is cut into pieces of at most `chunk`
 // instances (an empty tile gets one empty chunk so it still writes the
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restric
 __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restrict__ ranges, int num_tiles,
                                                           uint32_t chunk, uint32_t* __restrict__ chunk_cnt,
                                                           uint32_t* __restrict__ chunk_base,
-                                                          uint4* __restrict__ desc) {
+                                                          uint4* __restrict__ desc, float4* __restrict__ tmax) {
     const int t = blockIdx.x * kThreads + threadIdx.x;
     if (t >= num_tiles) return;
     const uint2 r = ranges[t];
@@ -148,7 +151,9 @@ __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restric
     for (uint32_t k = 0; k < cnt; ++k) {
         const uint32_t b = r.x + k * chunk;
         const uint32_t e = min(r.y, b + chunk);
-        desc[k == 0 ? (uint32_t)t : base + k - 1] = make_uint4((uint32_t)t, b, e, (cnt << 16) | k);
+        const uint32_t slot = k == 0 ? (uint32_t)t : base + k - 1;
+        desc[slot] = make_uint4((uint32_t)t, b, e, (cnt << 16) | k);
+        if (tmax && cnt > 1) tmax[slot] = make_float4(1.f, 1.f, 1.f, 1.f);  // nothing composited yet
     }
 }
 
@@ -163,32 +168,84 @@ __device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// readfirstlane of a float's bits (the builtin takes int: a float argument
+// would be value-converted)
+__device__ __forceinline__ float uniform_f(float v) {
+    return __uint_as_float((uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(v)));
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ float wave_prod(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v *= __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ const uint32_t* chunk_tmax(const float4* tmax, uint32_t tile, uint32_t base, uint32_t j) {
+    return reinterpret_cast<const uint32_t*>(tmax + (j == 0 ? tile : base + j - 1));
+}
+
+// Issue (no wait) the loads of the published slice maxima of chunks
+// 0..min(kk,64)-1, one chunk per lane; other lanes hold 1.0.
+__device__ __forceinline__ void load_prior(const float4* tmax, uint32_t tile, uint32_t base, uint32_t kk,
+                                           uint32_t prior[4]) {
+    const uint32_t j = __lane_id();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) prior[k] = 0x3f800000u;
+    if (j < kk) {
+        const uint32_t* w = chunk_tmax(tmax, tile, base, j);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) prior[k] = ld_relaxed(w + k);
+    }
+}
+
+// B[k] = product over chunks j < kk of their published maxima of slice k
+// (chunks beyond the first 64 are read here, synchronously: very deep tiles).
+__device__ __forceinline__ void prior_bound(const float4* tmax, uint32_t tile, uint32_t base, uint32_t kk,
+                                            const uint32_t prior[4], float B[4]) {
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = __uint_as_float(prior[k]);
+    for (uint32_t j = 64 + __lane_id(); j < kk; j += 64) {
+        const uint32_t* w = chunk_tmax(tmax, tile, base, j);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] *= __uint_as_float(ld_relaxed(w + k));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) B[k] = uniform_f(wave_prod(v[k]));
+}
+
 // One wave per chunk, 4 pixels per lane (four 16x4 slices of the 16x16 tile).
 // Records of the chunk are gathered 64 at a time (one 48-B record per lane,
 // prefetched one batch ahead in registers) into a wave-private LDS buffer and
 // then read back with wave-uniform (broadcast) ds_read_b128.  No workgroup
 // barriers: the four waves of a block are independent chunks.
 //
-// Saturation words (multi-chunk tiles only): sat[tile*4 + slice] holds
-// ~(smallest chunk index) (atomicMax of the complement, so a zeroed word means
-// "none") of the first chunk whose 64 pixels of that slice all reached a LOCAL
-// transmittance < t_min; the absolute transmittance after that chunk is then
-// < t_min too, so everything behind it contributes less than t_min (the same
-// bound as sequential early termination).  Later chunks stop compositing such
-// slices and k_merge folds each slice only up to that chunk.  The words are
-// read relaxed at agent scope; a stale read only costs work, never accuracy.
+// Early termination across the chunks of a tile (multi-chunk tiles only).
+// After every batch a chunk publishes, per 16x4 slice, the maximum over its 64
+// pixels of its LOCAL transmittance: tmax[slot].s (1.0 until first written;
+// it only decreases).  Chunk kk bounds the ABSOLUTE transmittance entering it
+// by B = prod_{j<kk} tmax[chunk j] (published values are upper bounds of the
+// final local ones, unstarted chunks count 1) and stops a slice once
+// B * (its own local max) < t_min: everything behind that point, in this and
+// all later chunks, contributes less than t_min -- the bound of sequential
+// front-to-back early termination, reached while the chunks run in parallel.
+// A later chunk's bound then falls below t_min too, so it skips the slice.
+// Saturation words sat[tile*4 + slice] hold ~(smallest stopping chunk index)
+// (atomicMax of the complement; zero = none): k_merge folds each slice only up
+// to that chunk.  All words are accessed relaxed at agent scope; a stale read
+// only costs work, never accuracy.
 template <int FRAG>
-__global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict__ desc,
-                                                        const uint32_t* __restrict__ n_chunks_dev,
-                                                        const uint32_t* __restrict__ list,
-                                                        const SplatRec* __restrict__ recs, CompositeArgs a,
-                                                        float* __restrict__ out, float4* __restrict__ partial,
-                                                        uint32_t* __restrict__ sat) {
-    __shared__ float4 lds[kThreads / 64][kBatch * 3];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t slot = blockIdx.x * (kThreads / 64) + wave;
-    if (slot >= (uint32_t)a.num_tiles + n_chunks_dev[0]) return;  // device count of extra chunks
-    const uint4 d = desc[slot];
+__device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t slot, float4* __restrict__ my,
+                                                const uint32_t* __restrict__ list,
+                                                const SplatRec* __restrict__ recs, const CompositeArgs& a,
+                                                float* __restrict__ out, float4* __restrict__ partial,
+                                                uint32_t* __restrict__ sat, float4* __restrict__ tmax) {
     const int tile = (int)d.x;
     const uint32_t begin = d.y, end = d.z;
     const uint32_t nchunks = d.w >> 16;
@@ -214,15 +271,16 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
     const float t_min = a.t_min;
     const bool track = (nchunks > 1) && (t_min > 0.f);
     uint32_t* my_sat = sat + (size_t)tile * 4;
-    // live slices (bit k): not yet saturated locally nor by an earlier chunk
+    [[maybe_unused]] uint32_t* my_tmax = reinterpret_cast<uint32_t*>(tmax + slot);
+    // slots of the earlier chunks: chunk 0 at `tile`, chunk j >= 1 at base + j - 1
+    [[maybe_unused]] const uint32_t base = slot - kk + 1;
+    const bool poll = track && kk > 0;
+    // live slices (bit k): not yet stopped
     uint32_t live = 0xfu;
-    if (track && kk > 0) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (0xffffffffu - ld_relaxed(my_sat + k) < kk) live &= ~(1u << k);
-        live = __builtin_amdgcn_readfirstlane(live);
-    }
-    float4* my = lds[wave];
+#ifdef GSR_COMP_BOUND
+    uint32_t prior[4];  // lane i < min(kk, 64): chunk i's published slice maxima (async)
+    if (poll) load_prior(tmax, (uint32_t)tile, base, kk, prior);
+#endif
 
     // Two-stage prefetch: the records of batch b+1 and the list indices of
     // batch b+2 are in flight while batch b is composited, so neither the
@@ -238,6 +296,31 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
         const uint32_t i2 = begin + kBatch + lane;
         if (i2 < end) idx_next = list[i2];
     }
+#ifdef GSR_COMP_BOUND
+    if (poll) {  // a chunk that starts behind saturated ones computes nothing
+        float B[4];
+        prior_bound(tmax, (uint32_t)tile, base, kk, prior, B);
+        uint32_t dead = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (B[k] < t_min) dead |= 1u << k;
+        dead = __builtin_amdgcn_readfirstlane(dead);
+        if (dead && lane == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (dead & (1u << k)) atomicMax(my_sat + k, 0xffffffffu - kk);
+        }
+        live &= ~dead;
+    }
+#else
+    if (poll) {  // slices an earlier chunk already saturated
+        uint32_t dead = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (0xffffffffu - ld_relaxed(my_sat + k) < kk) dead |= 1u << k;
+        live &= ~__builtin_amdgcn_readfirstlane(dead);
+    }
+#endif
     for (uint32_t b = begin; b < end && live; b += kBatch) {
         __builtin_amdgcn_wave_barrier();
         {
@@ -254,13 +337,17 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
             my[lane * 3 + 2] = f2;
         }
         __builtin_amdgcn_wave_barrier();
+#ifdef GSR_COMP_BOUND
+        // earlier chunks' published maxima, consumed after this batch
+        if (poll) load_prior(tmax, (uint32_t)tile, base, kk, prior);
+#else
         // saturation words of the other chunks, consumed after this batch
         uint32_t satw[4];
-        const bool poll = track && kk > 0;
         if (poll) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) satw[k] = ld_relaxed(my_sat + k);
         }
+#endif
         {  // prefetch: records of batch b+1, list indices of batch b+2
             const uint32_t i = b + kBatch + lane;
             if (i < end) {
@@ -336,27 +423,46 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
             }
         }
         if (t_min > 0.f) {
-            // a slice whose chunk-local T is below t_min everywhere is done
             uint32_t still = 0;
+#ifdef GSR_COMP_BOUND
+            if (track) {
+                // publish this chunk's slice maxima, then test bound * max against t_min
+                float m[4], B[4] = {1.f, 1.f, 1.f, 1.f};
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (__any(T[k] >= t_min)) still |= (1u << k);
-            const uint32_t newly = live & ~still;
-            if (track && newly) {
-                if (lane == 0) {
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        if (newly & (1u << k)) atomicMax(my_sat + k, 0xffffffffu - kk);
+                for (int k = 0; k < 4; ++k) m[k] = uniform_f(wave_max(T[k]));
+                if (lane < 4) {
+                    const float mine = lane == 0 ? m[0] : lane == 1 ? m[1] : lane == 2 ? m[2] : m[3];
+                    __hip_atomic_store(my_tmax + lane, __float_as_uint(mine), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
                 }
+                if (poll) prior_bound(tmax, (uint32_t)tile, base, kk, prior, B);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (B[k] * m[k] >= t_min) still |= 1u << k;
+            } else
+#endif
+            {
+                // stop a slice when every pixel's chunk-local T is below t_min
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (__any(T[k] >= t_min)) still |= 1u << k;
+            }
+            const uint32_t newly = live & ~still;
+            if (track && newly && lane == 0) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (newly & (1u << k)) atomicMax(my_sat + k, 0xffffffffu - kk);
             }
             live &= still;
+#ifndef GSR_COMP_BOUND
             if (poll && live) {
                 uint32_t dead = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    if (0xffffffffu - satw[k] < kk) dead |= (1u << k);
+                    if (0xffffffffu - satw[k] < kk) dead |= 1u << k;
                 live &= ~__builtin_amdgcn_readfirstlane(dead);
             }
+#endif
         }
     }
 
@@ -387,6 +493,43 @@ __global__ __launch_bounds__(kThreads) void k_composite(const uint4* __restrict_
             out[3 * pidx + 2] = b;
         }
     }
+}
+
+#ifdef GSR_COMP_TRACE
+// Tooling build only (tools/comp_trace.py): per-wave shader-clock stamps.
+__device__ uint4 g_comp_trace[2 * kTraceMax];
+#endif
+
+#ifdef GSR_COMP_WPE
+#define GSR_COMP_OCC __attribute__((amdgpu_waves_per_eu(GSR_COMP_WPE, 8)))
+#else
+#define GSR_COMP_OCC
+#endif
+template <int FRAG>
+__global__ __launch_bounds__(kThreads) GSR_COMP_OCC void k_composite(const uint4* __restrict__ desc,
+                                                        const uint32_t* __restrict__ n_chunks_dev,
+                                                        const uint32_t* __restrict__ list,
+                                                        const SplatRec* __restrict__ recs, CompositeArgs a,
+                                                        float* __restrict__ out, float4* __restrict__ partial,
+                                                        uint32_t* __restrict__ sat, float4* __restrict__ tmax) {
+    __shared__ float4 lds[kThreads / 64][kBatch * 3];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t slot = blockIdx.x * (kThreads / 64) + wave;
+    if (slot >= (uint32_t)a.num_tiles + n_chunks_dev[0]) return;  // device count of extra chunks
+#ifdef GSR_COMP_TRACE
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    const uint4 d = desc[slot];
+    composite_chunk<FRAG>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax);
+#ifdef GSR_COMP_TRACE
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (__lane_id() == 0 && slot < kTraceMax) {
+        const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));     // HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));   // XCC_ID
+        g_comp_trace[2 * slot] = make_uint4(slot, hw, d.z - d.y, xcc);
+        g_comp_trace[2 * slot + 1] = make_uint4((uint32_t)t0, (uint32_t)t1, (uint32_t)r0, (uint32_t)r1);
+    }
+#endif
 }
 
 // Fold the partial results of multi-chunk tiles in depth order: one block per
@@ -447,6 +590,16 @@ __global__ __launch_bounds__(kThreads) void k_merge(const uint32_t* __restrict__
 
 }  // namespace
 
+#ifdef GSR_COMP_TRACE
+// Copies the last composite launch's per-wave stamps to host memory (tooling).
+extern "C" int64_t gsr_debug_comp_trace(void* host_dst, int64_t max_entries) {
+    const int64_t n = max_entries < (int64_t)kTraceMax ? max_entries : (int64_t)kTraceMax;
+    if (hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(g_comp_trace), (size_t)n * 32, 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return n;
+}
+#endif
+
 size_t bin_tmp_elems(size_t n_vis) { return (n_vis + kBinBlock - 1) / kBinBlock + 1; }
 
 int launch_binning(const uint32_t* sorted_ids, const uint2* trect, uint32_t n_vis, int tiles_x, uint32_t* tmp,
@@ -484,13 +637,16 @@ static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float*
 }
 
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t* chunk_cnt, uint32_t* chunk_base,
-                  uint32_t* n_extra_dev, uint4* desc, hipStream_t s) {
+                  uint32_t* n_extra_dev, uint4* desc, float4* tmax, hipStream_t s) {
     const unsigned g = (unsigned)((num_tiles + kThreads - 1) / kThreads);
     k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_base);
     GSR_LAUNCH_CHECK("chunk_count");
     int rc = scan_exclusive(chunk_base, chunk_base, (size_t)num_tiles, nullptr, n_extra_dev, s);
     if (rc) return rc;
-    k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_cnt, chunk_base, desc);
+#ifndef GSR_COMP_BOUND
+    tmax = nullptr;  // the published maxima are only read by the bound variant
+#endif
+    k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_cnt, chunk_base, desc, tmax);
     GSR_LAUNCH_CHECK("chunk_write");
     return GSR_OK;
 }
@@ -498,24 +654,25 @@ int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t* 
 int launch_composite(const uint4* desc, const uint32_t* n_chunks_dev, uint32_t max_chunks, const uint32_t* chunk_cnt,
                      const uint32_t* chunk_base, uint32_t* sat, const uint32_t* tile_vals, const SplatRec* recs,
                      const FrameUniforms& u, int frag_class, float t_min, const float* bg, int out_layout, float* out,
-                     float4* partial, hipStream_t s) {
+                     float4* partial, float4* tmax, hipStream_t s) {
     const CompositeArgs a = make_args(u, t_min, bg, out_layout);
     const unsigned grid = (unsigned)((max_chunks + 3) / 4);
     switch (frag_class) {
         case kFragGauss:
-            k_composite<kFragGauss><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial, sat);
+            k_composite<kFragGauss><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial, sat,
+                                                              tmax);
             break;
         case kFragBillboard:
             k_composite<kFragBillboard><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial,
-                                                                  sat);
+                                                                  sat, tmax);
             break;
         case kFragFlatBall:
             k_composite<kFragFlatBall><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial,
-                                                                 sat);
+                                                                 sat, tmax);
             break;
         default:
             k_composite<kFragGaussBall><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial,
-                                                                  sat);
+                                                                  sat, tmax);
             break;
     }
     GSR_LAUNCH_CHECK("composite");
