@@ -102,7 +102,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from gsviewer_amd import _lib
-    from gsviewer_amd.camera import view_for_rank
+    from gsviewer_amd.multiview import broadcast_scene, timed_region, view_of
     from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into
 
     _lib.load()
@@ -114,29 +114,12 @@ def main():
 
     # ---- scene: generated on rank 0, broadcast once (RCCL over xGMI), untimed
     t_gen = time.perf_counter()
-    if rank == 0:
-        g, data_desc = make_scene(args.config, n, deg)
-        tensors = [torch.from_numpy(np.ascontiguousarray(getattr(g, f))).to(dev)
-                   for f in ("xyz", "rot", "scale", "opacity", "sh")]
-    else:
-        g, data_desc = None, None
-        tensors = [torch.empty(s, dtype=torch.float32, device=dev)
-                   for s in ((n, 3), (n, 4), (n, 3), (n, 1), (n, 3 * k_coef))]
+    g, data_desc = make_scene(args.config, n, deg) if rank == 0 else (None, None)
     t_gen = time.perf_counter() - t_gen
-    bcast = None
-    if world > 1:
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for t in tensors:
-            dist.broadcast(t, src=0)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        nbytes = sum(t.numel() * 4 for t in tensors)
-        bcast = dict(bytes=nbytes, seconds=dt, GBps=nbytes / dt / 1e9)
+    tensors, bcast = broadcast_scene(g, n, k_coef, dev)  # one RCCL broadcast at load (world > 1)
     scene = HipScene(*tensors)
     del tensors
-    cam = view_for_rank(H, W, rank)
+    cam = view_of(rank, H, W)
     camc = camera_from(cam)
     st = RenderSettings(t_min=args.t_min, out_layout=0)
     ctx = HipContext()
@@ -149,20 +132,8 @@ def main():
     if not args.no_profile:
         _lib.check(lib.gsr_context_set_profiling(ctx.handle, 1), "set_profiling")
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        render_into(ctx, scene, camc, st, out)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    # barrier + synchronize on both sides; MAX over ranks
+    elapsed = timed_region(lambda: render_into(ctx, scene, camc, st, out), args.steps, dev)
 
     stats = ctx.stats()
     # tile-list length distribution of the last frame (load balance of the compositor)

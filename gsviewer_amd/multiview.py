@@ -1,0 +1,104 @@
+"""Multi-GPU path: independent camera views, one process per GPU.
+
+SURVEY.md §8(e): the path shards over independent units (camera views).
+Every rank holds the whole scene and renders its own view, and nothing is
+exchanged per frame.  The only collective is ONE broadcast of the scene from
+rank 0 at load.  On MI355X the backend is "nccl" (RCCL over xGMI).  The CPU
+tests run the same code over gloo.
+
+bench.py and the world_size-2 gloo tests (tests/test_multiview_gloo.py) both
+use these helpers, so the tested code is the benchmarked code.
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .camera import Camera, view_for_rank
+
+SCENE_FIELDS = ("xyz", "rot", "scale", "opacity", "sh")
+
+
+def scene_shapes(n: int, k_coef: int) -> Tuple[Tuple[int, int], ...]:
+    """Shapes of the five scene tensors for n Gaussians with k_coef SH coefficients per channel."""
+    return ((n, 3), (n, 4), (n, 3), (n, 1), (n, 3 * k_coef))
+
+
+def broadcast_scene(g, n: int, k_coef: int, device, src: int = 0) -> Tuple[List[torch.Tensor], Optional[dict]]:
+    """Replicate the scene on every rank.
+
+    Rank `src` passes its GaussianData `g`; the other ranks pass None and
+    allocate receive buffers of the agreed shapes.  Returns the five float32
+    tensors on `device`, plus the broadcast's size/time (None when single-process).
+    """
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    if rank == src:
+        if g is None:
+            raise ValueError("broadcast_scene: the source rank must pass the scene")
+        tensors = [torch.from_numpy(np.ascontiguousarray(getattr(g, f), dtype=np.float32)).to(device)
+                   for f in SCENE_FIELDS]
+        for t, shp in zip(tensors, scene_shapes(n, k_coef)):
+            if tuple(t.shape) != shp:
+                raise ValueError(f"broadcast_scene: tensor shape {tuple(t.shape)} != expected {shp}")
+    else:
+        tensors = [torch.empty(shp, dtype=torch.float32, device=device) for shp in scene_shapes(n, k_coef)]
+    if world == 1:
+        return tensors, None
+    _sync(device)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for t in tensors:
+        dist.broadcast(t, src=src)
+    _sync(device)
+    dt = time.perf_counter() - t0
+    nbytes = sum(t.numel() * t.element_size() for t in tensors)
+    return tensors, dict(bytes=nbytes, seconds=dt, GBps=nbytes / max(dt, 1e-12) / 1e9)
+
+
+def view_of(rank: int, height: int, width: int) -> Camera:
+    """Camera of rank k: the default camera yawed by k*45 degrees."""
+    return view_for_rank(height, width, rank)
+
+
+def timed_region(step: Callable[[], None], steps: int, device) -> float:
+    """Time exactly `steps` calls of `step`.
+
+    The region is bracketed by a barrier and a device synchronize on both
+    sides.  Returns the MAX elapsed seconds over all ranks.
+    """
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    if world > 1:
+        dist.barrier()
+    _sync(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    _sync(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    return elapsed
+
+
+def gather_objects(obj, world: int) -> Sequence:
+    """All-gather a small picklable object (validation only, outside timed regions)."""
+    if world == 1:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def _sync(device) -> None:
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
