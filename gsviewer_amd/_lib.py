@@ -1,4 +1,5 @@
-"""ctypes binding of the C ABI in ``include/gsr.h`` (``gsviewer_amd/libgsr.so``).
+"""ctypes binding of the C ABI in ``include/gsr.h`` and ``include/gsr_io.h``
+(``gsviewer_amd/libgsr.so``).
 
 The shared library is the product: there is no Python or CPU fallback.  If it
 is missing or fails to load, every entry point raises ``RuntimeError``.
@@ -57,7 +58,31 @@ class GsrFrameStats(ctypes.Structure):
     ]
 
 
-# name -> (restype, argtypes); every symbol declared in include/gsr.h
+class GsrPlyInfo(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int64),
+        ("sh_dim", ctypes.c_int32),
+        ("format", ctypes.c_int32),
+        ("n_properties", ctypes.c_int32),
+        ("row_bytes", ctypes.c_int32),
+        ("body_offset", ctypes.c_int64),
+    ]
+
+
+class GsrBox(ctypes.Structure):
+    _fields_ = [
+        ("mode", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
+        ("cube_min", ctypes.c_double * 3),
+        ("cube_max", ctypes.c_double * 3),
+        ("rot_inv", ctypes.c_double * 9),
+    ]
+
+
+GSR_PLY_BINARY_LE, GSR_PLY_BINARY_BE, GSR_PLY_ASCII = 0, 1, 2
+GSR_BOX_NONE, GSR_BOX_AABB, GSR_BOX_OBB = 0, 1, 2
+
+# name -> (restype, argtypes); every symbol declared in include/gsr.h and include/gsr_io.h
 _P = ctypes.c_void_p
 SIGNATURES = {
     "gsr_abi_version": (ctypes.c_int, []),
@@ -77,6 +102,14 @@ SIGNATURES = {
     "gsr_debug_copy": (ctypes.c_int64, [_P, ctypes.c_int32, _P, ctypes.c_int64, _P]),
     "gsr_context_set_profiling": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gsr_context_stage_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+    # gsr_io.h
+    "gsr_ply_probe": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo)]),
+    "gsr_ply_read": (ctypes.c_int, [ctypes.c_char_p, _P, _P, _P, _P, _P, ctypes.c_int32]),
+    "gsr_ply_write_3dgs": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, _P, ctypes.c_int64, ctypes.c_int32]),
+    "gsr_points_center": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.POINTER(ctypes.c_float * 3), _P]),
+    "gsr_export_select": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_float * 3),
+                                         ctypes.POINTER(GsrBox), _P, ctypes.POINTER(ctypes.c_int64),
+                                         ctypes.POINTER(ctypes.c_float * 6), ctypes.POINTER(ctypes.c_int32), _P]),
 }
 
 STAGES = ["cull", "preprocess", "depth_sort", "binning", "tile_sort", "tile_ranges", "composite", "sync"]

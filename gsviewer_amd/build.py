@@ -21,7 +21,8 @@ BUILD = os.path.join(ROOT, "build", "gsr")
 LIB = os.path.join(PKG, "libgsr.so")
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["api.hip", "scene.hip", "scan.hip", "radix_sort.hip", "preprocess.hip", "composite.hip"]
+SOURCES = ["api.hip", "scene.hip", "scan.hip", "radix_sort.hip", "preprocess.hip", "composite.hip", "export.hip",
+           "ply.cpp"]
 # The per-Gaussian stage must evaluate exactly like the oracle: no contraction.
 EXTRA_FLAGS = {"preprocess.hip": ["-ffp-contract=off"]}
 
@@ -35,7 +36,8 @@ def hipcc():
 
 def _compile(src, debug, bdir=BUILD, defines=()):
     obj = os.path.join(bdir, os.path.basename(src) + ".o")
-    deps = [os.path.join(CSRC, src), os.path.join(CSRC, "gsr_internal.h"), os.path.join(INCLUDE, "gsr.h")]
+    deps = [os.path.join(CSRC, src), os.path.join(CSRC, "gsr_internal.h"), os.path.join(INCLUDE, "gsr.h"),
+            os.path.join(INCLUDE, "gsr_io.h")]
     if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in deps):
         return obj
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-c",

@@ -21,11 +21,19 @@ class GaussianData:
     opacity: np.ndarray
     sh: np.ndarray
     path: str | None = None
+    # positions as constructed (the reference keeps a copy of its original
+    # state, util_gau.py:18-36, and export_ply crops by it, :410-413)
+    original_xyz: np.ndarray | None = None
+
+    def __post_init__(self):
+        if self.original_xyz is None:
+            self.original_xyz = np.copy(self.xyz)
 
     def __len__(self):
         return len(self.xyz)
 
     def __getitem__(self, idx):
+        # a fresh instance whose original state is the current subset (util_gau.py:31-38)
         return GaussianData(self.xyz[idx], self.rot[idx], self.scale[idx], self.opacity[idx], self.sh[idx])
 
     def flat(self) -> np.ndarray:
@@ -74,7 +82,8 @@ class GaussianData:
 
     def astype32(self) -> "GaussianData":
         return GaussianData(*(np.ascontiguousarray(np.asarray(a, np.float32))
-                              for a in (self.xyz, self.rot, self.scale, self.opacity, self.sh)), path=self.path)
+                              for a in (self.xyz, self.rot, self.scale, self.opacity, self.sh)), path=self.path,
+                            original_xyz=self.original_xyz)
 
 
 def naive_gaussian() -> GaussianData:

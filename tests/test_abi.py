@@ -1,5 +1,5 @@
-"""The C-ABI library loads, exports every symbol include/gsr.h declares, and the
-ctypes struct layouts match the C header (no GPU calls)."""
+"""The C-ABI library loads, exports every symbol include/*.h declares, and the
+ctypes struct layouts match the C headers (no GPU calls)."""
 import ctypes
 import os
 import re
@@ -10,19 +10,23 @@ import pytest
 from gsviewer_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "gsr.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include")))
+           if h.endswith(".h")]
 
 
 def header_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(gsr_[a-z_]+)\s*\(", src)))
+    names = set()
+    for h in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(gsr_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_header_declares_expected_entry_points():
     names = header_functions()
     for must in ("gsr_scene_create", "gsr_scene_create_flat", "gsr_scene_destroy", "gsr_context_create",
-                 "gsr_render", "gsr_sort_depth", "gsr_last_error", "gsr_settings_default"):
+                 "gsr_render", "gsr_sort_depth", "gsr_last_error", "gsr_settings_default",
+                 "gsr_ply_probe", "gsr_ply_read", "gsr_ply_write_3dgs", "gsr_points_center", "gsr_export_select"):
         assert must in names
 
 
@@ -30,7 +34,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     missing = [n for n in header_functions() if not hasattr(lib, n)]
     assert not missing, missing
-    assert set(header_functions()) == set(_lib.SIGNATURES), "ctypes signatures out of sync with gsr.h"
+    assert set(header_functions()) == set(_lib.SIGNATURES), "ctypes signatures out of sync with include/*.h"
 
 
 def test_abi_version_and_defaults():
@@ -57,9 +61,11 @@ def test_struct_layout_matches_header(tmp_path):
     prog.write_text(r'''
 #include <stdio.h>
 #include <stddef.h>
-#include "gsr.h"
+#include "gsr_io.h"
 int main(void){
  printf("%zu %zu %zu\n", sizeof(gsr_camera), sizeof(gsr_settings), sizeof(gsr_frame_stats));
+ printf("%zu %zu %zu %zu\n", sizeof(gsr_ply_info), offsetof(gsr_ply_info, body_offset), sizeof(gsr_box),
+        offsetof(gsr_box, rot_inv));
  printf("%zu %zu %zu %zu\n", offsetof(gsr_settings, cube_rotation), offsetof(gsr_settings, bg),
         offsetof(gsr_settings, t_min), offsetof(gsr_settings, out_layout));
  printf("%zu %zu\n", offsetof(gsr_camera, hfovxy_focal), offsetof(gsr_camera, height));
@@ -69,6 +75,9 @@ int main(void){
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
     got = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
     S, C, FS = _lib.GsrSettings, _lib.GsrCamera, _lib.GsrFrameStats
-    want = [ctypes.sizeof(C), ctypes.sizeof(S), ctypes.sizeof(FS), S.cube_rotation.offset, S.bg.offset,
+    PI, B = _lib.GsrPlyInfo, _lib.GsrBox
+    want = [ctypes.sizeof(C), ctypes.sizeof(S), ctypes.sizeof(FS),
+            ctypes.sizeof(PI), PI.body_offset.offset, ctypes.sizeof(B), B.rot_inv.offset,
+            S.cube_rotation.offset, S.bg.offset,
             S.t_min.offset, S.out_layout.offset, C.hfovxy_focal.offset, C.height.offset]
     assert [int(x) for x in got] == want
