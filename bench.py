@@ -75,6 +75,31 @@ def cpu_baseline(g, cam, seconds):
                 ms_per_frame=1e3 * t_total / frames, sort_only_ms_1thread=1e3 * t_sort)
 
 
+# stage name -> kernel symbol in rocprofv3 summaries
+KERNEL_SYMBOL = {"composite": "k_composite<0>", "preprocess": "k_preprocess<3>", "cull": "k_cull", "merge": "k_merge"}
+PMC_PROFILE = os.path.join(ROOT, "profiles", "LATEST")
+
+
+def pmc_traffic(kernel, args):
+    """HBM bytes per launch of `kernel` (FETCH_SIZE, doubled per the gfx950
+    correction, + WRITE_SIZE) from the committed rocprofv3 --pmc summary of
+    this same bench command (profiles/<LATEST>/pmc_summary.csv, written by
+    tools/gpu_round.sh).  PMC collection needs its own profiler pass, so it is
+    read back here rather than measured inside the timed region."""
+    if kernel is None or args.config != "c2" or args.n or args.width or args.height:
+        return None
+    try:
+        d = open(PMC_PROFILE).read().strip()
+        path = os.path.join(ROOT, "profiles", d, "pmc_summary.csv")
+        rows = [ln.strip().split(",") for ln in open(path).read().splitlines()[1:]]
+    except OSError:
+        return None
+    got = {r[1]: float(r[4]) for r in rows if r[0].strip('"') == kernel}
+    if "FETCH_SIZE" not in got or "WRITE_SIZE" not in got:
+        return None
+    return got["FETCH_SIZE"] + got["WRITE_SIZE"], f"profiles/{d}/pmc_summary.csv ({kernel})"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -149,7 +174,7 @@ def main():
     stats["tile_len_mean"] = float(lens.mean())
     stage = {}
     if not args.no_profile:
-        ms = (ctypes.c_double * 8)()
+        ms = (ctypes.c_double * len(_lib.STAGES))()
         frames = ctypes.c_int64()
         _lib.check(lib.gsr_context_stage_times(ctx.handle, ms, ctypes.byref(frames)), "stage_times")
         stage = {name: ms[i] / max(frames.value, 1) for i, name in enumerate(_lib.STAGES)}
@@ -181,12 +206,17 @@ def main():
             "tile_sort": inst * 8 * 2 * 2 + inst * 4 * 2,
             "binning": nvis * (4 + 16 + 4 + 4 + 4) + inst * 8,
             "tile_ranges": inst * 4 * 2 + ntiles * 8,
+            "merge": stats.get("n_chunks_multi", 0) * 256 * 16 + W * H * 12,
         }[dom]
         achieved = alg / (stage[dom] * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg,
-                "ms_per_launch": stage[dom],
+                "ms_per_launch": stage[dom], "traffic_source": None,
                 "frame": {"bytes": b_frame, "GBps": b_frame * fps / 1e9, "frac": b_frame * fps / 1e9 / HBM_PEAK_GBS}}
+
+        traffic = pmc_traffic(KERNEL_SYMBOL.get(dom), args)
+        if traffic:
+            roof["traffic"], roof["traffic_source"] = traffic
 
     cpu = None
     if not args.no_cpu_baseline and world == 1 and g is not None:

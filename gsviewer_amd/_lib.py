@@ -112,11 +112,11 @@ SIGNATURES = {
                                          ctypes.POINTER(ctypes.c_float * 6), ctypes.POINTER(ctypes.c_int32), _P]),
 }
 
-STAGES = ["cull", "preprocess", "depth_sort", "binning", "tile_sort", "tile_ranges", "composite", "sync"]
+STAGES = ["cull", "preprocess", "depth_sort", "binning", "tile_sort", "tile_ranges", "composite", "sync", "merge"]
 
 GSR_DEBUG_RECORDS, GSR_DEBUG_DEPTH_ORDER, GSR_DEBUG_TILE_RANGES, GSR_DEBUG_TILE_LIST = 0, 1, 2, 3
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lib = None
 _lock = threading.Lock()

@@ -87,7 +87,7 @@ struct gsr_context {
     const uint2* last_ranges = nullptr;
     // profiling: 10 events per frame, two frames in flight
     bool prof_on = false;
-    hipEvent_t ev[2][11] = {};
+    hipEvent_t ev[2][12] = {};
     bool ev_pending[2] = {false, false};
     int64_t frame_idx = 0;
     double acc_ms[GSR_NUM_STAGES] = {};
@@ -195,10 +195,9 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
 }
 
 // Event slots: 0 start | cull+scan | 1 | preprocess | 2 ~sync~ 3 | depth sort | 4 |
-// counts+scan | 5 ~sync~ 6 | instance write | 7 | tile sort | 8 | ranges | 9 | composite | (end = slot 0 of next)
-// We record the end of the composite in slot [9] and the ranges end in [8] etc.
+// counts+scan | 5 ~sync~ 6 | instance write | 7 | tile sort | 8 | ranges | 9 | composite | 10 | merge | 11
 enum { EV_START = 0, EV_CULL, EV_PRE, EV_AFTER_SYNC1, EV_DSORT, EV_COUNTS, EV_AFTER_SYNC2, EV_DUPW, EV_TSORT,
-       EV_RANGES_END_COMPOSITE_START, EV_COUNT };
+       EV_RANGES_END_COMPOSITE_START, EV_COMPOSITE, EV_COUNT };
 
 int prof_record(gsr_context* c, int slot, int ev, hipStream_t s) {
     if (!c->prof_on) return GSR_OK;
@@ -223,7 +222,8 @@ void prof_accumulate(gsr_context* c, int slot, bool wait) {
     c->acc_ms[GSR_STAGE_BINNING] += el(EV_DSORT, EV_COUNTS) + el(EV_AFTER_SYNC2, EV_DUPW);
     c->acc_ms[GSR_STAGE_TILE_SORT] += el(EV_DUPW, EV_TSORT);
     c->acc_ms[GSR_STAGE_RANGES] += el(EV_TSORT, EV_RANGES_END_COMPOSITE_START);
-    c->acc_ms[GSR_STAGE_COMPOSITE] += el(EV_RANGES_END_COMPOSITE_START, EV_COUNT);
+    c->acc_ms[GSR_STAGE_COMPOSITE] += el(EV_RANGES_END_COMPOSITE_START, EV_COMPOSITE);
+    c->acc_ms[GSR_STAGE_MERGE] += el(EV_COMPOSITE, EV_COUNT);
     c->prof_frames += 1;
     c->ev_pending[slot] = false;
 }
@@ -454,6 +454,10 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
     if ((rc = launch_composite(c->chunk_desc.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
                                sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), st->t_min, st->bg,
                                st->out_layout, out, c->partial.p, c->tmax.p, s)))
+        return rc;
+    if ((rc = prof_record(c, slot, EV_COMPOSITE, s))) return rc;
+    if ((rc = launch_merge(c->chunk_cnt.p, c->chunk_base.p, c->partial.p, sat, u, st->t_min, st->bg, st->out_layout,
+                           out, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_COUNT, s))) return rc;
     if (c->prof_on) c->ev_pending[slot] = true;

@@ -676,6 +676,12 @@ int launch_composite(const uint4* desc, const uint32_t* n_chunks_dev, uint32_t m
             break;
     }
     GSR_LAUNCH_CHECK("composite");
+    return GSR_OK;
+}
+
+int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const float4* partial, const uint32_t* sat,
+                 const FrameUniforms& u, float t_min, const float* bg, int out_layout, float* out, hipStream_t s) {
+    const CompositeArgs a = make_args(u, t_min, bg, out_layout);
     k_merge<<<(unsigned)a.num_tiles, kThreads, 0, s>>>(chunk_cnt, chunk_base, partial, sat, a, out);
     GSR_LAUNCH_CHECK("merge");
     return GSR_OK;

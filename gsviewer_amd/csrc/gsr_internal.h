@@ -170,6 +170,9 @@ int launch_composite(const uint4* desc, const uint32_t* n_chunks_dev, uint32_t m
                      const uint32_t* tile_vals, const SplatRec* recs, const FrameUniforms& u,
                      int frag_class, float t_min, const float* bg, int out_layout, float* out,
                      float4* partial, float4* tmax, hipStream_t s);
+// k_merge: folds the partials of multi-chunk tiles into `out` (after launch_composite)
+int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const float4* partial, const uint32_t* sat,
+                 const FrameUniforms& u, float t_min, const float* bg, int out_layout, float* out, hipStream_t s);
 
 }  // namespace gsr
 

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 1
+#define GSR_ABI_VERSION 2
 
 typedef enum gsr_status {
     GSR_OK = 0,
@@ -150,7 +150,7 @@ int gsr_sort_depth(gsr_context* ctx, const gsr_scene* scene, const float view[16
  * `sync` = GPU idle time while the host reads the visible/instance counts. */
 enum { GSR_STAGE_CULL = 0, GSR_STAGE_PREPROCESS = 1, GSR_STAGE_DEPTH_SORT = 2, GSR_STAGE_BINNING = 3,
        GSR_STAGE_TILE_SORT = 4, GSR_STAGE_RANGES = 5, GSR_STAGE_COMPOSITE = 6, GSR_STAGE_SYNC = 7,
-       GSR_NUM_STAGES = 8 };
+       GSR_STAGE_MERGE = 8, GSR_NUM_STAGES = 9 };
 int gsr_context_set_profiling(gsr_context* ctx, int32_t enable);   /* resets the accumulators */
 /* Sum of per-stage milliseconds over the profiled frames since the last reset
  * (waits for the last profiled frame's events). */
