@@ -154,11 +154,16 @@ def main():
     for _ in range(args.warmup):
         render_into(ctx, scene, camc, st, out)
     torch.cuda.synchronize()
+
+    # barrier + synchronize on both sides; MAX over ranks.  No instrumentation
+    # inside: every HIP event record stalls the stream for several us.
+    elapsed = timed_region(lambda: render_into(ctx, scene, camc, st, out), args.steps, dev)
+
+    # Per-stage times: a second region of the same frames with libgsr's HIP
+    # events recorded on the render stream between the stages.
     if not args.no_profile:
         _lib.check(lib.gsr_context_set_profiling(ctx.handle, 1), "set_profiling")
-
-    # barrier + synchronize on both sides; MAX over ranks
-    elapsed = timed_region(lambda: render_into(ctx, scene, camc, st, out), args.steps, dev)
+        prof_elapsed = timed_region(lambda: render_into(ctx, scene, camc, st, out), args.steps, dev)
 
     stats = ctx.stats()
     # tile-list length distribution of the last frame (load balance of the compositor)
@@ -178,6 +183,7 @@ def main():
         frames = ctypes.c_int64()
         _lib.check(lib.gsr_context_stage_times(ctx.handle, ms, ctypes.byref(frames)), "stage_times")
         stage = {name: ms[i] / max(frames.value, 1) for i, name in enumerate(_lib.STAGES)}
+        stage["instrumented_ms_per_frame"] = 1e3 * prof_elapsed / args.steps
 
     if rank != 0:
         if world > 1:
@@ -192,7 +198,7 @@ def main():
 
     roof = None
     if stage:
-        kernels = {k: v for k, v in stage.items() if k != "sync"}
+        kernels = {k: v for k, v in stage.items() if k not in ("sync", "instrumented_ms_per_frame")}
         dom = max(kernels, key=kernels.get)
         inst = stats["n_instances"]
         ntiles = stats["tiles_x"] * stats["tiles_y"]

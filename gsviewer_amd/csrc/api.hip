@@ -4,15 +4,16 @@
 //   memset(per-frame zero block: counters, radix totals, tile ranges, saturation words)
 //   k_cull(N) -> scan(N/64 wave counts; total = V on device)
 //   k_preprocess(N): records, depth keys, tile rects; D accumulated on device
-//   async copy (V, D) -> pinned host, event
-//   depth radix sort (grid sized by N, count V read on device), 4 x 8-bit passes
-//   [host waits for the (V, D) event while the GPU runs the depth sort]
+//   (the last preprocess block stores (V, D, seq) to host-mapped memory)
+//   depth radix sort (grid sized by N, count V and key range read on device), 3 passes
+//   [host polls for (V, D, seq) while the GPU runs the depth sort]
 //   binning (reduce, scan, fused scan+write) -> stable tile radix sort over D
 //   k_tile_ranges -> chunk count / scan / write -> k_composite(chunks) -> k_merge
 // The only host wait overlaps GPU work, so no stage of the frame idles.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -64,6 +65,7 @@ struct DevBuf {
 struct gsr_context {
     gsr::DevBuf<uint64_t> vis_mask;
     gsr::DevBuf<uint32_t> wave_counts;
+    gsr::DevBuf<uint2> block_ranges;                        // per cull block: depth-key range
     gsr::DevBuf<uint32_t> scan_tmp;
     gsr::DevBuf<gsr::SplatRec> recs;
     gsr::DevBuf<uint32_t> keys_a, keys_b, vals_a, vals_b;   // depth sort (capacity N)
@@ -77,8 +79,10 @@ struct gsr_context {
     gsr::DevBuf<float4> partial;                  // per chunk x 256 px (multi-chunk tiles)
     gsr::DevBuf<float4> tmax;                     // per chunk: published slice maxima of local T
     uint32_t chunk = 192;                         // instances per compositing chunk (swept: 128-192 best)
-    uint32_t* host_counters = nullptr;  // pinned
-    hipEvent_t counts_ready = nullptr;
+    uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
+    uint32_t seq = 0;                       // frame sequence number the host waits for
+    uint32_t* host_counters_dev = nullptr;  // its device address
+    gsr::DevBuf<unsigned long long> done_ctr;  // preprocess completion + instance count (self re-arming)
     gsr_frame_stats stats{};
     // last frame's result arrays (for gsr_debug_copy)
     const uint32_t* last_depth_order = nullptr;
@@ -152,18 +156,26 @@ int build_uniforms(const gsr_scene* sc, const gsr_camera* cam, const gsr_setting
     return GSR_OK;
 }
 
+constexpr int kDepthPasses = 3;  // 32-bit depth keys: 3 passes of <= 11 bits (width chosen on the device)
+
 int bits_for(uint32_t v) {  // bits needed to represent values < v
     int b = 0;
     while (b < 32 && (1ull << b) < v) ++b;
     return b;
 }
 
-// Per-frame zero block (one memset): [0,4) counters {V, D, extra chunks, -},
-// [4, 4+2048) radix digit totals (depth passes, tile passes), then tile
-// ranges (uint2, 16-B aligned) and saturation words (4 per tile).
+// Per-frame scratch block: [0,4) counters {V, D, extra chunks, -} are
+// overwritten every frame; from `cleared` on, the depth-key range
+// {~kmin, kmax}, the radix digit totals (depth sort, tile sort), the tile
+// ranges (uint2, 16-B aligned) and the saturation words (4 per tile) are
+// zeroed by k_cull.
 struct ZeroLayout {
-    size_t counters = 0, totals_depth = 4, totals_tile = 4 + 1024, ranges = 2064, sat = 0, total = 0;
+    size_t counters = 0, cleared = 4, key_range = 4, totals_depth = 8, totals_tile = 0, ranges = 0, sat = 0,
+           total = 0;
     explicit ZeroLayout(int num_tiles) {
+        const size_t tot = radix_totals_elems();
+        totals_tile = totals_depth + tot;
+        ranges = (totals_tile + tot + 3) & ~(size_t)3;
         sat = ranges + 2 * (size_t)num_tiles;
         total = sat + 4 * (size_t)num_tiles;
     }
@@ -174,6 +186,7 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
     int rc;
     if ((rc = c->vis_mask.ensure(nw, "vis_mask"))) return rc;
     if ((rc = c->wave_counts.ensure(nw, "wave_counts"))) return rc;
+    if ((rc = c->block_ranges.ensure(n / kCullBlock + 1, "block_ranges"))) return rc;
     const size_t scan_need = std::max(scan_tmp_elems(nw), scan_tmp_elems(n));
     if ((rc = c->scan_tmp.ensure(scan_need, "scan_tmp"))) return rc;
     if ((rc = c->recs.ensure(n, "recs"))) return rc;
@@ -184,12 +197,18 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
     if ((rc = c->trect.ensure(n, "trect"))) return rc;
     if ((rc = c->bin_tmp.ensure(bin_tmp_elems(n), "bin_tmp"))) return rc;
     if ((rc = c->radix_tmp.ensure(radix_tmp_elems(n), "radix_tmp"))) return rc;
-    if (!c->counts_ready) GSR_HIP_CHECK(hipEventCreateWithFlags(&c->counts_ready, hipEventDisableTiming));
+    if (!c->done_ctr.p) {
+        if ((rc = c->done_ctr.ensure(1, "done_ctr"))) return rc;
+        GSR_HIP_CHECK(hipMemset(c->done_ctr.p, 0, c->done_ctr.cap * sizeof(unsigned long long)));
+    }
     if (!c->host_counters) {
-        if (hipHostMalloc(&c->host_counters, 4 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+        if (hipHostMalloc(&c->host_counters, 4 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess) {
             c->host_counters = nullptr;
             return set_error(GSR_ERR_NOMEM, "context: hipHostMalloc failed");
         }
+        std::memset(c->host_counters, 0, 4 * sizeof(uint32_t));
+        GSR_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->host_counters_dev), c->host_counters, 0));
     }
     return GSR_OK;
 }
@@ -226,6 +245,41 @@ void prof_accumulate(gsr_context* c, int slot, bool wait) {
     c->acc_ms[GSR_STAGE_MERGE] += el(EV_COMPOSITE, EV_COUNT);
     c->prof_frames += 1;
     c->ev_pending[slot] = false;
+}
+
+// Stable sort of (key, val) pairs; totals = digit-total scratch.
+int sort_pairs(gsr_context* c, uint32_t** ka, uint32_t** va, uint32_t** kb, uint32_t** vb, bool ident, size_t n,
+               const uint32_t* n_dev, int bits, int passes, const uint32_t* key_range, uint32_t* totals,
+               hipStream_t s) {
+    return radix_sort_pairs(ka, va, kb, vb, ident, n, n_dev, bits, passes, key_range, c->radix_tmp.p, totals, s);
+}
+
+// Wait until the last preprocess block has stored this frame's (V, D, seq) to
+// host-mapped memory.  Polling the sequence number needs no event record in
+// the stream (each one stalls the GPU for several microseconds).  Only after
+// a spin far longer than any frame is the stream queried (a query may itself
+// enqueue a marker, i.e. a stall): a stream that stopped making progress (a
+// fault) is then synchronised, which reports the error.
+int wait_counts(gsr_context* c, hipStream_t s) {
+    const uint32_t want = c->seq;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 0;; ++spin) {
+        if (__atomic_load_n(&c->host_counters[2], __ATOMIC_ACQUIRE) == want) return GSR_OK;
+        if ((spin & 4095) == 4095 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess) {  // stream drained: the store must be visible now
+                if (__atomic_load_n(&c->host_counters[2], __ATOMIC_ACQUIRE) == want) return GSR_OK;
+                return set_error(GSR_ERR_HIP, "render: frame counters were not published");
+            }
+            if (q != hipErrorNotReady) {
+                GSR_HIP_CHECK(hipStreamSynchronize(s));
+                return set_error(GSR_ERR_HIP, std::string("render: stream error ") + hipGetErrorString(q));
+            }
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
 }
 
 }  // namespace
@@ -338,12 +392,14 @@ int gsr_context_destroy(gsr_context* c) {
     if (!c) return GSR_OK;
     (void)hipDeviceSynchronize();
     c->vis_mask.release(); c->wave_counts.release(); c->scan_tmp.release(); c->recs.release();
+    c->block_ranges.release();
     c->keys_a.release(); c->keys_b.release(); c->vals_a.release(); c->vals_b.release();
     c->trect.release(); c->bin_tmp.release(); c->tkeys_a.release(); c->tkeys_b.release(); c->tvals_a.release();
     c->tvals_b.release(); c->radix_tmp.release(); c->zero.release();
     c->chunk_cnt.release(); c->chunk_base.release();
-    if (c->counts_ready) (void)hipEventDestroy(c->counts_ready); c->chunk_desc.release(); c->partial.release();
+    c->chunk_desc.release(); c->partial.release();
     c->tmax.release();
+    c->done_ctr.release();
     if (c->host_counters) (void)hipHostFree(c->host_counters);
     for (auto& row : c->ev)
         for (auto& e : row)
@@ -385,32 +441,38 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
     c->last_ranges = ranges;
 
     if ((rc = prof_record(c, slot, EV_START, s))) return rc;
-    GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * zl.total, s));
+    if (n == 0) GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * zl.total, s));
     if (n > 0) {
         const size_t nw = (n + 63) / 64;
-        if ((rc = launch_cull(sc->d, u, c->vis_mask.p, c->wave_counts.p, s))) return rc;
-        if ((rc = scan_exclusive(c->wave_counts.p, c->wave_counts.p, nw, c->scan_tmp.p, counters + 0, s))) return rc;
+        // k_cull clears the tile ranges and saturation words; every other word
+        // of the zero block is overwritten (not accumulated) before it is read
+        if ((rc = launch_cull(sc->d, u, c->vis_mask.p, c->wave_counts.p, c->block_ranges.p, c->zero.p + zl.cleared,
+                              (uint32_t)(zl.total - zl.cleared), s)))
+            return rc;
+        // visible-compaction offsets + V, and the frame's depth-key range
+        if ((rc = scan_exclusive(c->wave_counts.p, c->wave_counts.p, nw, c->scan_tmp.p, counters + 0, s,
+                                 c->block_ranges.p, (n + kCullBlock - 1) / kCullBlock, c->zero.p + zl.key_range)))
+            return rc;
     }
     if ((rc = prof_record(c, slot, EV_CULL, s))) return rc;
     if (n > 0 && (rc = launch_preprocess(sc->d, u, c->vis_mask.p, c->wave_counts.p, counters + 0, c->recs.p,
-                                         c->keys_a.p, c->trect.p, counters + 1, radii, s)))
+                                         c->keys_a.p, c->trect.p, counters, c->done_ctr.p, c->host_counters_dev,
+                                         ++c->seq, radii, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_PRE, s))) return rc;
-    GSR_HIP_CHECK(hipMemcpyAsync(c->host_counters, counters, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    GSR_HIP_CHECK(hipEventRecord(c->counts_ready, s));
     if ((rc = prof_record(c, slot, EV_AFTER_SYNC1, s))) return rc;
 
     // depth sort over the upper bound N; the device count V bounds the work
     uint32_t *ka = c->keys_a.p, *kb = c->keys_b.p, *va = c->vals_a.p, *vb = c->vals_b.p;
-    if (n > 0 && (rc = radix_sort_pairs(&ka, &va, &kb, &vb, true, n, counters + 0, 0, 32, c->radix_tmp.p,
-                                        c->zero.p + zl.totals_depth, s)))
+    if (n > 0 && (rc = sort_pairs(c, &ka, &va, &kb, &vb, true, n, counters + 0, 32, kDepthPasses,
+                                  c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_DSORT, s))) return rc;
 
     // host: V and D (the GPU is busy with the depth sort meanwhile)
-    GSR_HIP_CHECK(hipEventSynchronize(c->counts_ready));
-    const uint32_t n_vis = n > 0 ? c->host_counters[0] : 0u;
-    const uint32_t n_dup = n > 0 ? c->host_counters[1] : 0u;
+    if (n > 0 && (rc = wait_counts(c, s))) return rc;
+    const uint32_t n_vis = n > 0 ? __atomic_load_n(&c->host_counters[0], __ATOMIC_ACQUIRE) : 0u;
+    const uint32_t n_dup = n > 0 ? __atomic_load_n(&c->host_counters[1], __ATOMIC_ACQUIRE) : 0u;
     if (c->prof_on) prof_accumulate(c, slot ^ 1, false);
     if (n_vis > 0) c->last_depth_order = va;
 
@@ -431,8 +493,8 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
     uint32_t *tka = c->tkeys_a.p, *tkb = c->tkeys_b.p, *tva = c->tvals_a.p, *tvb = c->tvals_b.p;
     if (n_dup > 0) {
         const int tbits = bits_for((uint32_t)num_tiles);
-        if (tbits > 0 && (rc = radix_sort_pairs(&tka, &tva, &tkb, &tvb, false, n_dup, nullptr, 0, tbits,
-                                                c->radix_tmp.p, c->zero.p + zl.totals_tile, s)))
+        if (tbits > 0 && (rc = sort_pairs(c, &tka, &tva, &tkb, &tvb, false, n_dup, nullptr, tbits,
+                                          radix_passes_for(tbits), nullptr, c->zero.p + zl.totals_tile, s)))
             return rc;
         tile_list = tva;
         c->last_tile_list = tva;
@@ -442,7 +504,7 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
 
     // compositing chunks: at most one per tile plus one per `chunk` instances
     const size_t max_chunks = (size_t)num_tiles + n_dup / c->chunk + 1;
-    if ((rc = c->chunk_cnt.ensure((size_t)num_tiles, "chunk_cnt"))) return rc;
+    if ((rc = c->chunk_cnt.ensure((size_t)num_tiles + (size_t)num_tiles / 256 + 1, "chunk_cnt"))) return rc;
     if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
     if ((rc = c->chunk_desc.ensure(max_chunks, "chunk_desc"))) return rc;
     if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
@@ -505,6 +567,25 @@ int64_t gsr_debug_copy(const gsr_context* c, int32_t what, void* dst, int64_t ma
     return bytes;
 }
 
+int gsr_debug_sort_pairs(gsr_context* c, const uint32_t* keys_dev, int64_t n, int32_t bits, int32_t passes,
+                         uint32_t* keys_out_dev, uint32_t* vals_out_dev, void* stream) {
+    if (!c || !keys_dev || !keys_out_dev || !vals_out_dev || n < 0) return set_error(GSR_ERR_INVALID, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) return GSR_OK;
+    const size_t un = (size_t)n;
+    int rc = ensure_scene_buffers(c, un);
+    if (rc) return rc;
+    if ((rc = c->zero.ensure(ZeroLayout(0).total, "zero block"))) return rc;
+    GSR_HIP_CHECK(hipMemcpyAsync(c->keys_a.p, keys_dev, un * 4, hipMemcpyDeviceToDevice, s));
+    uint32_t *ka = c->keys_a.p, *kb = c->keys_b.p, *va = c->vals_a.p, *vb = c->vals_b.p;
+    if ((rc = sort_pairs(c, &ka, &va, &kb, &vb, true, un, nullptr, bits, passes, nullptr,
+                         c->zero.p + ZeroLayout(0).totals_depth, s)))
+        return rc;
+    GSR_HIP_CHECK(hipMemcpyAsync(keys_out_dev, ka, un * 4, hipMemcpyDeviceToDevice, s));
+    GSR_HIP_CHECK(hipMemcpyAsync(vals_out_dev, va, un * 4, hipMemcpyDeviceToDevice, s));
+    return GSR_OK;
+}
+
 int gsr_sort_depth(gsr_context* c, const gsr_scene* sc, const float view[16], int32_t* index_dev, void* stream) {
     if (!c || !sc || !view || !index_dev) return set_error(GSR_ERR_INVALID, "null argument");
     hipStream_t s = (hipStream_t)stream;
@@ -516,8 +597,8 @@ int gsr_sort_depth(gsr_context* c, const gsr_scene* sc, const float view[16], in
     GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * ZeroLayout(0).total, s));
     if ((rc = launch_depth_keys_all(sc->d, view, c->keys_a.p, s))) return rc;
     uint32_t *ka = c->keys_a.p, *kb = c->keys_b.p, *va = c->vals_a.p, *vb = c->vals_b.p;
-    if ((rc = radix_sort_pairs(&ka, &va, &kb, &vb, true, n, nullptr, 0, 32, c->radix_tmp.p,
-                               c->zero.p + ZeroLayout(0).totals_depth, s)))
+    if ((rc = sort_pairs(c, &ka, &va, &kb, &vb, true, n, nullptr, 32, kDepthPasses, nullptr,
+                         c->zero.p + ZeroLayout(0).totals_depth, s)))
         return rc;
     GSR_HIP_CHECK(hipMemcpyAsync(index_dev, va, n * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     return GSR_OK;

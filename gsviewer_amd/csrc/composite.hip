@@ -41,7 +41,10 @@ __global__ __launch_bounds__(kThreads) void k_bin_reduce(const uint32_t* __restr
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
         const uint32_t r = base + k * kThreads;
-        if (r < n_vis) s += rect_tiles(trect[sorted_ids[r]]);
+        if (r < n_vis) {
+            const uint32_t id = sorted_ids[r];
+            s += id < n_vis ? rect_tiles(trect[id]) : 0u;  // (ids are < n_vis by construction)
+        }
     }
     s = wave_reduce_sum(s);
     if (__lane_id() == 0) lds[threadIdx.x >> 6] = s;
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_write(const uint32_t* __restri
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
-        tr[k] = (base + k < n_vis) ? trect[id[k]] : make_uint2(0xffffu, 0u);
+        tr[k] = (base + k < n_vis && id[k] < n_vis) ? trect[id[k]] : make_uint2(0xffffu, 0u);
         s += rect_tiles(tr[k]);
     }
     const int w = threadIdx.x >> 6;
@@ -130,29 +133,53 @@ __device__ __forceinline__ uint32_t chunks_of(uint2 r, uint32_t chunk) {
     return len == 0 ? 1u : (len + chunk - 1) / chunk;
 }
 
+// Chunk descriptors in two parallel launches (one thread per tile):
+// k_chunk_count writes each block's total of extra chunks (beyond the first
+// per tile); k_chunk_write takes its block's offset as the sum of the earlier
+// block totals (a few dozen at 1080p), scans its tiles' extra chunks and
+// writes the descriptors (tile, begin, end, count << 16 | index).
 __global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restrict__ ranges, int num_tiles,
-                                                          uint32_t chunk, uint32_t* __restrict__ extra) {
+                                                          uint32_t chunk, uint32_t* __restrict__ block_extra) {
+    __shared__ uint32_t lds[kThreads / 64];
     const int t = blockIdx.x * kThreads + threadIdx.x;
-    if (t < num_tiles) extra[t] = chunks_of(ranges[t], chunk) - 1u;
+    uint32_t e = t < num_tiles ? chunks_of(ranges[t], chunk) - 1u : 0u;
+    e = wave_reduce_sum(e);
+    if (__lane_id() == 0) lds[threadIdx.x >> 6] = e;
+    __syncthreads();
+    if (threadIdx.x == 0) block_extra[blockIdx.x] = lds[0] + lds[1] + lds[2] + lds[3];
 }
 
-// extra_off = exclusive scan of extra (chunks beyond the first), in place.
 __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restrict__ ranges, int num_tiles,
-                                                          uint32_t chunk, uint32_t* __restrict__ chunk_cnt,
+                                                          uint32_t chunk, const uint32_t* __restrict__ block_extra,
+                                                          uint32_t* __restrict__ chunk_cnt,
                                                           uint32_t* __restrict__ chunk_base,
+                                                          uint32_t* __restrict__ n_extra_dev,
                                                           uint4* __restrict__ desc, float4* __restrict__ tmax) {
+    __shared__ uint32_t lds[kThreads / 64];
+    __shared__ uint32_t s_prefix;
     const int t = blockIdx.x * kThreads + threadIdx.x;
-    if (t >= num_tiles) return;
-    const uint2 r = ranges[t];
+    if (threadIdx.x < 64) {  // wave 0: offset of this block = sum of the earlier blocks' totals
+        uint32_t p = 0;
+        for (uint32_t b = __lane_id(); b < blockIdx.x; b += 64) p += block_extra[b];
+        p = wave_reduce_sum(p);
+        if (__lane_id() == 0) s_prefix = p;
+    }
+    const uint2 r = t < num_tiles ? ranges[t] : make_uint2(0u, 0u);
     const uint32_t cnt = chunks_of(r, chunk);
-    const uint32_t base = (uint32_t)num_tiles + chunk_base[t];  // chunk_base holds extra_off on entry
+    const uint32_t mine = t < num_tiles ? cnt - 1u : 0u;
+    uint32_t total;
+    const uint32_t excl = block_exclusive<kThreads>(mine, lds, total);  // (its barrier also publishes s_prefix)
+    const uint32_t extra = s_prefix + excl;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_extra_dev = s_prefix + total;
+    if (t >= num_tiles) return;
+    const uint32_t base = (uint32_t)num_tiles + extra;
     chunk_cnt[t] = cnt;
     chunk_base[t] = base;
-    for (uint32_t k = 0; k < cnt; ++k) {
-        const uint32_t b = r.x + k * chunk;
+    for (uint32_t j = 0; j < cnt; ++j) {
+        const uint32_t b = r.x + j * chunk;
         const uint32_t e = min(r.y, b + chunk);
-        const uint32_t slot = k == 0 ? (uint32_t)t : base + k - 1;
-        desc[slot] = make_uint4((uint32_t)t, b, e, (cnt << 16) | k);
+        const uint32_t slot = j == 0 ? (uint32_t)t : base + j - 1;
+        desc[slot] = make_uint4((uint32_t)t, b, e, (cnt << 16) | j);
         if (tmax && cnt > 1) tmax[slot] = make_float4(1.f, 1.f, 1.f, 1.f);  // nothing composited yet
     }
 }
@@ -544,7 +571,7 @@ __global__ __launch_bounds__(kThreads) void k_merge(const uint32_t* __restrict__
     if (cnt <= 1) return;
     const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = __lane_id();
-    const uint32_t last = min(cnt - 1, 0xffffffffu - sat[tile * 4 + k]);
+    const uint32_t last = min(cnt - 1, 0xffffffffu - ld_relaxed(sat + tile * 4 + k));  // written by atomics
     const uint32_t base = chunk_base[tile];
     float r = 0.f, g = 0.f, b = 0.f, T = 1.f;
     constexpr int kDepth = 8;
@@ -638,15 +665,15 @@ static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float*
 
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t* chunk_cnt, uint32_t* chunk_base,
                   uint32_t* n_extra_dev, uint4* desc, float4* tmax, hipStream_t s) {
-    const unsigned g = (unsigned)((num_tiles + kThreads - 1) / kThreads);
-    k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_base);
-    GSR_LAUNCH_CHECK("chunk_count");
-    int rc = scan_exclusive(chunk_base, chunk_base, (size_t)num_tiles, nullptr, n_extra_dev, s);
-    if (rc) return rc;
 #ifndef GSR_COMP_BOUND
     tmax = nullptr;  // the published maxima are only read by the bound variant
 #endif
-    k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_cnt, chunk_base, desc, tmax);
+    const unsigned g = (unsigned)((num_tiles + kThreads - 1) / kThreads);
+    // the per-block totals live in chunk_cnt past its num_tiles entries
+    k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_cnt + num_tiles);
+    GSR_LAUNCH_CHECK("chunk_count");
+    k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_cnt + num_tiles, chunk_cnt, chunk_base,
+                                         n_extra_dev, desc, tmax);
     GSR_LAUNCH_CHECK("chunk_write");
     return GSR_OK;
 }

@@ -124,23 +124,51 @@ __device__ __forceinline__ uint32_t wave_reduce_sum(uint32_t v) {
     return v;
 }
 
+// Exclusive scan of one value per thread across a block of NT threads.
+template <int NT>
+__device__ __forceinline__ uint32_t block_exclusive(uint32_t v, uint32_t* lds_waves,
+                                                    uint32_t& total) {
+    constexpr int NW = NT / 64;
+    const int w = threadIdx.x >> 6;
+    const uint32_t inc = wave_inclusive_scan(v);
+    if (__lane_id() == 63) lds_waves[w] = inc;
+    __syncthreads();
+    uint32_t woff = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const uint32_t t = lds_waves[i];
+        woff += (i < w) ? t : 0u;
+        tot += t;
+    }
+    total = tot;
+    return woff + inc - v;
+}
+
 // ---------------------------------------------------------------- host launchers
 // scan.hip: exclusive scan of n uint32 (in may equal out). Writes the total to
 // *total_dev (device) when non-null. tmp must hold scan_tmp_elems(n) uint32.
+// Optionally also reduces n_kr key ranges {~kmin, kmax} (componentwise max)
+// into kr_out[0..1].
 size_t scan_tmp_elems(size_t n);
 int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
-                   uint32_t* total_dev, hipStream_t s);
+                   uint32_t* total_dev, hipStream_t s, const uint2* kr_in = nullptr,
+                   size_t n_kr = 0, uint32_t* kr_out = nullptr);
 
-// radix_sort.hip: stable LSD sort of (key, val) by bits [begin_bit, end_bit).
-// Buffers are ping-ponged; the sorted result ends in (*keys_io, *vals_io)
-// (pointers swapped as needed). vals_in == nullptr means vals = 0..n-1.
-// n_dev (nullable): device-side element count <= n (grids are sized by n).
-// totals: radix_totals_elems() uint32 of scratch.
+// radix_sort.hip: stable LSD sort of (key, val), `passes` passes of
+// w = ceil(B / passes) <= 11 bits, where B = `bits` (keys < 2^bits) or, when
+// key_range (device {~kmin, kmax}) is given, B = bits(kmax - kmin) chosen on
+// the device (keys are then sorted as key - kmin).  Buffers are ping-ponged;
+// the sorted result ends in (*keys_io, *vals_io) (pointers swapped as needed).
+// identity_vals: vals = 0..n-1 (vals_io not read).  n_dev (nullable):
+// device-side element count <= n (grids are sized by n).  tmp holds
+// radix_tmp_elems(n) uint32, totals radix_totals_elems() uint32.
 size_t radix_tmp_elems(size_t n);
 size_t radix_totals_elems();
+int radix_passes_for(int bits);
 int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt,
                      uint32_t** vals_alt, bool identity_vals, size_t n, const uint32_t* n_dev,
-                     int begin_bit, int end_bit, uint32_t* tmp, uint32_t* totals, hipStream_t s);
+                     int bits, int passes, const uint32_t* key_range, uint32_t* tmp,
+                     uint32_t* totals, hipStream_t s);
 
 // scene.hip
 int scene_repack_from_fields(SceneData& sd, const float* xyz, const float* rot,
@@ -149,12 +177,20 @@ int scene_repack_from_fields(SceneData& sd, const float* xyz, const float* rot,
 int scene_repack_from_flat(SceneData& sd, const float* flat, hipStream_t s);
 
 // preprocess.hip
+// k_cull also zeroes n_zero words at zero_words (the frame's zero block) and
+// writes per block of kCullBlock Gaussians the depth-key range {~kmin, kmax}
+// of its visible ones ({0, 0} if none) to block_ranges.
+constexpr int kCullBlock = 256;
 int launch_cull(const SceneData& sd, const FrameUniforms& u, uint64_t* vis_mask,
-                uint32_t* wave_counts, hipStream_t s);
+                uint32_t* wave_counts, uint2* block_ranges, uint32_t* zero_words, uint32_t n_zero,
+                hipStream_t s);
+// counters[0] = V (input), counters[1] = D (written by the last block, which
+// also stores (V, D, seq) to host-mapped host_counters and re-arms done_ctr).
 int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_t* vis_mask,
                       const uint32_t* wave_off, const uint32_t* n_vis_dev, SplatRec* recs,
-                      uint32_t* depth_keys, uint2* trect, uint32_t* n_dup_dev, int32_t* radii,
-                      hipStream_t s);
+                      uint32_t* depth_keys, uint2* trect, uint32_t* counters,
+                      unsigned long long* done_ctr, uint32_t* host_counters, uint32_t seq,
+                      int32_t* radii, hipStream_t s);
 int launch_depth_keys_all(const SceneData& sd, const float* V, uint32_t* keys, hipStream_t s);
 
 // composite.hip
@@ -163,6 +199,7 @@ int launch_binning(const uint32_t* sorted_ids, const uint2* trect, uint32_t n_vi
                    uint32_t* tmp, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s);
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
                        hipStream_t s);
+// chunk_cnt must hold num_tiles + num_tiles / 256 + 1 entries (block totals after the tiles)
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, float4* tmax, hipStream_t s);
 int launch_composite(const uint4* desc, const uint32_t* n_chunks_dev, uint32_t max_chunks,

@@ -109,18 +109,46 @@ __device__ __forceinline__ uint32_t float_order_key(float f) {
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
+// Also clears the frame's zero block (tile ranges, saturation words): they
+// are first used several launches later, so no memset launch is needed.
 __global__ __launch_bounds__(kThreads) void k_cull(const float4* __restrict__ pos_op, int64_t n, FrameUniforms u,
-                                                   uint64_t* __restrict__ vis_mask, uint32_t* __restrict__ wave_counts) {
+                                                   uint64_t* __restrict__ vis_mask, uint32_t* __restrict__ wave_counts,
+                                                   uint2* __restrict__ block_ranges, uint32_t* __restrict__ zero_words,
+                                                   uint32_t n_zero) {
+    static_assert(kThreads == kCullBlock, "one key range per cull block");
+    __shared__ uint2 s_kr[kThreads / 64];
     const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    // write-through (sc1) stores: several of these words are later updated by
+    // atomics, which act at the coherence point, not in this XCD's L2
+    for (int64_t z = i; z < (int64_t)n_zero; z += (int64_t)gridDim.x * kThreads)
+        __hip_atomic_store(zero_words + z, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bool vis = false;
+    uint32_t key = 0;
     if (i < n) {
         const float4 p = pos_op[i];
-        vis = project(p.x, p.y, p.z, u).vis;
+        const Projected pr = project(p.x, p.y, p.z, u);
+        vis = pr.vis;
+        key = float_order_key(-pr.pv[2]);  // the depth key k_preprocess writes
     }
     const uint64_t m = __ballot(vis);
     if (__lane_id() == 0) {
         vis_mask[i >> 6] = m;
         wave_counts[i >> 6] = (uint32_t)__popcll(m);
+    }
+    // depth-key range of the visible Gaussians ({~kmin, kmax}, componentwise max)
+    uint32_t a = vis ? ~key : 0u, b = vis ? key : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a = max(a, (uint32_t)__shfl_xor((int)a, o, 64));
+        b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
+    }
+    if (__lane_id() == 0) s_kr[threadIdx.x >> 6] = make_uint2(a, b);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint2 r = s_kr[0];
+#pragma unroll
+        for (int w = 1; w < kThreads / 64; ++w) r = make_uint2(max(r.x, s_kr[w].x), max(r.y, s_kr[w].y));
+        block_ranges[blockIdx.x] = r;
     }
 }
 
@@ -403,7 +431,9 @@ __global__ __launch_bounds__(kThreads) void k_preprocess(const float4* __restric
                                                          const uint32_t* __restrict__ wave_off,
                                                          const uint32_t* __restrict__ n_vis_dev,
                                                          SplatRec* __restrict__ recs, uint32_t* __restrict__ depth_keys,
-                                                         uint2* __restrict__ trect, uint32_t* __restrict__ n_dup_dev,
+                                                         uint2* __restrict__ trect, uint32_t* __restrict__ counters,
+                                                         unsigned long long* __restrict__ done_ctr,
+                                                         uint32_t* __restrict__ host_counters, uint32_t seq,
                                                          int32_t* __restrict__ radii) {
     __shared__ uint32_t s_cnt[kThreads / 64];
     const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -418,8 +448,24 @@ __global__ __launch_bounds__(kThreads) void k_preprocess(const float4* __restric
     if (__lane_id() == 0) s_cnt[threadIdx.x >> 6] = ws;
     __syncthreads();
     if (threadIdx.x == 0) {
+        // One 64-bit atomic carries both this block's instance count (low 40
+        // bits) and its completion (high bits), so the block whose add
+        // completes the grid holds the frame's total without any fence.  It
+        // publishes (V, D) to the device counters and, with the frame's
+        // sequence number last, to host-mapped memory (the host sizes the
+        // tile sort from them while the GPU runs the depth sort), and re-arms
+        // the counter for the next frame.
         const uint32_t b = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
-        if (b) atomicAdd(n_dup_dev, b);
+        const unsigned long long old = atomicAdd(done_ctr, (1ull << 40) | (unsigned long long)b);
+        if ((old >> 40) == (unsigned long long)(gridDim.x - 1)) {
+            const uint32_t n_dup = (uint32_t)(old & ((1ull << 40) - 1)) + b;
+            const uint32_t n_vis = n_vis_dev[0];
+            counters[1] = n_dup;
+            __hip_atomic_store(host_counters + 0, n_vis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_counters + 1, n_dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_counters + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(done_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -435,16 +481,17 @@ __global__ __launch_bounds__(kThreads) void k_depth_keys_all(const float4* __res
 }  // namespace
 
 int launch_cull(const SceneData& sd, const FrameUniforms& u, uint64_t* vis_mask, uint32_t* wave_counts,
-                hipStream_t s) {
+                uint2* block_ranges, uint32_t* zero_words, uint32_t n_zero, hipStream_t s) {
     const unsigned grid = (unsigned)((sd.n + kThreads - 1) / kThreads);
-    k_cull<<<grid, kThreads, 0, s>>>(sd.pos_op, sd.n, u, vis_mask, wave_counts);
+    k_cull<<<grid, kThreads, 0, s>>>(sd.pos_op, sd.n, u, vis_mask, wave_counts, block_ranges, zero_words, n_zero);
     GSR_LAUNCH_CHECK("cull");
     return GSR_OK;
 }
 
 int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_t* vis_mask,
                       const uint32_t* wave_off, const uint32_t* n_vis_dev, SplatRec* recs, uint32_t* depth_keys,
-                      uint2* trect, uint32_t* n_dup_dev, int32_t* radii, hipStream_t s) {
+                      uint2* trect, uint32_t* counters, unsigned long long* done_ctr, uint32_t* host_counters,
+                      uint32_t seq, int32_t* radii, hipStream_t s) {
     const unsigned grid = (unsigned)((sd.n + kThreads - 1) / kThreads);
     // effective SH degree: the gates of gau_vert.glsl:289-313; -1 = colour not from SH
     const int m = u.render_mod;
@@ -452,7 +499,8 @@ int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_
     if (m == -3 || m == -2 || m == -1) deg = -1;
 #define GSR_PRE(D)                                                                                                  \
     k_preprocess<D><<<grid, kThreads, 0, s>>>(sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, u, vis_mask, wave_off,    \
-                                              n_vis_dev, recs, depth_keys, trect, n_dup_dev, radii)
+                                              n_vis_dev, recs, depth_keys, trect, counters, done_ctr,            \
+                                              host_counters, seq, radii)
     switch (deg) {
         case -1: GSR_PRE(-1); break;
         case 0: GSR_PRE(0); break;

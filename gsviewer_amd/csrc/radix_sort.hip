@@ -1,16 +1,28 @@
-// Stable LSD radix sort of (uint32 key, uint32 value) pairs, 8-bit digits.
+// Stable LSD radix sort of (uint32 key, uint32 value) pairs.
 //
-// One pass = three launches:
-//   k_radix_hist   per 1024-item block digit counts (wave digit matching, no
-//                  atomics of any kind), stored digit-major;
-//   k_radix_offsets one workgroup per digit: exclusive scan of that digit's
-//                  row of block counts (in place) and the row total;
-//   k_radix_scatter scans the 256 row totals itself (digit bases), then ranks
-//                  stably in-block with wave-level digit matching (8 ballots
-//                  per 64 items; waves own consecutive item ranges), stages in
-//                  LDS in digit order and writes contiguous runs.
+// Digit width is chosen per sort, up to 11 bits, so that a 32-bit key needs at
+// most 3 passes.  For the depth sort the width is chosen ON THE DEVICE: the
+// preprocess records the key range [kmin, kmax] of the frame, keys are sorted
+// as key - kmin, and B = bits(kmax - kmin) is split over the host's fixed
+// number of passes (w = ceil(B / passes)).  A camera's visible depths span
+// ~26 of the 32 key bits, so 3 passes of 9 bits replace 4 passes of 8 and the
+// host never has to know B.
+//
+// One pass = three launches over tiles of 256*R items (R = 4 at these sizes:
+// ~1000 tiles per million keys keep every CU busy and the latency chains of
+// 2-4 resident tiles per CU overlapped):
+//   k_rs_upsweep   per-tile digit counts (wave ballot digit matching, no
+//                  atomics), stored digit-major: hist[d * ntiles + tile];
+//   k_rs_offsets   one wave per digit: exclusive scan of that digit's row
+//                  (in place) and the row total;
+//   k_rs_scatter   digit bases (block scan of the row totals), stable in-tile
+//                  ranks (waves own consecutive 64*R-item ranges, R rounds of
+//                  64), staged in LDS in digit order, written as contiguous
+//                  runs.  The digit bases and this tile's row offsets are
+//                  loaded before the keys are ranked, so their latency hides
+//                  behind the ranking.
 // The element count may live in device memory (n_dev): grids are sized by a
-// host-side upper bound and blocks past the device count do nothing, so a
+// host-side upper bound and tiles past the device count do nothing, so a
 // frame needs no host round trip to size its sorts.
 #include "gsr_internal.h"
 
@@ -19,153 +31,214 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr int kRounds = 4;                       // 64-item rounds per wave
-constexpr int kBlockItems = kThreads * kRounds;  // 1024: enough blocks to fill 256 CUs at 1M keys
-constexpr int kRadix = 256;
+constexpr int kR = 4;                            // items per thread (64-item rounds per wave)
+constexpr int kTileItems = kThreads * kR;        // 1024
+constexpr int kMaxBits = 11;
+constexpr int kMaxRadix = 1 << kMaxBits;         // 2048
+constexpr int kDigitsPerThread = kMaxRadix / kThreads;  // 8
+
+struct PassArgs {
+    const uint32_t* key_range;  // device {~kmin, kmax} or null (then kmin = 0 and B = bits)
+    uint32_t bits;
+    uint32_t passes;
+    uint32_t pass;
+};
+
+struct Digit {
+    uint32_t kmin, shift, w, mask;
+    __device__ __forceinline__ uint32_t of(uint32_t key) const { return ((key - kmin) >> shift) & mask; }
+};
+
+__device__ __forceinline__ Digit digit_params(const PassArgs& p) {
+    Digit d;
+    uint32_t B;
+    if (p.key_range) {
+        d.kmin = ~p.key_range[0];
+        const uint32_t kmax = p.key_range[1];
+        B = kmax > d.kmin ? 32u - (uint32_t)__clz(kmax - d.kmin) : 0u;
+    } else {
+        d.kmin = 0u;
+        B = p.bits;
+    }
+    d.w = max(1u, (B + p.passes - 1u) / p.passes);
+    d.shift = p.pass * d.w;
+    d.mask = (1u << d.w) - 1u;
+    return d;
+}
 
 __device__ __forceinline__ uint32_t count_of(const uint32_t* n_dev, uint32_t n_host) {
     return n_dev ? min(n_host, n_dev[0]) : n_host;
 }
 
-__global__ __launch_bounds__(kThreads) void k_radix_hist(const uint32_t* __restrict__ keys,
-                                                         const uint32_t* __restrict__ n_dev, uint32_t n_host, int shift,
-                                                         uint32_t* __restrict__ hist, uint32_t nblocks) {
-    __shared__ uint32_t h[kWaves][kRadix];
+// Lanes of the wave holding the same w-bit digit (only `valid` lanes).
+__device__ __forceinline__ uint64_t match_digit(uint32_t digit, uint32_t w, bool valid) {
+    uint64_t peers = __ballot(valid);
+    for (uint32_t b = 0; b < w; ++b) {
+        const bool bit = (digit >> b) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+    }
+    return peers;
+}
+
+__global__ __launch_bounds__(kThreads) void k_rs_upsweep(const uint32_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ n_dev, uint32_t n_host,
+                                                         PassArgs pa, uint32_t* __restrict__ hist, uint32_t ntiles) {
+    __shared__ uint16_t h[kWaves][kMaxRadix];  // per-wave counts (<= 64*kR each)
+    const Digit dg = digit_params(pa);
+    const uint32_t radix = dg.mask + 1u;
     const uint32_t n = count_of(n_dev, n_host);
-    const uint32_t block0 = blockIdx.x * kBlockItems;
-    for (int i = threadIdx.x; i < kWaves * kRadix; i += kThreads) (&h[0][0])[i] = 0;
+    const uint32_t tile0 = blockIdx.x * kTileItems;
+    for (uint32_t i = threadIdx.x; i < kWaves * radix; i += kThreads) h[i / radix][i % radix] = 0u;
     const int w = threadIdx.x >> 6;
-    const uint32_t base = block0 + w * (kBlockItems / kWaves) + __lane_id();
-    uint32_t d[kRounds];
+    const uint32_t base = tile0 + w * (kTileItems / kWaves) + __lane_id();
+    uint32_t k[kR];
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) {  // issue every load first
+    for (int r = 0; r < kR; ++r) {  // issue every load first
         const uint32_t i = base + r * 64;
-        d[r] = i < n ? keys[i] : 0u;
+        k[r] = i < n ? keys[i] : 0u;
     }
     __syncthreads();
-    if (block0 < n) {
+    if (tile0 < n) {
 #pragma unroll
-        for (int r = 0; r < kRounds; ++r) {
+        for (int r = 0; r < kR; ++r) {
             const bool valid = base + r * 64 < n;
-            const uint32_t dg = (d[r] >> shift) & 0xffu;
-            const uint64_t peers = match_digit8(dg, valid);
-            if (valid && (peers & lanemask_lt()) == 0) h[w][dg] += (uint32_t)__popcll(peers);
+            const uint32_t d = dg.of(k[r]);
+            const uint64_t peers = match_digit(d, dg.w, valid);
+            if (valid && (peers & lanemask_lt()) == 0) h[w][d] = (uint16_t)(h[w][d] + __popcll(peers));
         }
     }
     __syncthreads();
-    const int dg = threadIdx.x;  // kThreads == kRadix
-    uint32_t s = 0;
+    for (uint32_t d = threadIdx.x; d < radix; d += kThreads) {
+        uint32_t s = 0;
 #pragma unroll
-    for (int k = 0; k < kWaves; ++k) s += h[k][dg];
-    hist[(size_t)dg * nblocks + blockIdx.x] = s;
+        for (int q = 0; q < kWaves; ++q) s += h[q][d];
+        hist[(size_t)d * ntiles + blockIdx.x] = s;
+    }
 }
 
-// Block d: exclusive scan of row d (nblocks counts) in place; row total out.
-__global__ __launch_bounds__(kThreads) void k_radix_offsets(uint32_t* __restrict__ hist, uint32_t nblocks,
-                                                            uint32_t* __restrict__ totals) {
-    __shared__ uint32_t lds[kWaves];
-    const int d = blockIdx.x;
-    const int w = threadIdx.x >> 6;
-    uint32_t* row = hist + (size_t)d * nblocks;
-    const uint32_t per = (nblocks + kThreads - 1) / kThreads;
-    const uint32_t b0 = threadIdx.x * per;
-    const uint32_t b1 = min(nblocks, b0 + per);
+// One wave per digit d: exclusive scan of row d (ntiles counts) in place; row total out.
+__global__ __launch_bounds__(64) void k_rs_offsets(uint32_t* __restrict__ hist, uint32_t ntiles, PassArgs pa,
+                                                   uint32_t* __restrict__ totals) {
+    const Digit dg = digit_params(pa);
+    const uint32_t d = blockIdx.x;
+    if (d > dg.mask) return;
+    uint32_t* row = hist + (size_t)d * ntiles;
+    const uint32_t per = (ntiles + 63) / 64;
+    const uint32_t b0 = __lane_id() * per;
+    const uint32_t b1 = min(ntiles, b0 + per);
     uint32_t s = 0;
     for (uint32_t i = b0; i < b1; ++i) s += row[i];
     const uint32_t inc = wave_inclusive_scan(s);
-    if (__lane_id() == 63) lds[w] = inc;
-    __syncthreads();
-    uint32_t run = inc - s, tot = 0;
-    for (int k = 0; k < kWaves; ++k) {
-        run += (k < w) ? lds[k] : 0u;
-        tot += lds[k];
-    }
+    uint32_t run = inc - s;
     for (uint32_t i = b0; i < b1; ++i) {
         const uint32_t t = row[i];
         row[i] = run;
         run += t;
     }
-    if (threadIdx.x == 0) totals[d] = tot;
+    if (__lane_id() == 63) totals[d] = inc;
 }
 
-__global__ __launch_bounds__(kThreads) void k_radix_scatter(
+__global__ __launch_bounds__(kThreads) void k_rs_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, bool identity_vals,
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ n_dev,
-    uint32_t n_host, int shift, const uint32_t* __restrict__ hist_off, const uint32_t* __restrict__ totals,
-    uint32_t nblocks) {
-    __shared__ uint32_t s_keys[kBlockItems];
-    __shared__ uint32_t s_vals[kBlockItems];
-    __shared__ uint32_t wcnt[kWaves][kRadix];  // per-wave digit counts, then per-wave prefixes
-    __shared__ uint32_t dbase[kRadix];         // block-local exclusive digit offsets
-    __shared__ uint32_t gbase[kRadix];         // global offset of this block's digit run
-    __shared__ uint32_t wsum[kWaves];
+    uint32_t n_host, PassArgs pa, const uint32_t* __restrict__ hist_off, const uint32_t* __restrict__ totals,
+    uint32_t ntiles) {
+    __shared__ uint32_t s_keys[kTileItems];
+    __shared__ uint32_t s_vals[kTileItems];
+    __shared__ uint16_t wcnt[kWaves][kMaxRadix];  // per-wave digit counts, then per-wave prefixes
+    __shared__ uint32_t dbase[kMaxRadix];         // tile-local exclusive digit offsets
+    __shared__ uint32_t gbase[kMaxRadix];         // global position of LDS index 0 of digit d's run
+    __shared__ uint32_t wsum[2][kWaves];
 
     const uint32_t n = count_of(n_dev, n_host);
-    const uint32_t block0 = blockIdx.x * kBlockItems;
-    if (block0 >= n) return;
-    for (int i = threadIdx.x; i < kWaves * kRadix; i += kThreads) (&wcnt[0][0])[i] = 0;
+    const uint32_t tile0 = blockIdx.x * kTileItems;
+    if (tile0 >= n) return;
+    const Digit dg = digit_params(pa);
+    const uint32_t radix = dg.mask + 1u;
+    // thread t owns digits [t*q, t*q + q): issue their global loads first
+    const uint32_t q = (radix + kThreads - 1) / kThreads;
+    const uint32_t d0 = threadIdx.x * q;
+    uint32_t gt[kDigitsPerThread], ho[kDigitsPerThread];
+#pragma unroll
+    for (int j = 0; j < kDigitsPerThread; ++j) {
+        const uint32_t d = d0 + j;
+        const bool mine = j < (int)q && d < radix;
+        gt[j] = mine ? totals[d] : 0u;
+        ho[j] = mine ? hist_off[(size_t)d * ntiles + blockIdx.x] : 0u;
+    }
+    for (uint32_t i = threadIdx.x; i < kWaves * radix; i += kThreads) wcnt[i / radix][i % radix] = 0u;
 
     const int w = threadIdx.x >> 6;
-    const uint32_t base = block0 + w * (kBlockItems / kWaves) + __lane_id();
+    const uint32_t base = tile0 + w * (kTileItems / kWaves) + __lane_id();
     const uint64_t lt = lanemask_lt();
 
-    uint32_t k_reg[kRounds], v_reg[kRounds], rank[kRounds];
+    uint32_t k_reg[kR], v_reg[kR], rank[kR];
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) {  // issue every load first
+    for (int r = 0; r < kR; ++r) {  // issue every load first
         const uint32_t i = base + r * 64;
         const bool valid = i < n;
-        k_reg[r] = valid ? keys_in[i] : 0xffffffffu;
+        k_reg[r] = valid ? keys_in[i] : 0u;
         v_reg[r] = valid ? (identity_vals ? i : vals_in[i]) : 0u;
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
+    for (int r = 0; r < kR; ++r) {
         const bool valid = base + r * 64 < n;
-        const uint32_t d = (k_reg[r] >> shift) & 0xffu;
-        const uint64_t peers = match_digit8(d, valid);
+        const uint32_t d = dg.of(k_reg[r]);
+        const uint64_t peers = match_digit(d, dg.w, valid);
         uint32_t rk = 0xffffffffu;
         if (valid) {
             const uint32_t old = wcnt[w][d];
             rk = old + (uint32_t)__popcll(peers & lt);
-            if ((peers & lt) == 0) wcnt[w][d] = old + (uint32_t)__popcll(peers);
+            if ((peers & lt) == 0) wcnt[w][d] = (uint16_t)(old + __popcll(peers));
         }
         rank[r] = rk;
     }
     __syncthreads();
 
-    {  // per digit: wave prefixes, block-local digit offsets, global run base
-        const int d = threadIdx.x;
-        uint32_t tot = 0;
+    {
+        // per owned digit: wave prefixes, then two block scans over digits
+        // (tile-local offsets, global digit bases)
+        uint32_t tot[kDigitsPerThread];
+        uint32_t s_loc = 0, s_glob = 0;
 #pragma unroll
-        for (int k = 0; k < kWaves; ++k) {
-            const uint32_t c = wcnt[k][d];
-            wcnt[k][d] = tot;
-            tot += c;
+        for (int j = 0; j < kDigitsPerThread; ++j) {
+            const uint32_t d = d0 + j;
+            tot[j] = 0u;
+            if (j < (int)q && d < radix) {
+                uint32_t run = 0;
+#pragma unroll
+                for (int k = 0; k < kWaves; ++k) {
+                    const uint32_t c = wcnt[k][d];
+                    wcnt[k][d] = (uint16_t)run;
+                    run += c;
+                }
+                tot[j] = run;
+            }
+            s_loc += tot[j];
+            s_glob += gt[j];
         }
-        const uint32_t inc = wave_inclusive_scan(tot);
-        if (__lane_id() == 63) wsum[w] = inc;
-        __syncthreads();
-        uint32_t woff = 0;
+        uint32_t t_loc, t_glob;
+        uint32_t e_loc = block_exclusive<kThreads>(s_loc, wsum[0], t_loc);
+        uint32_t e_glob = block_exclusive<kThreads>(s_glob, wsum[1], t_glob);
 #pragma unroll
-        for (int k = 0; k < kWaves; ++k) woff += (k < w) ? wsum[k] : 0u;
-        dbase[d] = woff + inc - tot;
-        // digit base = exclusive scan of the row totals over digits
-        const uint32_t t = totals[d];
-        const uint32_t tinc = wave_inclusive_scan(t);
-        __syncthreads();
-        if (__lane_id() == 63) wsum[w] = tinc;
-        __syncthreads();
-        uint32_t tb = 0;
-#pragma unroll
-        for (int k = 0; k < kWaves; ++k) tb += (k < w) ? wsum[k] : 0u;
-        gbase[d] = tb + tinc - t + hist_off[(size_t)d * nblocks + blockIdx.x];
+        for (int j = 0; j < kDigitsPerThread; ++j) {
+            const uint32_t d = d0 + j;
+            if (j < (int)q && d < radix) {
+                dbase[d] = e_loc;
+                gbase[d] = e_glob + ho[j] - e_loc;
+            }
+            e_loc += tot[j];
+            e_glob += gt[j];
+        }
     }
     __syncthreads();
 
 #pragma unroll
-    for (int r = 0; r < kRounds; ++r) {
+    for (int r = 0; r < kR; ++r) {
         if (rank[r] != 0xffffffffu) {
-            const uint32_t d = (k_reg[r] >> shift) & 0xffu;
+            const uint32_t d = dg.of(k_reg[r]);
             const uint32_t p = dbase[d] + wcnt[w][d] + rank[r];
             s_keys[p] = k_reg[r];
             s_vals[p] = v_reg[r];
@@ -173,11 +246,10 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
     }
     __syncthreads();
 
-    const uint32_t cnt = min(n - block0, (uint32_t)kBlockItems);
+    const uint32_t cnt = min(n - tile0, (uint32_t)kTileItems);
     for (uint32_t j = threadIdx.x; j < cnt; j += kThreads) {
         const uint32_t key = s_keys[j];
-        const uint32_t d = (key >> shift) & 0xffu;
-        const uint32_t g = gbase[d] + (j - dbase[d]);
+        const uint32_t g = gbase[dg.of(key)] + j;
         keys_out[g] = key;
         vals_out[g] = s_vals[j];
     }
@@ -186,29 +258,34 @@ __global__ __launch_bounds__(kThreads) void k_radix_scatter(
 }  // namespace
 
 size_t radix_tmp_elems(size_t n) {
-    const size_t nb = (n + kBlockItems - 1) / kBlockItems;
-    return (nb < 1 ? 1 : nb) * kRadix;
+    const size_t nb = (n + kTileItems - 1) / kTileItems;
+    return (nb < 1 ? 1 : nb) * kMaxRadix;
 }
 
-size_t radix_totals_elems() { return (size_t)kRadix; }  // digit totals scratch (rewritten every pass)
+size_t radix_totals_elems() { return (size_t)kMaxRadix; }  // digit totals scratch (rewritten every pass)
+
+int radix_passes_for(int bits) { return bits <= 0 ? 0 : (bits + kMaxBits - 1) / kMaxBits; }
 
 int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
-                     bool identity_vals, size_t n, const uint32_t* n_dev, int begin_bit, int end_bit, uint32_t* tmp,
-                     uint32_t* totals, hipStream_t s) {
-    if (n == 0) return GSR_OK;
-    if (n > 0xffffffffull - kBlockItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
-    if ((end_bit - begin_bit + 7) / 8 > 4) return set_error(GSR_ERR_INVALID, "radix sort: more than 4 passes");
-    const uint32_t nb = (uint32_t)((n + kBlockItems - 1) / kBlockItems);
-    uint32_t* hist = tmp;
+                     bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
+                     const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s) {
+    if (n == 0 || passes == 0) return GSR_OK;
+    if (n > 0xffffffffull - kTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
+    if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
+        return set_error(GSR_ERR_INVALID, "radix sort: digit width out of range");
+    const uint32_t nt = (uint32_t)((n + kTileItems - 1) / kTileItems);
+    // upper bound of the radix over the passes (device-chosen widths never exceed it)
+    const uint32_t radix_max = 1u << ((bits + passes - 1) / passes);
     bool ident = identity_vals;
-    for (int shift = begin_bit; shift < end_bit; shift += 8) {
-        k_radix_hist<<<nb, kThreads, 0, s>>>(*keys_io, n_dev, (uint32_t)n, shift, hist, nb);
-        GSR_LAUNCH_CHECK("radix_hist");
-        k_radix_offsets<<<kRadix, kThreads, 0, s>>>(hist, nb, totals);
-        GSR_LAUNCH_CHECK("radix_offsets");
-        k_radix_scatter<<<nb, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev, (uint32_t)n,
-                                                shift, hist, totals, nb);
-        GSR_LAUNCH_CHECK("radix_scatter");
+    for (int p = 0; p < passes; ++p) {
+        const PassArgs pa{key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p};
+        k_rs_upsweep<<<nt, kThreads, 0, s>>>(*keys_io, n_dev, (uint32_t)n, pa, tmp, nt);
+        GSR_LAUNCH_CHECK("rs_upsweep");
+        k_rs_offsets<<<radix_max, 64, 0, s>>>(tmp, nt, pa, totals);
+        GSR_LAUNCH_CHECK("rs_offsets");
+        k_rs_scatter<<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev, (uint32_t)n, pa,
+                                             tmp, totals, nt);
+        GSR_LAUNCH_CHECK("rs_scatter");
         ident = false;
         uint32_t* t = *keys_io; *keys_io = *keys_alt; *keys_alt = t;
         t = *vals_io; *vals_io = *vals_alt; *vals_alt = t;
@@ -217,3 +294,4 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
 }
 
 }  // namespace gsr
+

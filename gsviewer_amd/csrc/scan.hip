@@ -14,26 +14,6 @@ constexpr int kTileItems = kThreads * kItems;  // 4096
 constexpr int kPartialThreads = 1024;
 constexpr size_t kSingleMax = 131072;  // single-workgroup scan up to this many elements
 
-// Exclusive scan of one value per thread across a block of NT threads.
-template <int NT>
-__device__ __forceinline__ uint32_t block_exclusive(uint32_t v, uint32_t* lds_waves,
-                                                    uint32_t& total) {
-    constexpr int NW = NT / 64;
-    const int w = threadIdx.x >> 6;
-    const uint32_t inc = wave_inclusive_scan(v);
-    if (__lane_id() == 63) lds_waves[w] = inc;
-    __syncthreads();
-    uint32_t woff = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-        const uint32_t t = lds_waves[i];
-        woff += (i < w) ? t : 0u;
-        tot += t;
-    }
-    total = tot;
-    return woff + inc - v;
-}
-
 __device__ __forceinline__ void load16(const uint32_t* in, size_t base, size_t n, uint32_t (&v)[kItems]) {
     if (base + kItems <= n) {
         const uint4* p = reinterpret_cast<const uint4*>(in + base);
@@ -70,9 +50,41 @@ __global__ __launch_bounds__(kThreads) void k_scan_reduce(const uint32_t* __rest
 
 // Single block: exclusive scan of the block sums, in place; writes the grand
 // total to total_dev when non-null.
+// Optional side job of the single-block kernels: componentwise max over n_kr
+// uint2 entries (the per-block depth-key ranges {~kmin, kmax} of k_cull) into
+// kr_out[0..1].
+__device__ __forceinline__ void reduce_ranges(const uint2* __restrict__ kr_in, size_t n_kr, uint32_t* __restrict__ kr_out,
+                                              uint2* lds) {
+    uint2 m = make_uint2(0u, 0u);
+    for (size_t i = threadIdx.x; i < n_kr; i += kPartialThreads) {
+        const uint2 v = kr_in[i];
+        m.x = max(m.x, v.x);
+        m.y = max(m.y, v.y);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        m.x = max(m.x, (uint32_t)__shfl_xor((int)m.x, o, 64));
+        m.y = max(m.y, (uint32_t)__shfl_xor((int)m.y, o, 64));
+    }
+    if (__lane_id() == 0) lds[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kPartialThreads / 64; ++w) {
+            m.x = max(m.x, lds[w].x);
+            m.y = max(m.y, lds[w].y);
+        }
+        kr_out[0] = m.x;
+        kr_out[1] = m.y;
+    }
+}
+
 __global__ __launch_bounds__(kPartialThreads) void k_scan_partials(uint32_t* __restrict__ sums, size_t nb,
-                                                                   uint32_t* __restrict__ total_dev) {
+                                                                   uint32_t* __restrict__ total_dev,
+                                                                   const uint2* __restrict__ kr_in, size_t n_kr,
+                                                                   uint32_t* __restrict__ kr_out) {
     __shared__ uint32_t lds[kPartialThreads / 64];
+    __shared__ uint2 lds_kr[kPartialThreads / 64];
+    if (kr_in) reduce_ranges(kr_in, n_kr, kr_out, lds_kr);
     const size_t per = (nb + kPartialThreads - 1) / kPartialThreads;
     const size_t b0 = (size_t)threadIdx.x * per;
     const size_t b1 = (b0 + per < nb) ? b0 + per : nb;
@@ -122,8 +134,12 @@ __global__ __launch_bounds__(kThreads) void k_scan_final(const uint32_t* __restr
 // prefetched), a block scan per chunk, a running carry.
 __global__ __launch_bounds__(kPartialThreads) void k_scan_single(const uint32_t* __restrict__ in,
                                                                  uint32_t* __restrict__ out, size_t n,
-                                                                 uint32_t* __restrict__ total_dev) {
+                                                                 uint32_t* __restrict__ total_dev,
+                                                                 const uint2* __restrict__ kr_in, size_t n_kr,
+                                                                 uint32_t* __restrict__ kr_out) {
     __shared__ uint32_t lds[2][kPartialThreads / 64];
+    __shared__ uint2 lds_kr[kPartialThreads / 64];
+    if (kr_in) reduce_ranges(kr_in, n_kr, kr_out, lds_kr);
     constexpr size_t kChunk = 4 * kPartialThreads;
     const bool aligned = (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
     auto load4 = [&](size_t c, uint32_t (&v)[4]) {
@@ -171,13 +187,14 @@ size_t scan_tmp_elems(size_t n) {
 }
 
 int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
-                   uint32_t* total_dev, hipStream_t s) {
+                   uint32_t* total_dev, hipStream_t s, const uint2* kr_in, size_t n_kr, uint32_t* kr_out) {
     if (n == 0) {
         if (total_dev) GSR_HIP_CHECK(hipMemsetAsync(total_dev, 0, sizeof(uint32_t), s));
+        if (kr_out) GSR_HIP_CHECK(hipMemsetAsync(kr_out, 0, 2 * sizeof(uint32_t), s));
         return GSR_OK;
     }
     if (n <= kSingleMax) {
-        k_scan_single<<<1, kPartialThreads, 0, s>>>(in, out, n, total_dev);
+        k_scan_single<<<1, kPartialThreads, 0, s>>>(in, out, n, total_dev, kr_in, n_kr, kr_out);
         GSR_LAUNCH_CHECK("scan_single");
         return GSR_OK;
     }
@@ -185,7 +202,7 @@ int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
     const size_t nb = (n + kTileItems - 1) / kTileItems;
     k_scan_reduce<<<dim3((unsigned)nb), dim3(kThreads), 0, s>>>(in, n, tmp);
     GSR_LAUNCH_CHECK("scan_reduce");
-    k_scan_partials<<<1, kPartialThreads, 0, s>>>(tmp, nb, total_dev);
+    k_scan_partials<<<1, kPartialThreads, 0, s>>>(tmp, nb, total_dev, kr_in, n_kr, kr_out);
     GSR_LAUNCH_CHECK("scan_partials");
     k_scan_final<<<dim3((unsigned)nb), dim3(kThreads), 0, s>>>(in, out, n, tmp);
     GSR_LAUNCH_CHECK("scan_final");

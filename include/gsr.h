@@ -143,6 +143,12 @@ int gsr_context_stats(const gsr_context* ctx, gsr_frame_stats* out);
 int gsr_sort_depth(gsr_context* ctx, const gsr_scene* scene, const float view[16],
                    int32_t* index_dev, void* stream);
 
+/* Test hook: stable sort of n uint32 keys < 2^bits (values = 0..n-1) with
+ * the frame's radix sort, in `passes` passes of ceil(bits/passes) <= 11 bits.
+ * Asynchronous on `stream`, like gsr_render. */
+int gsr_debug_sort_pairs(gsr_context* ctx, const uint32_t* keys_dev, int64_t n, int32_t bits, int32_t passes,
+                         uint32_t* keys_out_dev, uint32_t* vals_out_dev, void* stream);
+
 /* Optional per-stage GPU timing with HIP events recorded on the render stream
  * (no extra synchronisation in the frame; accumulated lazily).
  * Stages: cull (+ visible-count scan), preprocess, depth sort, binning
