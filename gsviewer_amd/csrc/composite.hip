@@ -559,41 +559,65 @@ __global__ __launch_bounds__(kThreads) GSR_COMP_OCC void k_composite(const uint4
 #endif
 }
 
-// Fold the partial results of multi-chunk tiles in depth order: one block per
-// tile, wave k folds slice k up to its saturating chunk (if any).
-__global__ __launch_bounds__(kThreads) void k_merge(const uint32_t* __restrict__ chunk_cnt,
-                                                    const uint32_t* __restrict__ chunk_base,
-                                                    const float4* __restrict__ partial,
-                                                    const uint32_t* __restrict__ sat, CompositeArgs a,
-                                                    float* __restrict__ out) {
+// Fold the partial results of multi-chunk tiles in depth order: one block of
+// 16 waves per tile; wave w folds slice (w & 3) over the w >> 2 quarter of the
+// tile's chunks (up to the saturating chunk, if any) with 16 partial loads in
+// flight, and the four quarters are combined in order through LDS.  The
+// deepest tiles (~100 chunks) set this kernel's length, so their fold is
+// spread over 4 waves instead of walked by one.
+constexpr int kMergeThreads = 1024;
+constexpr int kMergeParts = kMergeThreads / 64 / 4;  // 4
+constexpr int kMergeDepth = 16;
+
+__global__ __launch_bounds__(kMergeThreads) void k_merge(const uint32_t* __restrict__ chunk_cnt,
+                                                         const uint32_t* __restrict__ chunk_base,
+                                                         const float4* __restrict__ partial,
+                                                         const uint32_t* __restrict__ sat, CompositeArgs a,
+                                                         float* __restrict__ out) {
+    __shared__ float4 part[kMergeParts][4][64];
     const int tile = blockIdx.x;
     const uint32_t cnt = chunk_cnt[tile];
     if (cnt <= 1) return;
-    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int k = w & 3, q = w >> 2;
     const int lane = __lane_id();
     const uint32_t last = min(cnt - 1, 0xffffffffu - ld_relaxed(sat + tile * 4 + k));  // written by atomics
+    const uint32_t nfold = last + 1;
+    const uint32_t per = (nfold + kMergeParts - 1) / kMergeParts;
+    const uint32_t c_begin = min(nfold, q * per), c_end = min(nfold, c_begin + per);
     const uint32_t base = chunk_base[tile];
     float r = 0.f, g = 0.f, b = 0.f, T = 1.f;
-    constexpr int kDepth = 8;
-    for (uint32_t c0 = 0; c0 <= last; c0 += kDepth) {
-        float4 q[kDepth];
+    for (uint32_t c0 = c_begin; c0 < c_end; c0 += kMergeDepth) {
+        float4 v[kMergeDepth];
 #pragma unroll
-        for (int j = 0; j < kDepth; ++j) {
+        for (int j = 0; j < kMergeDepth; ++j) {
             const uint32_t c = c0 + j;
-            if (c <= last) {
+            if (c < c_end) {
                 const uint32_t slot = c == 0 ? (uint32_t)tile : base + c - 1;
-                q[j] = partial[(size_t)slot * 256 + k * 64 + lane];
+                v[j] = partial[(size_t)slot * 256 + k * 64 + lane];
             } else {
-                q[j] = make_float4(0.f, 0.f, 0.f, 1.f);
+                v[j] = make_float4(0.f, 0.f, 0.f, 1.f);
             }
         }
 #pragma unroll
-        for (int j = 0; j < kDepth; ++j) {
-            r += T * q[j].x;
-            g += T * q[j].y;
-            b += T * q[j].z;
-            T *= q[j].w;
+        for (int j = 0; j < kMergeDepth; ++j) {
+            r += T * v[j].x;
+            g += T * v[j].y;
+            b += T * v[j].z;
+            T *= v[j].w;
         }
+    }
+    part[q][k][lane] = make_float4(r, g, b, T);
+    __syncthreads();
+    if (q != 0) return;
+    // (C1, T1) then (C2, T2) == (C1 + T1*C2, T1*T2), quarters in depth order
+#pragma unroll
+    for (int p = 1; p < kMergeParts; ++p) {
+        const float4 v = part[p][k][lane];
+        r += T * v.x;
+        g += T * v.y;
+        b += T * v.z;
+        T *= v.w;
     }
     const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
     const int x = tx * kTile + (lane & 15);
@@ -709,7 +733,7 @@ int launch_composite(const uint4* desc, const uint32_t* n_chunks_dev, uint32_t m
 int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const float4* partial, const uint32_t* sat,
                  const FrameUniforms& u, float t_min, const float* bg, int out_layout, float* out, hipStream_t s) {
     const CompositeArgs a = make_args(u, t_min, bg, out_layout);
-    k_merge<<<(unsigned)a.num_tiles, kThreads, 0, s>>>(chunk_cnt, chunk_base, partial, sat, a, out);
+    k_merge<<<(unsigned)a.num_tiles, kMergeThreads, 0, s>>>(chunk_cnt, chunk_base, partial, sat, a, out);
     GSR_LAUNCH_CHECK("merge");
     return GSR_OK;
 }
