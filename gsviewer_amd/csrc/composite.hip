@@ -247,6 +247,12 @@ __device__ __forceinline__ void prior_bound(const float4* tmax, uint32_t tile, u
     for (int k = 0; k < 4; ++k) B[k] = uniform_f(wave_prod(v[k]));
 }
 
+#ifdef GSR_COMP_STATS
+// Tooling build only (tools/comp_stats.py): {slice evaluations, evaluations
+// of an already saturated slice, records visited, records in the chunks}.
+__device__ unsigned long long g_comp_stats[4];
+#endif
+
 // One wave per chunk, 4 pixels per lane (four 16x4 slices of the 16x16 tile).
 // Records of the chunk are gathered 64 at a time (one 48-B record per lane,
 // prefetched one batch ahead in registers) into a wave-private LDS buffer and
@@ -348,6 +354,9 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         live &= ~__builtin_amdgcn_readfirstlane(dead);
     }
 #endif
+#ifdef GSR_COMP_STATS
+    uint32_t st_evals = 0, st_wasted = 0, st_records = 0;
+#endif
     for (uint32_t b = begin; b < end && live; b += kBatch) {
         __builtin_amdgcn_wave_barrier();
         {
@@ -404,6 +413,15 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
 #endif
             // scalar mask of the 16x4 slices the splat touches (and still live)
             const uint32_t smask = __builtin_amdgcn_readfirstlane(__float_as_uint(q1.w)) & live;
+#ifdef GSR_COMP_STATS
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((smask >> k) & 1u) {
+                    st_evals += 1;
+                    if (!__any(T[k] >= t_min)) st_wasted += 1;
+                }
+            st_records += 1;
+#endif
             // lane coverage: bit 4k = this lane's pixel of slice k is inside the splat's quad
             // (all-zero when the column is not: bfe_i32 gives 0 or ~0)
             const uint32_t cov = __float_as_uint(q0.w);
@@ -493,6 +511,14 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         }
     }
 
+#ifdef GSR_COMP_STATS
+    if (lane == 0) {
+        atomicAdd(&g_comp_stats[0], (unsigned long long)st_evals);
+        atomicAdd(&g_comp_stats[1], (unsigned long long)st_wasted);
+        atomicAdd(&g_comp_stats[2], (unsigned long long)st_records);
+        atomicAdd(&g_comp_stats[3], (unsigned long long)(end - begin));
+    }
+#endif
     if (nchunks > 1) {
         // partial (C, T) per pixel, folded by k_merge; layout [slot][k][lane]
         float4* p = partial + (size_t)slot * 256;
@@ -640,6 +666,15 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(const uint32_t* __restr
 }
 
 }  // namespace
+
+#ifdef GSR_COMP_STATS
+extern "C" int gsr_debug_comp_stats(unsigned long long* host4) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(host4, HIP_SYMBOL(gsr::g_comp_stats), 32, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    static const unsigned long long zeros[4] = {0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_comp_stats), zeros, 32, 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef GSR_COMP_TRACE
 // Copies the last composite launch's per-wave stamps to host memory (tooling).

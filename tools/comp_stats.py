@@ -1,0 +1,39 @@
+"""Compositor work statistics on the bench workload (GSR_COMP_STATS build):
+slice evaluations, those spent on already-saturated slices, records visited.
+    python -m gsviewer_amd.build -D GSR_COMP_STATS --out gsviewer_amd/libgsr_stats.so
+    GSR_LIB_PATH=gsviewer_amd/libgsr_stats.so python tools/comp_stats.py"""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from gsviewer_amd import _lib  # noqa: E402
+from gsviewer_amd.camera import Camera  # noqa: E402
+from gsviewer_amd.gaussian_data import garden_standin  # noqa: E402
+from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into  # noqa: E402
+
+
+def main():
+    lib = _lib.load()
+    g = garden_standin(1_000_000, seed=1)
+    scene = HipScene.from_gaussian_data(g)
+    ctx = HipContext()
+    out = torch.empty((3, 1080, 1920), dtype=torch.float32, device="cuda")
+    buf = (ctypes.c_ulonglong * 4)()
+    for t_min in (1e-4, 0.0):
+        st = RenderSettings(t_min=t_min, out_layout=0)
+        render_into(ctx, scene, camera_from(Camera(1080, 1920)), st, out)
+        lib.gsr_debug_comp_stats(buf)  # discard warm-up frame
+        render_into(ctx, scene, camera_from(Camera(1080, 1920)), st, out)
+        torch.cuda.synchronize()
+        lib.gsr_debug_comp_stats(buf)
+        ev, wasted, recs, inst = list(buf)
+        print(f"t_min={t_min}: instances {inst} records visited {recs} ({recs / inst:.3f}), slice evals {ev} "
+              f"({ev / max(recs, 1):.2f} per record), on saturated slices {wasted} ({wasted / max(ev, 1):.3f})")
+
+
+if __name__ == "__main__":
+    main()
