@@ -70,6 +70,7 @@ struct gsr_context {
     gsr::DevBuf<gsr::SplatRec> recs;
     gsr::DevBuf<uint32_t> keys_a, keys_b, vals_a, vals_b;   // depth sort (capacity N)
     gsr::DevBuf<uint2> trect;                               // per record: packed tile rectangle
+    gsr::DevBuf<uint2> trect_sorted;                        // the same, in depth order (binning)
     gsr::DevBuf<uint32_t> bin_tmp;                          // binning block offsets
     gsr::DevBuf<uint32_t> tkeys_a, tkeys_b, tvals_a, tvals_b;  // tile sort (capacity D)
     gsr::DevBuf<uint32_t> radix_tmp;
@@ -195,6 +196,7 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
     if ((rc = c->vals_a.ensure(n, "vals"))) return rc;
     if ((rc = c->vals_b.ensure(n, "vals"))) return rc;
     if ((rc = c->trect.ensure(n, "trect"))) return rc;
+    if ((rc = c->trect_sorted.ensure(n, "trect_sorted"))) return rc;
     if ((rc = c->bin_tmp.ensure(bin_tmp_elems(n), "bin_tmp"))) return rc;
     if ((rc = c->radix_tmp.ensure(radix_tmp_elems(n), "radix_tmp"))) return rc;
     if (!c->done_ctr.p) {
@@ -394,7 +396,7 @@ int gsr_context_destroy(gsr_context* c) {
     c->vis_mask.release(); c->wave_counts.release(); c->scan_tmp.release(); c->recs.release();
     c->block_ranges.release();
     c->keys_a.release(); c->keys_b.release(); c->vals_a.release(); c->vals_b.release();
-    c->trect.release(); c->bin_tmp.release(); c->tkeys_a.release(); c->tkeys_b.release(); c->tvals_a.release();
+    c->trect.release(); c->trect_sorted.release(); c->bin_tmp.release(); c->tkeys_a.release(); c->tkeys_b.release(); c->tvals_a.release();
     c->tvals_b.release(); c->radix_tmp.release(); c->zero.release();
     c->chunk_cnt.release(); c->chunk_base.release();
     c->chunk_desc.release(); c->partial.release();
@@ -484,7 +486,8 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
         if ((rc = c->tvals_b.ensure(n_dup, "tile_vals"))) return rc;
         if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(n_dup), radix_tmp_elems(n)), "radix_tmp")))
             return rc;
-        if ((rc = launch_binning(va, c->trect.p, n_vis, u.tiles_x, c->bin_tmp.p, c->tkeys_a.p, c->tvals_a.p, s)))
+        if ((rc = launch_binning(va, c->trect.p, n_vis, u.tiles_x, c->bin_tmp.p, c->trect_sorted.p, c->tkeys_a.p,
+                                 c->tvals_a.p, s)))
             return rc;
     }
     if ((rc = prof_record(c, slot, EV_COUNTS, s))) return rc;

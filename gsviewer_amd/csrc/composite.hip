@@ -32,9 +32,12 @@ __device__ __forceinline__ uint32_t rect_tiles(uint2 tr) {
     return (tx0 <= tx1) ? (tx1 - tx0 + 1) * (ty1 - ty0 + 1) : 0u;
 }
 
+// Also writes the gathered rects in depth order (trect_sorted), so that
+// k_bin_write reads them coalesced instead of gathering them a second time.
 __global__ __launch_bounds__(kThreads) void k_bin_reduce(const uint32_t* __restrict__ sorted_ids,
                                                          const uint2* __restrict__ trect, uint32_t n_vis,
-                                                         uint32_t* __restrict__ block_sums) {
+                                                         uint32_t* __restrict__ block_sums,
+                                                         uint2* __restrict__ trect_sorted) {
     __shared__ uint32_t lds[kThreads / 64];
     const uint32_t base = blockIdx.x * kBinBlock + threadIdx.x;
     uint32_t s = 0;
@@ -43,7 +46,10 @@ __global__ __launch_bounds__(kThreads) void k_bin_reduce(const uint32_t* __restr
         const uint32_t r = base + k * kThreads;
         if (r < n_vis) {
             const uint32_t id = sorted_ids[r];
-            s += id < n_vis ? rect_tiles(trect[id]) : 0u;  // (ids are < n_vis by construction)
+            // (ids are < n_vis by construction)
+            const uint2 tr = id < n_vis ? trect[id] : make_uint2(0xffffu, 0u);
+            trect_sorted[r] = tr;
+            s += rect_tiles(tr);
         }
     }
     s = wave_reduce_sum(s);
@@ -55,7 +61,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_reduce(const uint32_t* __restr
 // Exclusive offsets of the block's splats (block prefix + in-block scan), then
 // one (tile key, record slot) instance per covered tile, row-major.
 __global__ __launch_bounds__(kThreads) void k_bin_write(const uint32_t* __restrict__ sorted_ids,
-                                                        const uint2* __restrict__ trect, uint32_t n_vis,
+                                                        const uint2* __restrict__ trect_sorted, uint32_t n_vis,
                                                         const uint32_t* __restrict__ block_off, int tiles_x,
                                                         uint32_t* __restrict__ tile_keys,
                                                         uint32_t* __restrict__ tile_vals) {
@@ -71,7 +77,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_write(const uint32_t* __restri
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
-        tr[k] = (base + k < n_vis && id[k] < n_vis) ? trect[id[k]] : make_uint2(0xffffu, 0u);
+        tr[k] = (base + k < n_vis) ? trect_sorted[base + k] : make_uint2(0xffffu, 0u);
         s += rect_tiles(tr[k]);
     }
     const int w = threadIdx.x >> 6;
@@ -689,14 +695,14 @@ extern "C" int64_t gsr_debug_comp_trace(void* host_dst, int64_t max_entries) {
 size_t bin_tmp_elems(size_t n_vis) { return (n_vis + kBinBlock - 1) / kBinBlock + 1; }
 
 int launch_binning(const uint32_t* sorted_ids, const uint2* trect, uint32_t n_vis, int tiles_x, uint32_t* tmp,
-                   uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s) {
+                   uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s) {
     if (n_vis == 0) return GSR_OK;
     const uint32_t nb = (n_vis + kBinBlock - 1) / kBinBlock;
-    k_bin_reduce<<<nb, kThreads, 0, s>>>(sorted_ids, trect, n_vis, tmp);
+    k_bin_reduce<<<nb, kThreads, 0, s>>>(sorted_ids, trect, n_vis, tmp, trect_sorted);
     GSR_LAUNCH_CHECK("bin_reduce");
     int rc = scan_exclusive(tmp, tmp, nb, nullptr, nullptr, s);
     if (rc) return rc;
-    k_bin_write<<<nb, kThreads, 0, s>>>(sorted_ids, trect, n_vis, tmp, tiles_x, tile_keys, tile_vals);
+    k_bin_write<<<nb, kThreads, 0, s>>>(sorted_ids, trect_sorted, n_vis, tmp, tiles_x, tile_keys, tile_vals);
     GSR_LAUNCH_CHECK("bin_write");
     return GSR_OK;
 }

@@ -195,8 +195,10 @@ int launch_depth_keys_all(const SceneData& sd, const float* V, uint32_t* keys, h
 
 // composite.hip
 size_t bin_tmp_elems(size_t n_vis);
+// trect_sorted: n_vis uint2 of scratch (the rects in depth order)
 int launch_binning(const uint32_t* sorted_ids, const uint2* trect, uint32_t n_vis, int tiles_x,
-                   uint32_t* tmp, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s);
+                   uint32_t* tmp, uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals,
+                   hipStream_t s);
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
                        hipStream_t s);
 // chunk_cnt must hold num_tiles + num_tiles / 256 + 1 entries (block totals after the tiles)
