@@ -25,6 +25,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+SIMDS = 256 * 4        # MI355X CUs x SIMDs
+CLOCK_HZ = 2.4e9       # MI355X engine clock (MI355X_MICROARCH.md)
 
 CONFIGS = {
     # name: (N, sh_degree, width, height, description)
@@ -45,6 +47,19 @@ def make_scene(cfg, n, deg):
         return random_scene(n, sh_degree=deg, seed=0), "synthetic: random uniform (seed 0)"
     seed = 2 if cfg == "c3" else 1
     return garden_standin(n, seed=seed, sh_degree=deg), f"synthetic: garden stand-in (seed {seed}), no PLY offline"
+
+
+def box_settings(g, kind):
+    """SURVEY.md 8d C5 box cull settings (RenderSettings fields)."""
+    if kind == "aabb":
+        lo, hi, _ = g.compute_aabb
+        return dict(enable_aabb=1, cube_min=[float(v) for v in np.float32(lo) * np.float32(0.5)],
+                    cube_max=[float(v) for v in np.float32(hi) * np.float32(0.5)],
+                    points_center=[float(v) for v in g.points_center.astype(np.float32)])
+    from gsviewer_amd.camera import euler_to_rotation_matrix
+    return dict(enable_obb=1, cube_rotation=euler_to_rotation_matrix([30.0, 15.0, 0.0]).tolist(),
+                cube_min=[-1.5, -1.5, -1.5], cube_max=[1.5, 1.5, 1.5],
+                points_center=[float(v) for v in g.points_center.astype(np.float32)])
 
 
 def cpu_baseline(g, cam, seconds):
@@ -80,24 +95,43 @@ KERNEL_SYMBOL = {"composite": "k_composite<0>", "preprocess": "k_preprocess<3>",
 PMC_PROFILE = os.path.join(ROOT, "profiles", "LATEST")
 
 
-def pmc_traffic(kernel, args):
-    """HBM bytes per launch of `kernel` (FETCH_SIZE, doubled per the gfx950
-    correction, + WRITE_SIZE) from the committed rocprofv3 --pmc summary of
-    this same bench command (profiles/<LATEST>/pmc_summary.csv, written by
-    tools/gpu_round.sh).  PMC collection needs its own profiler pass, so it is
-    read back here rather than measured inside the timed region."""
-    if kernel is None or args.config != "c2" or args.n or args.width or args.height:
-        return None
+def pmc_counters(kernel, args):
+    """Per-dispatch PMC counters of `kernel` from the committed rocprofv3 --pmc
+    summary of this same bench command (profiles/<LATEST>/pmc_summary.csv,
+    written by tools/gpu_round.sh; FETCH_SIZE already doubled per the gfx950
+    correction).  PMC collection needs its own profiler passes, so the values
+    are read back here rather than measured inside the timed region."""
+    if kernel is None or args.config != "c2" or args.n or args.width or args.height or args.box != "none":
+        return None, None
     try:
         d = open(PMC_PROFILE).read().strip()
         path = os.path.join(ROOT, "profiles", d, "pmc_summary.csv")
         rows = [ln.strip().split(",") for ln in open(path).read().splitlines()[1:]]
     except OSError:
+        return None, None
+    return {r[1]: float(r[4]) for r in rows if r[0].strip('"') == kernel}, f"profiles/{d}/pmc_summary.csv ({kernel})"
+
+
+def pmc_traffic(kernel, args):
+    """HBM bytes per launch (FETCH_SIZE + WRITE_SIZE) of `kernel`."""
+    got, src = pmc_counters(kernel, args)
+    if not got or "FETCH_SIZE" not in got or "WRITE_SIZE" not in got:
         return None
-    got = {r[1]: float(r[4]) for r in rows if r[0].strip('"') == kernel}
-    if "FETCH_SIZE" not in got or "WRITE_SIZE" not in got:
+    return got["FETCH_SIZE"] + got["WRITE_SIZE"], src
+
+
+def valu_issue(kernel, args, ms_per_launch):
+    """The compositor's real limiter: VALU issue.  A wave64 VALU instruction
+    occupies its SIMD for 4 cycles, a transcendental (v_exp_f32) for 16;
+    MI355X has 256 CUs x 4 SIMDs at ~2.4 GHz (MI355X_MICROARCH.md)."""
+    got, src = pmc_counters(kernel, args)
+    if not got or "SQ_INSTS_VALU" not in got:
         return None
-    return got["FETCH_SIZE"] + got["WRITE_SIZE"], f"profiles/{d}/pmc_summary.csv ({kernel})"
+    valu, trans = got["SQ_INSTS_VALU"], got.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
+    cycles = 4.0 * (valu - trans) + 16.0 * trans
+    t_issue = cycles / (SIMDS * CLOCK_HZ)
+    return {"valu_instr_per_launch": valu, "trans_instr_per_launch": trans, "issue_us": t_issue * 1e6,
+            "launch_us": ms_per_launch * 1e3, "frac": t_issue / (ms_per_launch * 1e-3), "source": src}
 
 
 def main():
@@ -113,6 +147,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage HIP events")
+    ap.add_argument("--box", default="none", choices=["none", "aabb", "obb"],
+                    help="boundary-box cull (SURVEY.md 8d C5): aabb = compute_aabb min/max x 0.5 around "
+                         "points_center; obb = euler(30, 15, 0) deg, +-1.5")
     args = ap.parse_args()
 
     import torch
@@ -147,6 +184,14 @@ def main():
     cam = view_of(rank, H, W)
     camc = camera_from(cam)
     st = RenderSettings(t_min=args.t_min, out_layout=0)
+    if args.box != "none":
+        box = box_settings(g, args.box) if rank == 0 else None
+        if world > 1:
+            obj = [box]
+            dist.broadcast_object_list(obj, src=0)
+            box = obj[0]
+        for k, v in box.items():
+            setattr(st, k, v)
     ctx = HipContext()
     lib = _lib.load()
     out = torch.empty((3, H, W), dtype=torch.float32, device=dev)
@@ -223,6 +268,8 @@ def main():
         traffic = pmc_traffic(KERNEL_SYMBOL.get(dom), args)
         if traffic:
             roof["traffic"], roof["traffic_source"] = traffic
+        if dom == "composite":
+            roof["valu_issue"] = valu_issue(KERNEL_SYMBOL[dom], args, stage[dom])
 
     cpu = None
     if not args.no_cpu_baseline and world == 1 and g is not None:
@@ -244,7 +291,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": data_desc,
-        "config": {"workload": desc, "n_gaussians": n, "sh_degree": deg, "width": W, "height": H,
+        "config": {"workload": desc + ("" if args.box == "none" else f", {args.box.upper()} box cull"),
+                   "n_gaussians": n, "sh_degree": deg, "width": W, "height": H,
                    "views": "view k = default camera yawed k*45 deg (one per GPU)", "t_min": args.t_min,
                    "parallelism": f"replicated scene, {world} independent views"},
         "frame_stats": stats,

@@ -31,12 +31,13 @@ if [ "$MODE" = quick ]; then
 else
     step bench 300 bash -c "python bench.py > $O/bench.json 2> $O/bench.err"
 fi
-step rocprof_stats 240 rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- $B
+step rocprof_stats 240 bash -c "rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- $B > $O/bench_under_rocprof.json 2> $O/rocprof.err"
 find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \;
 if [ "$MODE" != quick ]; then
-    step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o pmc --output-format csv -- $B
-    step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o pmc --output-format csv -- $B
+    step pmc_fetch 240 bash -c "rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o pmc --output-format csv -- $B > $O/pmc_fetch.log 2>&1"
+    step pmc_write 240 bash -c "rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o pmc --output-format csv -- $B > $O/pmc_write.log 2>&1"
+    step pmc_valu 240 bash -c "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_WAVES -d $O/pmc_valu -o pmc --output-format csv -- $B > $O/pmc_valu.log 2>&1"
     python profiles/summarize_pmc.py $O/pmc_summary.csv \
-        $(find $O/pmc_fetch $O/pmc_write -name '*counter_collection.csv' -printf '%h\n' | sort -u)
+        $(find $O/pmc_fetch $O/pmc_write $O/pmc_valu -name '*counter_collection.csv' -printf '%h\n' | sort -u)
 fi
 echo "[gpu_round] done"
