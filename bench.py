@@ -146,11 +146,20 @@ def main():
     ap.add_argument("--t-min", type=float, default=1e-4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=4,
+                    help="independent views in flight per GPU (own stream and context each); 1 = one at a time")
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage HIP events")
     ap.add_argument("--box", default="none", choices=["none", "aabb", "obb"],
                     help="boundary-box cull (SURVEY.md 8d C5): aabb = compute_aabb min/max x 0.5 around "
                          "points_center; obb = euler(30, 15, 0) deg, +-1.5")
     args = ap.parse_args()
+
+    # One hardware queue per in-flight view stream (+ torch's own): HIP maps
+    # streams round-robin onto GPU_MAX_HW_QUEUES queues (4 by default), and two
+    # view streams sharing a queue serialise.  Must be set before HIP starts.
+    want_q = min(32, max(8, args.inflight + 2))
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < want_q:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
 
     import torch
     import torch.distributed as dist
@@ -192,23 +201,42 @@ def main():
             box = obj[0]
         for k, v in box.items():
             setattr(st, k, v)
-    ctx = HipContext()
     lib = _lib.load()
-    out = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+    # K independent views in flight on K streams (one context and output per
+    # view): frame i renders view i mod K.  Rank r's views are r + world*j.
+    K = max(1, args.inflight)
+    ctxs = [HipContext() for _ in range(K)]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(K)]
+    outs = [torch.empty((3, H, W), dtype=torch.float32, device=dev) for _ in range(K)]
+    cams = [cam] + [view_of(rank + world * j, H, W) for j in range(1, K)]
+    camcs = [camera_from(c) for c in cams]
+    ctx = ctxs[0]
+    frame_no = [0]
 
-    for _ in range(args.warmup):
-        render_into(ctx, scene, camc, st, out)
+    def batched_frame():
+        k = frame_no[0] % K
+        frame_no[0] += 1
+        with torch.cuda.stream(streams[k]):
+            render_into(ctxs[k], scene, camcs[k], st, outs[k])
+
+    def serial_frame():
+        render_into(ctx, scene, camc, st, outs[0])
+
+    for _ in range(max(args.warmup, K)):
+        batched_frame()
     torch.cuda.synchronize()
 
     # barrier + synchronize on both sides; MAX over ranks.  No instrumentation
     # inside: every HIP event record stalls the stream for several us.
-    elapsed = timed_region(lambda: render_into(ctx, scene, camc, st, out), args.steps, dev)
+    elapsed = timed_region(batched_frame, args.steps, dev)
+    # single-view latency: the same number of frames of view 0, one at a time
+    latency = timed_region(serial_frame, args.steps, dev) if K > 1 else elapsed
 
-    # Per-stage times: a second region of the same frames with libgsr's HIP
-    # events recorded on the render stream between the stages.
+    # Per-stage times: a third region (view 0, one at a time) with libgsr's
+    # HIP events recorded on the render stream between the stages.
     if not args.no_profile:
         _lib.check(lib.gsr_context_set_profiling(ctx.handle, 1), "set_profiling")
-        prof_elapsed = timed_region(lambda: render_into(ctx, scene, camc, st, out), args.steps, dev)
+        prof_elapsed = timed_region(serial_frame, args.steps, dev)
 
     stats = ctx.stats()
     # tile-list length distribution of the last frame (load balance of the compositor)
@@ -235,6 +263,8 @@ def main():
             dist.destroy_process_group()
         return
 
+    for c in ctxs[1:]:
+        c.close()
     ms_per_step = 1e3 * elapsed / args.steps
     fps = args.steps / elapsed
     value = n * args.steps * world / elapsed
@@ -285,16 +315,21 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "fps_per_gpu": fps,
+        "latency_ms_per_frame": 1e3 * latency / args.steps,
+        "views_in_flight": K,
         "splats_per_s_per_gpu": value / world,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": data_desc,
-        "config": {"workload": desc + ("" if args.box == "none" else f", {args.box.upper()} box cull"),
+        "config": {"workload": desc + ("" if args.box == "none" else f", {args.box.upper()} box cull")
+                   + (f", {K} views in flight per GPU" if K > 1 else ""),
                    "n_gaussians": n, "sh_degree": deg, "width": W, "height": H,
-                   "views": "view k = default camera yawed k*45 deg (one per GPU)", "t_min": args.t_min,
-                   "parallelism": f"replicated scene, {world} independent views"},
+                   "views": f"view v = default camera yawed v*45 deg; rank r renders v = r + {world}*j, j < {K}, "
+                            f"round-robin, one stream per view",
+                   "t_min": args.t_min,
+                   "parallelism": f"replicated scene, {world * K} independent views ({K} per GPU in flight)"},
         "frame_stats": stats,
         "stage_ms": stage,
         "roofline": roof,
