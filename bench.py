@@ -147,7 +147,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=4,
-                    help="independent views in flight per GPU (own stream and context each); 1 = one at a time")
+                    help="independent views in flight per GPU (own stream and context each, pipelined with "
+                         "gsr_render_begin/finish); 1 = one at a time")
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage HIP events")
     ap.add_argument("--box", default="none", choices=["none", "aabb", "obb"],
                     help="boundary-box cull (SURVEY.md 8d C5): aabb = compute_aabb min/max x 0.5 around "
@@ -173,7 +174,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from gsviewer_amd import _lib
-    from gsviewer_amd.multiview import broadcast_scene, timed_region, view_of
+    from gsviewer_amd.multiview import ViewPipeline, broadcast_scene, timed_region, view_of
     from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into
 
     _lib.load()
@@ -211,24 +212,25 @@ def main():
     cams = [cam] + [view_of(rank + world * j, H, W) for j in range(1, K)]
     camcs = [camera_from(c) for c in cams]
     ctx = ctxs[0]
-    frame_no = [0]
-
-    def batched_frame():
-        k = frame_no[0] % K
-        frame_no[0] += 1
-        with torch.cuda.stream(streams[k]):
-            render_into(ctxs[k], scene, camcs[k], st, outs[k])
+    pipe = ViewPipeline(ctxs, streams, scene, camcs, st, outs)
 
     def serial_frame():
         render_into(ctx, scene, camc, st, outs[0])
 
     for _ in range(max(args.warmup, K)):
-        batched_frame()
+        pipe.step()
+    pipe.drain()
     torch.cuda.synchronize()
 
     # barrier + synchronize on both sides; MAX over ranks.  No instrumentation
-    # inside: every HIP event record stalls the stream for several us.
-    elapsed = timed_region(batched_frame, args.steps, dev)
+    # inside: every HIP event record stalls the stream for several us.  Every
+    # begun frame is finished (drain) before the closing synchronize.
+    def pipelined(steps):
+        for _ in range(steps):
+            pipe.step()
+        pipe.drain()
+
+    elapsed = timed_region(lambda: pipelined(args.steps), 1, dev)
     # single-view latency: the same number of frames of view 0, one at a time
     latency = timed_region(serial_frame, args.steps, dev) if K > 1 else elapsed
 

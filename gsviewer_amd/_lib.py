@@ -97,8 +97,11 @@ SIGNATURES = {
     "gsr_context_create": (ctypes.c_int, [ctypes.POINTER(_P)]),
     "gsr_context_destroy": (ctypes.c_int, [_P]),
     "gsr_render": (ctypes.c_int, [_P, _P, ctypes.POINTER(GsrCamera), ctypes.POINTER(GsrSettings), _P, _P, _P]),
+    "gsr_render_begin": (ctypes.c_int, [_P, _P, ctypes.POINTER(GsrCamera), ctypes.POINTER(GsrSettings), _P, _P, _P]),
+    "gsr_render_finish": (ctypes.c_int, [_P, _P]),
     "gsr_context_stats": (ctypes.c_int, [_P, ctypes.POINTER(GsrFrameStats)]),
     "gsr_sort_depth": (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_float * 16), _P, _P]),
+    "gsr_debug_host_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "gsr_debug_sort_pairs": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _P, _P, _P]),
     "gsr_debug_copy": (ctypes.c_int64, [_P, ctypes.c_int32, _P, ctypes.c_int64, _P]),
     "gsr_context_set_profiling": (ctypes.c_int, [_P, ctypes.c_int32]),

@@ -62,6 +62,22 @@ struct DevBuf {
 }  // namespace
 }  // namespace gsr
 
+namespace gsr {
+// A frame between gsr_render_begin and gsr_render_finish.
+struct PendingFrame {
+    bool active = false;
+    FrameUniforms u{};
+    float t_min = 0.f;
+    float bg[3] = {0.f, 0.f, 0.f};
+    int32_t out_layout = 0;
+    float* out = nullptr;
+    hipStream_t stream = nullptr;
+    size_t n = 0;
+    int slot = 0;
+    uint32_t *ka = nullptr, *va = nullptr, *kb = nullptr, *vb = nullptr;  // depth sort buffers (result in ka/va)
+};
+}  // namespace gsr
+
 struct gsr_context {
     gsr::DevBuf<uint64_t> vis_mask;
     gsr::DevBuf<uint32_t> wave_counts;
@@ -96,6 +112,9 @@ struct gsr_context {
     bool ev_pending[2] = {false, false};
     int64_t frame_idx = 0;
     double acc_ms[GSR_NUM_STAGES] = {};
+    gsr::PendingFrame pend;
+    double host_ms[3] = {};  // host time in gsr_render: enqueue before the wait, the wait, enqueue after
+    int64_t host_frames = 0;
     int64_t prof_frames = 0;
 };
 
@@ -416,10 +435,12 @@ int gsr_context_stats(const gsr_context* c, gsr_frame_stats* out) {
     return GSR_OK;
 }
 
-int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, float* out,
-               int32_t* radii, void* stream) {
+int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, float* out,
+                     int32_t* radii, void* stream) {
     if (!c || !sc || !cam || !st || !out) return set_error(GSR_ERR_INVALID, "null argument");
+    if (c->pend.active) return set_error(GSR_ERR_INVALID, "render_begin: the previous frame was not finished");
     hipStream_t s = (hipStream_t)stream;
+    const auto h0 = std::chrono::steady_clock::now();
     FrameUniforms u;
     int rc = build_uniforms(sc, cam, st, u);
     if (rc) return rc;
@@ -429,8 +450,6 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
     const ZeroLayout zl(num_tiles);
     if ((rc = c->zero.ensure(zl.total, "zero block"))) return rc;
     uint32_t* counters = c->zero.p + zl.counters;
-    uint2* ranges = reinterpret_cast<uint2*>(c->zero.p + zl.ranges);
-    uint32_t* sat = c->zero.p + zl.sat;
     const int slot = (int)(c->frame_idx & 1);
     if (c->prof_on) prof_accumulate(c, slot, true);  // slot reuse: frame k-2 is long done
 
@@ -440,7 +459,7 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
     c->stats.tiles_y = u.tiles_y;
     c->last_depth_order = c->last_tile_list = nullptr;
     c->last_tiles = num_tiles;
-    c->last_ranges = ranges;
+    c->last_ranges = reinterpret_cast<uint2*>(c->zero.p + zl.ranges);
 
     if ((rc = prof_record(c, slot, EV_START, s))) return rc;
     if (n == 0) GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * zl.total, s));
@@ -465,18 +484,50 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
     if ((rc = prof_record(c, slot, EV_AFTER_SYNC1, s))) return rc;
 
     // depth sort over the upper bound N; the device count V bounds the work
-    uint32_t *ka = c->keys_a.p, *kb = c->keys_b.p, *va = c->vals_a.p, *vb = c->vals_b.p;
-    if (n > 0 && (rc = sort_pairs(c, &ka, &va, &kb, &vb, true, n, counters + 0, 32, kDepthPasses,
+    PendingFrame& f = c->pend;
+    f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
+    if (n > 0 && (rc = sort_pairs(c, &f.ka, &f.va, &f.kb, &f.vb, true, n, counters + 0, 32, kDepthPasses,
                                   c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_DSORT, s))) return rc;
+    f.active = true;
+    f.u = u;
+    f.t_min = st->t_min;
+    std::memcpy(f.bg, st->bg, sizeof(f.bg));
+    f.out_layout = st->out_layout;
+    f.out = out;
+    f.stream = s;
+    f.n = n;
+    f.slot = slot;
+    c->host_ms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+    return GSR_OK;
+}
+
+int gsr_render_finish(gsr_context* c, void* stream) {
+    if (!c) return set_error(GSR_ERR_INVALID, "null argument");
+    PendingFrame& f = c->pend;
+    if (!f.active) return set_error(GSR_ERR_INVALID, "render_finish: no frame was begun");
+    if ((hipStream_t)stream != f.stream) return set_error(GSR_ERR_INVALID, "render_finish: not the frame's stream");
+    f.active = false;
+    hipStream_t s = f.stream;
+    const FrameUniforms& u = f.u;
+    const size_t n = f.n;
+    const int slot = f.slot;
+    const int num_tiles = u.tiles_x * u.tiles_y;
+    const ZeroLayout zl(num_tiles);
+    uint32_t* counters = c->zero.p + zl.counters;
+    uint2* ranges = reinterpret_cast<uint2*>(c->zero.p + zl.ranges);
+    uint32_t* sat = c->zero.p + zl.sat;
+    int rc;
 
     // host: V and D (the GPU is busy with the depth sort meanwhile)
+    const auto h1 = std::chrono::steady_clock::now();
     if (n > 0 && (rc = wait_counts(c, s))) return rc;
+    const auto h2 = std::chrono::steady_clock::now();
     const uint32_t n_vis = n > 0 ? __atomic_load_n(&c->host_counters[0], __ATOMIC_ACQUIRE) : 0u;
     const uint32_t n_dup = n > 0 ? __atomic_load_n(&c->host_counters[1], __ATOMIC_ACQUIRE) : 0u;
     if (c->prof_on) prof_accumulate(c, slot ^ 1, false);
-    if (n_vis > 0) c->last_depth_order = va;
+    if (n_vis > 0) c->last_depth_order = f.va;
 
     uint32_t* tile_list = c->tvals_a.p;
     if (n_dup > 0) {
@@ -486,7 +537,7 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
         if ((rc = c->tvals_b.ensure(n_dup, "tile_vals"))) return rc;
         if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(n_dup), radix_tmp_elems(n)), "radix_tmp")))
             return rc;
-        if ((rc = launch_binning(va, c->trect.p, n_vis, u.tiles_x, c->bin_tmp.p, c->trect_sorted.p, c->tkeys_a.p,
+        if ((rc = launch_binning(f.va, c->trect.p, n_vis, u.tiles_x, c->bin_tmp.p, c->trect_sorted.p, c->tkeys_a.p,
                                  c->tvals_a.p, s)))
             return rc;
     }
@@ -517,19 +568,33 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
         return rc;
     if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
     if ((rc = launch_composite(c->chunk_desc.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
-                               sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), st->t_min, st->bg,
-                               st->out_layout, out, c->partial.p, c->tmax.p, s)))
+                               sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.t_min, f.bg,
+                               f.out_layout, f.out, c->partial.p, c->tmax.p, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_COMPOSITE, s))) return rc;
-    if ((rc = launch_merge(c->chunk_cnt.p, c->chunk_base.p, c->partial.p, sat, u, st->t_min, st->bg, st->out_layout,
-                           out, s)))
+    if ((rc = launch_merge(c->chunk_cnt.p, c->chunk_base.p, c->partial.p, sat, u, f.t_min, f.bg, f.out_layout,
+                           f.out, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_COUNT, s))) return rc;
     if (c->prof_on) c->ev_pending[slot] = true;
+    {
+        const auto h3 = std::chrono::steady_clock::now();
+        using ms = std::chrono::duration<double, std::milli>;
+        c->host_ms[1] += ms(h2 - h1).count();
+        c->host_ms[2] += ms(h3 - h2).count();
+        c->host_frames += 1;
+    }
     c->frame_idx += 1;
     c->stats.n_visible = n_vis;
     c->stats.n_instances = n_dup;
     return GSR_OK;
+}
+
+int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, float* out,
+               int32_t* radii, void* stream) {
+    int rc = gsr_render_begin(c, sc, cam, st, out, radii, stream);
+    if (rc) return rc;
+    return gsr_render_finish(c, stream);
 }
 
 int gsr_context_set_profiling(gsr_context* c, int32_t enable) {
@@ -550,6 +615,13 @@ int gsr_context_stage_times(gsr_context* c, double* ms_out, int64_t* frames_out)
     for (int k = 0; k < 2; ++k) prof_accumulate(c, (int)((c->frame_idx + k) & 1), true);
     for (int k = 0; k < GSR_NUM_STAGES; ++k) ms_out[k] = c->acc_ms[k];
     if (frames_out) *frames_out = c->prof_frames;
+    return GSR_OK;
+}
+
+int gsr_debug_host_times(const gsr_context* c, double ms_out[3], int64_t* frames_out) {
+    if (!c || !ms_out) return set_error(GSR_ERR_INVALID, "null argument");
+    for (int k = 0; k < 3; ++k) ms_out[k] = c->host_ms[k];
+    if (frames_out) *frames_out = c->host_frames;
     return GSR_OK;
 }
 

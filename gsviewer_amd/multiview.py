@@ -102,3 +102,39 @@ def _sync(device) -> None:
     dev = torch.device(device)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+
+
+class ViewPipeline:
+    """Several independent views in flight on one GPU, one context and stream
+    each.  step() renders the next frame round-robin: it finishes that view's
+    previous frame (gsr_render_finish: host wait for its counts, then the
+    binning, tile sort and compositing launches) and begins its next one
+    (gsr_render_begin: culling, preprocess, depth sort).  A view's counts are
+    therefore waited on only after the other views' frames have been
+    enqueued, so the GPU always has work queued.  drain() finishes every
+    pending frame; a frame counts once begun, and is complete after drain()
+    and a device synchronize."""
+
+    def __init__(self, ctxs, streams, scene, cams, settings, outs):
+        assert len(ctxs) == len(streams) == len(cams) == len(outs) >= 1
+        self.ctxs, self.streams, self.scene, self.cams = ctxs, streams, scene, cams
+        self.settings, self.outs = settings, outs
+        self.pending = [False] * len(ctxs)
+        self.next = 0
+
+    def step(self):
+        from .rasterizer import render_begin, render_finish
+        k = self.next
+        self.next = (k + 1) % len(self.ctxs)
+        s = self.streams[k]
+        if self.pending[k]:
+            render_finish(self.ctxs[k], s)
+        render_begin(self.ctxs[k], self.scene, self.cams[k], self.settings, self.outs[k], stream=s)
+        self.pending[k] = True
+
+    def drain(self):
+        from .rasterizer import render_finish
+        for k, p in enumerate(self.pending):
+            if p:
+                render_finish(self.ctxs[k], self.streams[k])
+                self.pending[k] = False

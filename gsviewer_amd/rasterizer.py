@@ -211,6 +211,29 @@ def render_into(ctx: HipContext, scene: HipScene, cam: _lib.GsrCamera, settings:
     return out
 
 
+def render_begin(ctx: HipContext, scene: HipScene, cam: _lib.GsrCamera, settings: RenderSettings,
+                 out: torch.Tensor, radii: Optional[torch.Tensor] = None, stream=None):
+    """First half of render_into (gsr_render_begin): enqueue culling,
+    preprocess and the depth sort without waiting.  Finish with render_finish
+    on the same stream; meanwhile begin other views' frames on their own
+    contexts and streams."""
+    if not (out.is_cuda and out.dtype == torch.float32 and out.is_contiguous()):
+        raise RuntimeError("out must be a contiguous float32 CUDA tensor")
+    if out.numel() != 3 * cam.width * cam.height:
+        raise RuntimeError("out has the wrong number of elements")
+    rp = ctypes.c_void_p(radii.data_ptr()) if radii is not None else None
+    st = settings.to_c()
+    _lib.check(_lib.load().gsr_render_begin(ctx.handle, scene.handle, ctypes.byref(cam), ctypes.byref(st),
+                                            ctypes.c_void_p(out.data_ptr()), rp, _stream_handle(stream)),
+               "gsr_render_begin")
+    return out
+
+
+def render_finish(ctx: HipContext, stream=None):
+    """Second half of render_into (gsr_render_finish)."""
+    _lib.check(_lib.load().gsr_render_finish(ctx.handle, _stream_handle(stream)), "gsr_render_finish")
+
+
 _default_ctx = {}
 
 

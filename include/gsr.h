@@ -134,6 +134,18 @@ int gsr_render(gsr_context* ctx, const gsr_scene* scene, const gsr_camera* cam,
                const gsr_settings* settings, float* out_image_dev, int32_t* radii_dev,
                void* stream);
 
+/* gsr_render in two halves, for callers that keep several independent views
+ * in flight (one context and stream each).  _begin enqueues culling,
+ * preprocess and the depth sort and returns at once; _finish waits (on the
+ * host) for the frame's visible/instance counts and enqueues the rest.  A
+ * caller begins the next view's frame before finishing this one, so the
+ * host never idles while the GPU could take more work.  One frame per
+ * context may be pending; _finish takes the same stream. */
+int gsr_render_begin(gsr_context* ctx, const gsr_scene* scene, const gsr_camera* cam,
+                     const gsr_settings* settings, float* out_image_dev, int32_t* radii_dev,
+                     void* stream);
+int gsr_render_finish(gsr_context* ctx, void* stream);
+
 int gsr_context_stats(const gsr_context* ctx, gsr_frame_stats* out);
 
 /* Back-to-front Gaussian order for a view matrix: the renderer_ogl
@@ -161,6 +173,11 @@ int gsr_context_set_profiling(gsr_context* ctx, int32_t enable);   /* resets the
 /* Sum of per-stage milliseconds over the profiled frames since the last reset
  * (waits for the last profiled frame's events). */
 int gsr_context_stage_times(gsr_context* ctx, double* ms_out /* [GSR_NUM_STAGES] */, int64_t* frames_out);
+
+/* Host time spent inside gsr_render on this context since creation, in ms:
+ * [0] enqueue before the wait for the frame's counts, [1] that wait,
+ * [2] enqueue after it; *frames_out = number of frames. */
+int gsr_debug_host_times(const gsr_context* ctx, double ms_out[3], int64_t* frames_out);
 
 /* Test hook: copy an internal array of the last gsr_render on `ctx` into
  * dst_dev (device memory, at most max_bytes). Returns the number of bytes

@@ -25,7 +25,7 @@ def header_functions():
 def test_header_declares_expected_entry_points():
     names = header_functions()
     for must in ("gsr_scene_create", "gsr_scene_create_flat", "gsr_scene_destroy", "gsr_context_create",
-                 "gsr_render", "gsr_sort_depth", "gsr_debug_sort_pairs", "gsr_last_error", "gsr_settings_default",
+                 "gsr_render", "gsr_render_begin", "gsr_render_finish", "gsr_sort_depth", "gsr_debug_sort_pairs", "gsr_debug_host_times", "gsr_last_error", "gsr_settings_default",
                  "gsr_ply_probe", "gsr_ply_read", "gsr_ply_write_3dgs", "gsr_points_center", "gsr_export_select"):
         assert must in names
 

@@ -46,6 +46,13 @@ for K in [int(a) for a in sys.argv[1:]]:
     h = np.array(host) * 1e3
     print(f"K={K}: {dt * 1e3:.4f} ms per frame; host per call mean {h.mean():.4f} ms, median {np.median(h):.4f}, "
           f"p90 {np.percentile(h, 90):.4f}", flush=True)
+    import ctypes
+    for k in range(K):
+        ms = (ctypes.c_double * 3)()
+        fr = ctypes.c_int64()
+        _lib.load().gsr_debug_host_times(ctxs[k].handle, ms, ctypes.byref(fr))
+        print(f"   view {k}: per frame enqueue-before {ms[0] / fr.value * 1e3:.1f} us, wait {ms[1] / fr.value * 1e3:.1f} us, "
+              f"enqueue-after {ms[2] / fr.value * 1e3:.1f} us", flush=True)
     # one host thread per view (ctypes releases the GIL inside gsr_render)
     import threading
 
