@@ -1,14 +1,14 @@
 #!/bin/bash
 # Bench lines for the other BASELINE.json configs (the driver's bench runs c2):
 # c1 (100k, deg 0, 640x480), c3 (6M, 1080p), c5 (1M, 4K) plain / AABB / OBB cull.
-# usage (GPU box): bash tools/bench_configs.sh OUT_DIR
+# usage (GPU box): [BENCH_EXTRA="--inflight 1"] bash tools/bench_configs.sh OUT_DIR
 O=${1:-gpurun_out/configs}
 mkdir -p $O
 run() {  # run NAME ARGS...
     local name=$1
     shift
     echo "[bench_configs] $name"
-    timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $O/$name.json 2> $O/$name.err || { echo "$name FAILED"; exit 1; }
+    timeout -k 10 300 python bench.py --no-cpu-baseline $BENCH_EXTRA "$@" > $O/$name.json 2> $O/$name.err || { echo "$name FAILED"; exit 1; }
 }
 run c1 --config c1
 run c3 --config c3 --steps 50
