@@ -8,9 +8,7 @@
 // ~26 of the 32 key bits, so 3 passes of 9 bits replace 4 passes of 8 and the
 // host never has to know B.
 //
-// One pass = three launches over tiles of 256*R items (R = 4 at these sizes:
-// ~1000 tiles per million keys keep every CU busy and the latency chains of
-// 2-4 resident tiles per CU overlapped):
+// One pass = three launches over tiles of 256*R items:
 //   k_rs_upsweep   per-tile digit counts (wave ballot digit matching, no
 //                  atomics), stored digit-major: hist[d * ntiles + tile];
 //   k_rs_offsets   one wave per digit: exclusive scan of that digit's row
@@ -31,8 +29,12 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
-constexpr int kR = 4;                            // items per thread (64-item rounds per wave)
-constexpr int kTileItems = kThreads * kR;        // 1024
+// Items per thread (64-item rounds per wave) is a template parameter R: a
+// tile holds 256*R items.  Bigger tiles mean longer digit runs in the
+// scatter's writes and a smaller digit matrix; the host picks R = 8 for wide
+// digits (depth keys, up to 11 bits) and R = 16 for narrow ones (tile ids).
+constexpr int kRMin = 8;
+constexpr int kMinTileItems = kThreads * kRMin;  // sizes the digit matrix for any R
 constexpr int kMaxBits = 11;
 constexpr int kMaxRadix = 1 << kMaxBits;         // 2048
 constexpr int kDigitsPerThread = kMaxRadix / kThreads;  // 8
@@ -81,9 +83,11 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t digit, uint32_t w, bool
     return peers;
 }
 
+template <int kR>
 __global__ __launch_bounds__(kThreads) void k_rs_upsweep(const uint32_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ n_dev, uint32_t n_host,
                                                          PassArgs pa, uint32_t* __restrict__ hist, uint32_t ntiles) {
+    constexpr int kTileItems = kThreads * kR;
     __shared__ uint16_t h[kWaves][kMaxRadix];  // per-wave counts (<= 64*kR each)
     const Digit dg = digit_params(pa);
     const uint32_t radix = dg.mask + 1u;
@@ -139,11 +143,13 @@ __global__ __launch_bounds__(64) void k_rs_offsets(uint32_t* __restrict__ hist, 
     if (__lane_id() == 63) totals[d] = inc;
 }
 
+template <int kR>
 __global__ __launch_bounds__(kThreads) void k_rs_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, bool identity_vals,
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ n_dev,
     uint32_t n_host, PassArgs pa, const uint32_t* __restrict__ hist_off, const uint32_t* __restrict__ totals,
     uint32_t ntiles) {
+    constexpr int kTileItems = kThreads * kR;
     __shared__ uint32_t s_keys[kTileItems];
     __shared__ uint32_t s_vals[kTileItems];
     __shared__ uint16_t wcnt[kWaves][kMaxRadix];  // per-wave digit counts, then per-wave prefixes
@@ -258,7 +264,7 @@ __global__ __launch_bounds__(kThreads) void k_rs_scatter(
 }  // namespace
 
 size_t radix_tmp_elems(size_t n) {
-    const size_t nb = (n + kTileItems - 1) / kTileItems;
+    const size_t nb = (n + kMinTileItems - 1) / kMinTileItems;
     return (nb < 1 ? 1 : nb) * kMaxRadix;
 }
 
@@ -266,25 +272,23 @@ size_t radix_totals_elems() { return (size_t)kMaxRadix; }  // digit totals scrat
 
 int radix_passes_for(int bits) { return bits <= 0 ? 0 : (bits + kMaxBits - 1) / kMaxBits; }
 
-int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
-                     bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
-                     const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s) {
-    if (n == 0 || passes == 0) return GSR_OK;
-    if (n > 0xffffffffull - kTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
-    if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
-        return set_error(GSR_ERR_INVALID, "radix sort: digit width out of range");
+template <int kR>
+static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
+                       bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
+                       const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s) {
+    constexpr int kTileItems = kThreads * kR;
     const uint32_t nt = (uint32_t)((n + kTileItems - 1) / kTileItems);
     // upper bound of the radix over the passes (device-chosen widths never exceed it)
     const uint32_t radix_max = 1u << ((bits + passes - 1) / passes);
     bool ident = identity_vals;
     for (int p = 0; p < passes; ++p) {
         const PassArgs pa{key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p};
-        k_rs_upsweep<<<nt, kThreads, 0, s>>>(*keys_io, n_dev, (uint32_t)n, pa, tmp, nt);
+        k_rs_upsweep<kR><<<nt, kThreads, 0, s>>>(*keys_io, n_dev, (uint32_t)n, pa, tmp, nt);
         GSR_LAUNCH_CHECK("rs_upsweep");
         k_rs_offsets<<<radix_max, 64, 0, s>>>(tmp, nt, pa, totals);
         GSR_LAUNCH_CHECK("rs_offsets");
-        k_rs_scatter<<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev, (uint32_t)n, pa,
-                                             tmp, totals, nt);
+        k_rs_scatter<kR><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev, (uint32_t)n,
+                                                 pa, tmp, totals, nt);
         GSR_LAUNCH_CHECK("rs_scatter");
         ident = false;
         uint32_t* t = *keys_io; *keys_io = *keys_alt; *keys_alt = t;
@@ -293,5 +297,19 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
     return GSR_OK;
 }
 
-}  // namespace gsr
+int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
+                     bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
+                     const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s) {
+    if (n == 0 || passes == 0) return GSR_OK;
+    if (n > 0xffffffffull - 4 * kMinTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
+    if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
+        return set_error(GSR_ERR_INVALID, "radix sort: digit width out of range");
+    // measured on MI355X: 2048-item tiles for wide digits, 4096 for <= 8-bit digits
+    if ((bits + passes - 1) / passes <= 8)
+        return sort_passes<16>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes, key_range,
+                               tmp, totals, s);
+    return sort_passes<8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes, key_range, tmp,
+                          totals, s);
+}
 
+}  // namespace gsr

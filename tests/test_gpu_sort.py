@@ -1,6 +1,7 @@
 """The frame's radix sort on its own (C-ABI test hook gsr_debug_sort_pairs):
 stable (key, index) order must equal NumPy's stable argsort exactly, across
-sizes from one tile to ~1800 tiles, digit widths 6..11 bits and exact ties.
+sizes from one tile to ~1800 tiles (both tile sizes: 2048 items for wider
+digits, 4096 for <= 8-bit digits), digit widths 6..11 bits and exact ties.
 The depth-sort service and the in-frame sorts are checked against the
 reference in test_gpu_scale.py; this isolates the sort itself."""
 import ctypes
@@ -34,7 +35,7 @@ def ctx(gpu):
     c.close()
 
 
-@pytest.mark.parametrize("n", [1, 100, 1024, 1025, 70_001, 300_000, 1_817_600])
+@pytest.mark.parametrize("n", [1, 100, 1024, 1025, 2049, 4097, 70_001, 300_000, 1_817_600])
 @pytest.mark.parametrize("bits,passes", [(9, 1), (13, 2), (32, 3)])
 def test_sort_matches_stable_argsort(ctx, n, bits, passes):
     rng = np.random.default_rng(n * 31 + bits)
