@@ -122,13 +122,6 @@ struct gsr_context {
 namespace gsr {
 namespace {
 
-int frag_class_of(int mode) {
-    if (mode == -4 || mode == -1) return kFragBillboard;
-    if (mode == -5) return kFragFlatBall;
-    if (mode == -6) return kFragGaussBall;
-    return kFragGauss;
-}
-
 int build_uniforms(const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, FrameUniforms& u) {
     if (cam->width <= 0 || cam->height <= 0 || cam->width > 32768 || cam->height > 32768)
         return set_error(GSR_ERR_INVALID, "camera: width/height out of range");

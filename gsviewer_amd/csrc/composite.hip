@@ -435,7 +435,9 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
             // power*log2(e) = qa dx^2 + qb dx dy + qc dy^2 in pixel units
             // (gau_frag.glsl:37 with coordxy's scale folded in by the preprocess)
             const float dx = px - q0.x;
-            const float p0 = q1.x * dx * dx;
+            // kFragGauss: q2.w = mid, and p0 is shifted by it (interval form, SplatRec)
+            const float mid = FRAG == kFragGauss ? q2.w : 0.f;
+            const float p0 = FRAG == kFragGauss ? fmaf(q1.x * dx, dx, -mid) : q1.x * dx * dx;
             const float p1 = q1.y * dx;
             const float c2 = q1.z;
 #pragma unroll
@@ -446,7 +448,14 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                 // opacity where the pixel is covered, +0 elsewhere (bit mask, no compare)
                 const uint32_t covk = (uint32_t)__builtin_amdgcn_sbfe((int)rb, 4 * k, 1);
                 float alpha, fr = q2.x, fg = q2.y, fb = q2.z;
-                if (FRAG == kFragBillboard) {
+                if (FRAG == kFragGauss) {
+                    // pw' = pw - mid; keep <=> |pw'| <= -mid; alpha / 0.99 = clamp(s * 2^pw')
+                    const float dy = pyw[k] - q0.y;
+                    const float pw = (c2 * dy + p1) * dy + p0;
+                    const float e = __builtin_amdgcn_exp2f(pw);
+                    const float a1 = __builtin_amdgcn_fmed3f(__uint_as_float(covk & __float_as_uint(q0.z)) * e, 0.f, 1.f);
+                    alpha = (fabsf(pw) <= -mid) ? a1 : 0.0f;
+                } else if (FRAG == kFragBillboard) {
                     alpha = __uint_as_float(covk & 0x3f800000u);  // 1.0 or 0.0
                 } else {
                     const float dy = pyw[k] - q0.y;
@@ -470,7 +479,8 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                 cr[k] += fr * w;
                 cg[k] += fg * w;
                 cb[k] += fb * w;
-                T[k] = T[k] - w;
+                // kFragGauss: alpha = 0.99 * a1 (the colour already carries its 0.99)
+                T[k] = FRAG == kFragGauss ? fmaf(w, -0.99f, T[k]) : T[k] - w;
             }
         }
         if (t_min > 0.f) {

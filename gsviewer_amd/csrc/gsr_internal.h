@@ -27,13 +27,30 @@ struct alignas(16) SplatRec {
     float qa, qb, qc;   // falloff quadratic form (see above)
     uint32_t yspan;     // covered pixel rows r0 | r1 << 16, inclusive (image coords, row 0 = top)
     float r, g, b;      // colour varying (clamped to [0,1] unless mode -6)
-    float pad;
+    float mid;          // kFragGauss only (else 0): see below
 };
+// kFragGauss records carry the fragment's alpha in "interval form", so the
+// compositor tests both discards of gau_frag.glsl:38-42 with ONE compare and
+// gets min(0.99, .) from the clamp output modifier:
+//   a = opacity * 2^pw,  keep  <=>  pw <= 0  and  a >= 1/255
+//                              <=>  thr <= pw <= 0,  thr = -log2(255 * opacity)
+//   mid = thr / 2:         keep  <=>  |pw - mid| <= -mid
+//   min(0.99, a) = 0.99 * clamp(s * 2^(pw - mid), 0, 1),  s = sqrt(opacity / 255) / 0.99
+// so `opacity` holds s and r, g, b hold 0.99 * colour (the 0.99 of the alpha
+// is folded into the colour and into the transmittance update).  Other
+// fragment classes keep the plain opacity and colour, and mid = 0.
 static_assert(sizeof(SplatRec) == 48, "SplatRec must be 48 bytes");
 constexpr float kLog2e = 1.4426950408889634f;
 
 // Render-mode classes of the fragment stage (gau_frag.glsl:16-52).
 enum FragClass : int { kFragGauss = 0, kFragBillboard = 1, kFragFlatBall = 2, kFragGaussBall = 3 };
+
+__host__ __device__ constexpr int frag_class_of(int mode) {
+    return (mode == -4 || mode == -1) ? kFragBillboard
+           : mode == -5              ? kFragFlatBall
+           : mode == -6              ? kFragGaussBall
+                                     : kFragGauss;
+}
 
 // Everything the per-Gaussian stage needs, passed by value (kernarg).
 struct FrameUniforms {

@@ -375,7 +375,6 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     const bool nonempty = (x0 <= x1) && (r0 <= r1);
     rec.xspan = nonempty ? ((uint32_t)x0 | ((uint32_t)x1 << 16)) : 0xffffu;  // empty: x0 > x1
     rec.yspan = nonempty ? ((uint32_t)r0 | ((uint32_t)r1 << 16)) : 0xffffu;
-    rec.pad = 0.f;
 
     // colour varying
     const int mode = u.render_mod;
@@ -402,11 +401,19 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     rec.r = col.x;
     rec.g = col.y;
     rec.b = col.z;
+    rec.mid = 0.f;
+    if (frag_class_of(mode) == kFragGauss) {  // interval form (gsr_internal.h, SplatRec)
+        rec.mid = -0.5f * log2f(255.0f * po.w);
+        rec.opacity = sqrtf(po.w / 255.0f) / 0.99f;
+        rec.r = 0.99f * col.x;
+        rec.g = 0.99f * col.y;
+        rec.b = 0.99f * col.z;
+    }
 
     float4* dst = reinterpret_cast<float4*>(recs + slot);
     dst[0] = make_float4(rec.cx, rec.cy, rec.opacity, __uint_as_float(rec.xspan));
     dst[1] = make_float4(rec.qa, rec.qb, rec.qc, __uint_as_float(rec.yspan));
-    dst[2] = make_float4(rec.r, rec.g, rec.b, 0.f);
+    dst[2] = make_float4(rec.r, rec.g, rec.b, rec.mid);
     depth_keys[slot] = float_order_key(-pr.pv[2]);
     if (radii) {
         const float rr = ceilf(fmaxf(qs[0], qs[1]));

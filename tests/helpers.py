@@ -86,7 +86,22 @@ def decode_records(raw):
     u = raw.view(np.uint32).reshape(-1, 12)
     return dict(center=f[:, 0:2], opacity=f[:, 2], x0=(u[:, 3] & 0xFFFF).astype(np.int64),
                 x1=(u[:, 3] >> 16).astype(np.int64), qa=f[:, 4], qb=f[:, 5], qc=f[:, 6],
-                r0=(u[:, 7] & 0xFFFF).astype(np.int64), r1=(u[:, 7] >> 16).astype(np.int64), color=f[:, 8:11])
+                r0=(u[:, 7] & 0xFFFF).astype(np.int64), r1=(u[:, 7] >> 16).astype(np.int64), color=f[:, 8:11],
+                mid=f[:, 11])
+
+
+def expected_interval_form(opacity, color):
+    """kFragGauss record fields in interval form (gsr_internal.h, SplatRec):
+    s = sqrt(opacity/255)/0.99 and 0.99*colour, both correctly rounded float32
+    (exact), and mid = -log2(255*opacity)/2 (device log2f: compare with a
+    tolerance)."""
+    F = np.float32
+    op = np.asarray(opacity, F)
+    s = (np.sqrt(op / F(255.0)) / F(0.99)).astype(F)
+    col = (F(0.99) * np.asarray(color, F)).astype(F)
+    with np.errstate(divide="ignore"):
+        mid = -0.5 * np.log2(255.0 * op.astype(np.float64))
+    return s, col, mid
 
 
 def expected_quadratic(vs):

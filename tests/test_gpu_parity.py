@@ -6,7 +6,8 @@ import pytest
 from gsviewer_amd.camera import Camera, euler_to_rotation_matrix
 from gsviewer_amd.gaussian_data import garden_standin, naive_gaussian, random_scene
 from oracle import gl_oracle as O
-from helpers import TOL_TMIN, compare_images, decode_records, expected_quadratic, gpu_frame, uniforms_for
+from helpers import (TOL_TMIN, compare_images, decode_records, expected_interval_form, expected_quadratic, gpu_frame,
+                     uniforms_for)
 
 pytestmark = pytest.mark.gpu
 
@@ -55,14 +56,33 @@ def test_preprocess_records_bit_exact(gpu):
     np.testing.assert_array_equal(rec["qa"], qa[vis_desc])
     np.testing.assert_array_equal(rec["qb"], qb[vis_desc])
     np.testing.assert_array_equal(rec["qc"], qc[vis_desc])
-    np.testing.assert_array_equal(rec["opacity"], vs["opacity"][vis_desc])
-    np.testing.assert_array_equal(rec["color"], np.clip(vs["color"][vis_desc], 0, 1))
+    s, col, mid = expected_interval_form(vs["opacity"][vis_desc], np.clip(vs["color"][vis_desc], 0, 1))
+    np.testing.assert_array_equal(rec["opacity"], s)
+    np.testing.assert_array_equal(rec["color"], col)
+    np.testing.assert_allclose(rec["mid"], mid, rtol=1e-6, atol=1e-6)
     x0, x1, r0, r1 = O.splat_rects(vs, U)
     nonempty = (x0 <= x1) & (r0 <= r1)
     ne = nonempty[vis_desc]
     for a, b in [(rec["x0"], x0), (rec["x1"], x1), (rec["r0"], r0), (rec["r1"], r1)]:
         np.testing.assert_array_equal(a[ne], b[vis_desc][ne])
     assert np.all(rec["x0"][~ne] > rec["x1"][~ne])
+
+
+@pytest.mark.parametrize("mode", [-6, -5, -4])
+def test_preprocess_records_plain_for_other_fragment_classes(gpu, mode):
+    """Ball / billboard classes keep the plain opacity and colour (mid = 0)."""
+    g = random_scene(1500, sh_degree=1, seed=4)
+    cam = Camera(64, 96).yaw(10)
+    st = _settings(render_mod=mode, t_min=0.0)
+    res = gpu_frame(g, cam, st, with_debug=True)
+    U = uniforms_for(cam, st)
+    vs = O.vertex_stage(g.flat(), g.sh_dim, U)
+    vis_desc = np.nonzero(vs["visible"])[0][::-1]
+    rec = decode_records(res["records"])
+    np.testing.assert_array_equal(rec["opacity"], vs["opacity"][vis_desc])
+    col = vs["color"][vis_desc] if mode == -6 else np.clip(vs["color"][vis_desc], 0, 1)
+    np.testing.assert_array_equal(rec["color"], col)
+    assert np.all(rec["mid"] == 0)
 
 
 def test_depth_order_and_tile_lists_exact(gpu):
