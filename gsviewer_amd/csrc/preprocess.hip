@@ -255,9 +255,8 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
                                                   const uint32_t* __restrict__ n_vis_dev, SplatRec* __restrict__ recs,
                                                   uint32_t* __restrict__ depth_keys, uint2* __restrict__ trect,
                                                   int32_t* __restrict__ radii) {
-    const uint32_t slot = n_vis_dev[0] - 1u - (wave_off[i >> 6] + (uint32_t)__popcll(m & lanemask_lt()));
-
-    // issue every load of this Gaussian up front (all unconditional at this DEG)
+    // issue every load of this Gaussian up front (all unconditional at this
+    // DEG), the ones needed first first: vmcnt waits are in issue order
     const float4 po = pos_op[i];
     const float4 q1 = rot[i];
     const float4 sc4 = scale[i];
@@ -274,6 +273,11 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
             f[4 * p + 0] = f[4 * p + 1] = f[4 * p + 2] = f[4 * p + 3] = 0.f;
         }
     }
+    const uint32_t slot_base = n_vis_dev[0] - 1u - wave_off[i >> 6];
+    // keep the compiler from sinking the loads below the arithmetic (it would
+    // otherwise wait for pos/rot/scale before issuing the SH planes: two
+    // dependent memory round trips per wave instead of one)
+    __builtin_amdgcn_sched_barrier(0);
     const float x = po.x, y = po.y, z = po.z;
     const Projected pr = project(x, y, z, u);
 
@@ -410,6 +414,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
         rec.b = 0.99f * col.z;
     }
 
+    const uint32_t slot = slot_base - (uint32_t)__popcll(m & lanemask_lt());
     float4* dst = reinterpret_cast<float4*>(recs + slot);
     dst[0] = make_float4(rec.cx, rec.cy, rec.opacity, __uint_as_float(rec.xspan));
     dst[1] = make_float4(rec.qa, rec.qb, rec.qc, __uint_as_float(rec.yspan));
@@ -430,8 +435,13 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     return tiles;
 }
 
+#ifdef GSR_PRE_WPE
+#define GSR_PRE_OCC __attribute__((amdgpu_waves_per_eu(GSR_PRE_WPE, 8)))
+#else
+#define GSR_PRE_OCC
+#endif
 template <int DEG>
-__global__ __launch_bounds__(kThreads) void k_preprocess(const float4* __restrict__ pos_op, const float4* __restrict__ rot,
+__global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess(const float4* __restrict__ pos_op, const float4* __restrict__ rot,
                                                          const float4* __restrict__ scale, const float4* __restrict__ sh,
                                                          int64_t n, FrameUniforms u,
                                                          const uint64_t* __restrict__ vis_mask,
