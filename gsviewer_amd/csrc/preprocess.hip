@@ -104,6 +104,42 @@ __device__ __forceinline__ void pixel_span(float lo, float hi, int limit, int& p
     p1 = min(max(b, -1), limit);
 }
 
+// The fragment's alpha box (kFragGauss): the pixel rectangle outside which
+// every fragment is discarded by alpha < 1/255 (gau_frag.glsl:42).  With the
+// falloff pw = qa dx^2 + qb dx dy + qc dy^2 (power * log2 e, pixel offsets,
+// negative definite) a pixel is kept only if pw >= thr = -log2(255 opacity);
+// the set {pw >= thr} is an ellipse with half-extents
+//   hx = sqrt(thr / (qa - qb^2 / (4 qc))),  hy = sqrt(thr / (qc - qb^2 / (4 qa))).
+// The covered rectangle [x0, x1] x [r0, r1] (the 3-sigma quad, image rows) is
+// intersected with that box widened by 0.2 % + 0.01 px (far above the float
+// rounding of pw and of the box), so no kept fragment is ever dropped: the
+// result only narrows the tiles and 16x4 slices a splat is composited over.
+// opacity < 1/255 (thr > 0, or NaN): nothing is ever drawn, the rectangle is
+// emptied.  Degenerate or nearly degenerate forms keep the quad unchanged.
+// Evaluated without contraction in this fixed order: tests/helpers.py
+// (alpha_box_rects) mirrors it bit for bit.
+__device__ __forceinline__ void alpha_box(float qa, float qb, float qc, float thr, float cx, float cy, int height,
+                                          int& x0, int& x1, int& r0, int& r1) {
+    if (!(thr <= 0.0f)) {
+        x0 = 1;
+        x1 = 0;
+        return;
+    }
+    const float d4 = (4.0f * qa) * qc;
+    const float disc = d4 - qb * qb;
+    if (!(qa < 0.0f && qc < 0.0f && disc > 1e-4f * d4)) return;
+    const float hx = sqrtf(thr / (qa - (qb * qb) / (4.0f * qc))) * 1.002f + 0.01f;
+    const float hy = sqrtf(thr / (qc - (qb * qb) / (4.0f * qa))) * 1.002f + 0.01f;
+    if (!(hx < 65536.0f && hy < 65536.0f)) return;  // (cx, cy are within 1.3x of the viewport)
+    // pixel p is a candidate if its centre p + 0.5 is within [c - h, c + h]
+    const int bx0 = (int)ceilf((cx - hx) - 0.5f), bx1 = (int)floorf((cx + hx) - 0.5f);
+    const int bj0 = (int)ceilf((cy - hy) - 0.5f), bj1 = (int)floorf((cy + hy) - 0.5f);  // window rows
+    x0 = max(x0, bx0);
+    x1 = min(x1, bx1);
+    r0 = max(r0, (height - 1) - bj1);  // image rows
+    r1 = min(r1, (height - 1) - bj0);
+}
+
 __device__ __forceinline__ uint32_t float_order_key(float f) {
     const uint32_t b = __float_as_uint(f);
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
@@ -375,13 +411,16 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     x1 = min(x1, u.width - 1);
     j0i = max(j0i, 0);
     j1i = min(j1i, u.height - 1);
-    const int r0 = (u.height - 1) - j1i, r1 = (u.height - 1) - j0i;
+    int r0 = (u.height - 1) - j1i, r1 = (u.height - 1) - j0i;
+    const int mode = u.render_mod;
+    const bool gauss = frag_class_of(mode) == kFragGauss;
+    const float mid = gauss ? -0.5f * log2f(255.0f * po.w) : 0.f;
+    if (gauss) alpha_box(rec.qa, rec.qb, rec.qc, 2.0f * mid, rec.cx, rec.cy, u.height, x0, x1, r0, r1);
     const bool nonempty = (x0 <= x1) && (r0 <= r1);
     rec.xspan = nonempty ? ((uint32_t)x0 | ((uint32_t)x1 << 16)) : 0xffffu;  // empty: x0 > x1
     rec.yspan = nonempty ? ((uint32_t)r0 | ((uint32_t)r1 << 16)) : 0xffffu;
 
     // colour varying
-    const int mode = u.render_mod;
     V3 col;
     if (mode == -3) {  // depth (gau_vert.glsl:252-259)
         float d = -pr.pv[2];
@@ -405,9 +444,8 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     rec.r = col.x;
     rec.g = col.y;
     rec.b = col.z;
-    rec.mid = 0.f;
-    if (frag_class_of(mode) == kFragGauss) {  // interval form (gsr_internal.h, SplatRec)
-        rec.mid = -0.5f * log2f(255.0f * po.w);
+    rec.mid = mid;
+    if (gauss) {  // interval form (gsr_internal.h, SplatRec)
         rec.opacity = sqrtf(po.w / 255.0f) / 0.99f;
         rec.r = 0.99f * col.x;
         rec.g = 0.99f * col.y;

@@ -125,3 +125,75 @@ def compare_images(gpu, ref, tol=TOL_EXACT, frac=TOL_EXACT_FRAC, tol_max=TOL_MAX
     assert ok_frac >= frac, info
     assert d.max() <= tol_max, info
     return info
+
+
+def alpha_box_rects(rec, rects, height):
+    """The preprocess's alpha-box narrowing of the covered rectangles
+    (preprocess.hip alpha_box), mirrored op for op in float32 from the
+    record's own quadratic form, centre and mid (kFragGauss records).
+    `rects` = (x0, x1, r0, r1) of the same splats from the oracle."""
+    F = np.float32
+    qa, qb, qc = rec["qa"].astype(F), rec["qb"].astype(F), rec["qc"].astype(F)
+    cx, cy = rec["center"][:, 0].astype(F), rec["center"][:, 1].astype(F)
+    thr = (F(2.0) * rec["mid"].astype(F)).astype(F)
+    x0, x1, r0, r1 = (np.asarray(a, np.int64).copy() for a in rects)
+    with np.errstate(all="ignore"):
+        empty = ~(thr <= F(0.0))
+        d4 = (F(4.0) * qa) * qc
+        disc = d4 - qb * qb
+        ok = ~empty & (qa < F(0.0)) & (qc < F(0.0)) & (disc > F(1e-4) * d4)
+        hx = np.sqrt(thr / (qa - (qb * qb) / (F(4.0) * qc))) * F(1.002) + F(0.01)
+        hy = np.sqrt(thr / (qc - (qb * qb) / (F(4.0) * qa))) * F(1.002) + F(0.01)
+        ok &= (hx < F(65536.0)) & (hy < F(65536.0))
+        bx0 = np.ceil((cx - hx) - F(0.5)); bx1 = np.floor((cx + hx) - F(0.5))
+        bj0 = np.ceil((cy - hy) - F(0.5)); bj1 = np.floor((cy + hy) - F(0.5))
+    bx0 = np.where(ok, bx0, 0).astype(np.int64); bx1 = np.where(ok, bx1, 0).astype(np.int64)
+    bj0 = np.where(ok, bj0, 0).astype(np.int64); bj1 = np.where(ok, bj1, 0).astype(np.int64)
+    x0 = np.where(ok, np.maximum(x0, bx0), x0); x1 = np.where(ok, np.minimum(x1, bx1), x1)
+    r0 = np.where(ok, np.maximum(r0, (height - 1) - bj1), r0); r1 = np.where(ok, np.minimum(r1, (height - 1) - bj0), r1)
+    x0 = np.where(empty, 1, x0); x1 = np.where(empty, 0, x1)
+    return x0, x1, r0, r1
+
+
+def narrowed_rects(res, vs, U):
+    """Per-Gaussian covered rectangles as the GPU bins them (kFragGauss):
+    the oracle's quad narrowed by the alpha box, indexed by Gaussian id.
+    Needs res from gpu_frame(..., with_debug=True)."""
+    vis_desc = np.nonzero(vs["visible"])[0][::-1]
+    rec = decode_records(res["records"])
+    rects = O.splat_rects(vs, U)
+    x0, x1, r0, r1 = alpha_box_rects(rec, tuple(a[vis_desc] for a in rects), U["height"])
+    out = [a.astype(np.int64).copy() for a in rects]
+    for dst, v in zip(out, (x0, x1, r0, r1)):
+        dst[vis_desc] = v
+    return tuple(out)
+
+
+def tile_lists_for(vs, U, rects, tile=16):
+    """O.tile_lists with the given per-Gaussian rectangles (front-to-back)."""
+    W, H = U["width"], U["height"]
+    tx_n, ty_n = (W + tile - 1) // tile, (H + tile - 1) // tile
+    x0, x1, r0, r1 = rects[:4]
+    order = O.sort_back_to_front(vs["view_z"], vs["visible"])[::-1]
+    lists = [[] for _ in range(tx_n * ty_n)]
+    for g in order:
+        if x0[g] > x1[g] or r0[g] > r1[g]:
+            continue
+        for ty in range(r0[g] // tile, r1[g] // tile + 1):
+            for tx in range(x0[g] // tile, x1[g] // tile + 1):
+                lists[ty * tx_n + tx].append(int(g))
+    return lists
+
+
+def kept_fragments(vs, U, g, xs, rows):
+    """Oracle fragment keep mask (gau_frag.glsl discards) of Gaussian g over
+    pixel columns xs x image rows `rows`, ignoring the quad's coverage."""
+    F = np.float32
+    H = U["height"]
+    px = np.asarray(xs).astype(F) + F(0.5)
+    pyw = (F(H - 1) - np.asarray(rows).astype(F)) + F(0.5)
+    dx = (px - vs["center"][g, 0]) * vs["coord_scale"][g, 0]
+    dy = (pyw - vs["center"][g, 1]) * vs["coord_scale"][g, 1]
+    DX, DY = np.meshgrid(dx.astype(F), dy.astype(F))
+    _, _, keep = O.fragment(vs, g, DX, DY, U["render_mod"])
+    return keep

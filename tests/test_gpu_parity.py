@@ -6,7 +6,8 @@ import pytest
 from gsviewer_amd.camera import Camera, euler_to_rotation_matrix
 from gsviewer_amd.gaussian_data import garden_standin, naive_gaussian, random_scene
 from oracle import gl_oracle as O
-from helpers import (TOL_TMIN, compare_images, decode_records, expected_interval_form, expected_quadratic, gpu_frame,
+from helpers import (TOL_TMIN, alpha_box_rects, compare_images, decode_records, kept_fragments, narrowed_rects,
+                     tile_lists_for, expected_interval_form, expected_quadratic, gpu_frame,
                      uniforms_for)
 
 pytestmark = pytest.mark.gpu
@@ -60,13 +61,17 @@ def test_preprocess_records_bit_exact(gpu):
     np.testing.assert_array_equal(rec["opacity"], s)
     np.testing.assert_array_equal(rec["color"], col)
     np.testing.assert_allclose(rec["mid"], mid, rtol=1e-6, atol=1e-6)
-    x0, x1, r0, r1 = O.splat_rects(vs, U)
-    nonempty = (x0 <= x1) & (r0 <= r1)
-    ne = nonempty[vis_desc]
+    # covered rectangle = the oracle's quad narrowed by the alpha box (bit-exact mirror)
+    rx0, rx1, rr0, rr1 = (a[vis_desc] for a in O.splat_rects(vs, U))
+    x0, x1, r0, r1 = alpha_box_rects(rec, (rx0, rx1, rr0, rr1), U["height"])
+    ne = (x0 <= x1) & (r0 <= r1)
     for a, b in [(rec["x0"], x0), (rec["x1"], x1), (rec["r0"], r0), (rec["r1"], r1)]:
-        np.testing.assert_array_equal(a[ne], b[vis_desc][ne])
+        np.testing.assert_array_equal(a[ne], b[ne])
     assert np.all(rec["x0"][~ne] > rec["x1"][~ne])
-
+    # it only narrows, and it does narrow a sizeable share of this scene
+    assert np.all((x0[ne] >= rx0[ne]) & (x1[ne] <= rx1[ne]) & (r0[ne] >= rr0[ne]) & (r1[ne] <= rr1[ne]))
+    area = lambda a0, a1, b0, b1: ((a1 - a0 + 1) * (b1 - b0 + 1))[ne]
+    assert (area(x0, x1, r0, r1) < area(rx0, rx1, rr0, rr1)).mean() > 0.1
 
 @pytest.mark.parametrize("mode", [-6, -5, -4])
 def test_preprocess_records_plain_for_other_fragment_classes(gpu, mode):
@@ -95,14 +100,56 @@ def test_depth_order_and_tile_lists_exact(gpu):
     # global front-to-back order == reverse of the GL draw order
     f2b = O.sort_back_to_front(vs["view_z"], vs["visible"])[::-1]
     np.testing.assert_array_equal(vis_desc[res["depth_order"]], f2b)
-    # per-tile instance lists == GL order restricted to the tile, reversed
-    lists = O.tile_lists(vs, U)
+    # per-tile instance lists == GL order restricted to the tile, reversed, over
+    # the quads narrowed by the alpha box
+    rects = narrowed_rects(res, vs, U)
+    lists = tile_lists_for(vs, U, rects)
     ranges, tl = res["ranges"], res["tile_list"]
     for t, want in enumerate(lists):
         b, e = ranges[t]
         got = vis_desc[tl[b:e]] if e > b else np.zeros(0, np.int64)
         np.testing.assert_array_equal(got, np.asarray(want, np.int64), err_msg=f"tile {t}")
     assert res["stats"]["n_instances"] == sum(len(x) for x in lists)
+    # the narrowing drops only instances without a single kept fragment in the tile
+    full = O.tile_lists(vs, U)
+    qx0, qx1, qr0, qr1 = O.splat_rects(vs, U)
+    tx_n = (U["width"] + 15) // 16
+    dropped = 0
+    for t, (f, ours) in enumerate(zip(full, lists)):
+        keep = set(ours)
+        assert [x for x in f if x in keep] == ours, f"tile {t}: order"
+        ty, tx = divmod(t, tx_n)
+        for gid in set(f) - keep:
+            xs = np.arange(max(qx0[gid], 16 * tx), min(qx1[gid], 16 * tx + 15) + 1)
+            rows = np.arange(max(qr0[gid], 16 * ty), min(qr1[gid], 16 * ty + 15) + 1)
+            assert not kept_fragments(vs, U, gid, xs, rows).any(), f"tile {t}: Gaussian {gid} dropped"
+            dropped += 1
+    assert dropped > 0
+
+
+def test_alpha_box_keeps_every_fragment(gpu):
+    """The narrowed rectangle holds every fragment of the quad that the alpha
+    test keeps (opacities over the whole range, anisotropic splats)."""
+    rng = np.random.default_rng(12)
+    g = random_scene(3000, sh_degree=0, seed=12, scale_range=(0.01, 0.12))
+    g.opacity[:] = rng.uniform(0.0, 1.0, g.opacity.shape).astype(np.float32)
+    cam = Camera(96, 128).yaw(25)
+    res = gpu_frame(g, cam, _settings(t_min=0.0), with_debug=True)
+    U = uniforms_for(cam)
+    vs = O.vertex_stage(g.flat(), 3, U)
+    x0, x1, r0, r1 = narrowed_rects(res, vs, U)
+    qx0, qx1, qr0, qr1 = O.splat_rects(vs, U)
+    ids = np.nonzero(vs["visible"] & (qx0 <= qx1) & (qr0 <= qr1))[0]
+    narrowed = 0
+    for gid in ids:
+        xs = np.arange(qx0[gid], qx1[gid] + 1)
+        rows = np.arange(qr0[gid], qr1[gid] + 1)
+        keep = kept_fragments(vs, U, gid, xs, rows)
+        inside = ((xs >= x0[gid]) & (xs <= x1[gid]))[None, :] & ((rows >= r0[gid]) & (rows <= r1[gid]))[:, None]
+        assert not (keep & ~inside).any(), f"Gaussian {gid}"
+        narrowed += int(not inside.all())
+    assert narrowed > len(ids) // 10
+    compare_images(res["image"], O.composite(vs, U))
 
 
 def test_radii(gpu):

@@ -12,7 +12,7 @@ import pytest
 from gsviewer_amd.camera import Camera
 from gsviewer_amd.gaussian_data import GaussianData, garden_standin, random_scene
 from oracle import gl_oracle as O
-from helpers import gpu_frame, uniforms_for
+from helpers import gpu_frame, narrowed_rects, uniforms_for
 
 pytestmark = pytest.mark.gpu
 
@@ -24,11 +24,11 @@ def _settings(**kw):
     return RenderSettings(**kw)
 
 
-def expected_instances(vs, U):
+def expected_instances(vs, U, rects):
     """(tile, gid) of every tile instance of the visible splats, vectorized."""
     W, H = U["width"], U["height"]
     tiles_x = (W + TILE - 1) // TILE
-    x0, x1, r0, r1 = O.splat_rects(vs, U)
+    x0, x1, r0, r1 = rects[:4]
     ok = vs["visible"] & (x0 <= x1) & (r0 <= r1)
     gid = np.nonzero(ok)[0]
     tx0, tx1, ty0, ty1 = x0[gid] // TILE, x1[gid] // TILE, r0[gid] // TILE, r1[gid] // TILE
@@ -51,7 +51,8 @@ def check_frame_order(res, vs, U):
     # every tile list == the global order restricted to the tile
     rank = np.empty(len(vis), np.int64)
     rank[f2b] = np.arange(nv)
-    tile_e, gid_e = expected_instances(vs, U)
+    # the quads narrowed by the alpha box (tests/helpers.py mirrors preprocess.hip)
+    tile_e, gid_e = expected_instances(vs, U, narrowed_rects(res, vs, U))
     o = np.lexsort((rank[gid_e], tile_e))
     tile_e, gid_e = tile_e[o], gid_e[o]
     ranges = res["ranges"].astype(np.int64)
