@@ -26,7 +26,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 SIMDS = 256 * 4        # MI355X CUs x SIMDs
-CLOCK_HZ = 2.4e9       # MI355X engine clock (MI355X_MICROARCH.md)
+VALU_NS = 1.6          # measured issue cost of a wave64 f32 VALU instruction per SIMD (valu_rate.hip)
+TRANS_NS = 3.5         # ... of a transcendental (v_exp_f32)
 
 CONFIGS = {
     # name: (N, sh_degree, width, height, description)
@@ -121,17 +122,19 @@ def pmc_traffic(kernel, args):
 
 
 def valu_issue(kernel, args, ms_per_launch):
-    """The compositor's real limiter: VALU issue.  A wave64 VALU instruction
-    occupies its SIMD for 4 cycles, a transcendental (v_exp_f32) for 16;
-    MI355X has 256 CUs x 4 SIMDs at ~2.4 GHz (MI355X_MICROARCH.md)."""
+    """The compositor's real limiter: VALU issue.  Issue cost per wave64
+    instruction per SIMD, measured on this chip with 8 waves/SIMD of
+    independent instructions (tools/microbench/valu_rate.hip, output in
+    profiles/<round>/valu_rate.txt): 1.6 ns for an f32 add/mul/fma or a
+    compare/select, 3.5 ns for a transcendental (v_exp_f32).  256 CUs x 4 SIMDs."""
     got, src = pmc_counters(kernel, args)
     if not got or "SQ_INSTS_VALU" not in got:
         return None
     valu, trans = got["SQ_INSTS_VALU"], got.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
-    cycles = 4.0 * (valu - trans) + 16.0 * trans
-    t_issue = cycles / (SIMDS * CLOCK_HZ)
+    t_issue = (VALU_NS * (valu - trans) + TRANS_NS * trans) * 1e-9 / SIMDS
     return {"valu_instr_per_launch": valu, "trans_instr_per_launch": trans, "issue_us": t_issue * 1e6,
-            "launch_us": ms_per_launch * 1e3, "frac": t_issue / (ms_per_launch * 1e-3), "source": src}
+            "launch_us": ms_per_launch * 1e3, "frac": t_issue / (ms_per_launch * 1e-3),
+            "issue_ns_per_instr": {"valu": VALU_NS, "trans": TRANS_NS}, "source": src}
 
 
 def main():
