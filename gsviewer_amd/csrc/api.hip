@@ -93,6 +93,7 @@ struct gsr_context {
     gsr::DevBuf<uint32_t> zero;                   // per-frame zeroed block (see zero_layout)
     gsr::DevBuf<uint32_t> chunk_cnt, chunk_base;  // per tile
     gsr::DevBuf<uint4> chunk_desc;                // per chunk
+    gsr::DevBuf<uint32_t> chunk_order;            // per chunk: dispatch position -> chunk slot
     gsr::DevBuf<float4> partial;                  // per chunk x 256 px (multi-chunk tiles)
     gsr::DevBuf<float4> tmax;                     // per chunk: published slice maxima of local T
     uint32_t chunk = 128;                         // instances per compositing chunk (swept: 128 best latency;
@@ -412,7 +413,7 @@ int gsr_context_destroy(gsr_context* c) {
     c->trect.release(); c->trect_sorted.release(); c->bin_tmp.release(); c->tkeys_a.release(); c->tkeys_b.release(); c->tvals_a.release();
     c->tvals_b.release(); c->radix_tmp.release(); c->zero.release();
     c->chunk_cnt.release(); c->chunk_base.release();
-    c->chunk_desc.release(); c->partial.release();
+    c->chunk_desc.release(); c->chunk_order.release(); c->partial.release();
     c->tmax.release();
     c->done_ctr.release();
     if (c->host_counters) (void)hipHostFree(c->host_counters);
@@ -552,16 +553,17 @@ int gsr_render_finish(gsr_context* c, void* stream) {
 
     // compositing chunks: at most one per tile plus one per `chunk` instances
     const size_t max_chunks = (size_t)num_tiles + n_dup / c->chunk + 1;
-    if ((rc = c->chunk_cnt.ensure((size_t)num_tiles + (size_t)num_tiles / 256 + 1, "chunk_cnt"))) return rc;
+    if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
     if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
     if ((rc = c->chunk_desc.ensure(max_chunks, "chunk_desc"))) return rc;
+    if ((rc = c->chunk_order.ensure(max_chunks, "chunk_order"))) return rc;
     if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
     if ((rc = c->tmax.ensure(max_chunks, "tmax"))) return rc;
     if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
-                            c->chunk_desc.p, c->tmax.p, s)))
+                            c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s)))
         return rc;
     if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
-    if ((rc = launch_composite(c->chunk_desc.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
+    if ((rc = launch_composite(c->chunk_desc.p, c->chunk_order.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
                                sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.t_min, f.bg,
                                f.out_layout, f.out, c->partial.p, c->tmax.p, s)))
         return rc;

@@ -117,6 +117,23 @@ struct CompositeArgs {
 };
 
 constexpr int kBatch = 64;  // records staged per wave per LDS batch
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// kFragGauss keep test in two VALU ops, with no compare and lane-mask select
+// (whose VCC hand-off also costs an s_nop on gfx950).  With m = -mid > 0 and
+// pw' = pw - mid, a fragment is kept iff |pw'| <= m (SplatRec).
+//   u = fma(-K, |pw'|, K m (1 + 2^-22)),  K = 2^64
+// is K (m (1 + 2^-22) - |pw'|) rounded once, so its sign is exact, and when it
+// is >= 0 it is >= K m 2^-23 >= 1 for any m > 2^-41; so
+//   alpha = med3(u, 0, a1)  (a1 in [0, 1])
+// is a1 inside the interval and 0 outside it.  The interval is widened by
+// 2^-22 relative (a few ulps): fragments exactly on its ends are kept, as the
+// reference's non-strict tests keep them; ulp-level boundary flips are inside
+// the tolerance the evaluation order already has (the quadratic is not the
+// reference's expression).
+constexpr float kKeepScale = 18446744073709551616.0f;      // K = 2^64
+constexpr float kKeepScaleWide = 18446748471756062720.0f;  // K (1 + 2^-22), exact
 #ifdef GSR_COMP_TRACE
 constexpr uint32_t kTraceMax = 1u << 16;  // waves traced per launch
 #endif
@@ -130,63 +147,122 @@ constexpr uint32_t kTraceMax = 1u << 16;  // waves traced per launch
 // wave, which is what the heavy tiles of a real scene (horizon lines,
 // dense cores) need.
 //
-// Chunk slots: slot t (< num_tiles) is chunk 0 of tile t, so every tile's
-// front chunk is dispatched first; chunks k >= 1 of tile t follow at
-// num_tiles + extra_off[t] + k - 1.  Built by ONE workgroup (num_tiles is at
-// most a few tens of thousands).
+// Chunk slots (where a chunk's descriptor, partial and maxima live): slot t
+// (< num_tiles) is chunk 0 of tile t; chunks k >= 1 of tile t are at
+// num_tiles + extra_off[t] + k - 1.
+//
+// Dispatch order (longest first): order[i] is the slot the i-th compositing
+// wave takes.  Every full chunk (`chunk` instances) is dispatched before every
+// partial one (a tile's last, shorter chunk, or its only one), so the waves
+// that start last are the short ones.  In slot order the full extra chunks of
+// the deep tiles started last and ran alone at the end of the launch (trace:
+// the last third of the launch at falling occupancy).
 __device__ __forceinline__ uint32_t chunks_of(uint2 r, uint32_t chunk) {
     const uint32_t len = r.y - r.x;
     return len == 0 ? 1u : (len + chunk - 1) / chunk;
 }
 
+// Chunks of a tile that hold exactly `chunk` instances (all but the last).
+__device__ __forceinline__ uint32_t full_chunks_of(uint2 r, uint32_t chunk) { return (r.y - r.x) / chunk; }
+
 // Chunk descriptors in two parallel launches (one thread per tile):
-// k_chunk_count writes each block's total of extra chunks (beyond the first
-// per tile); k_chunk_write takes its block's offset as the sum of the earlier
-// block totals (a few dozen at 1080p), scans its tiles' extra chunks and
-// writes the descriptors (tile, begin, end, count << 16 | index).
+// k_chunk_count writes each block's totals of extra chunks (beyond the first
+// per tile) and of full chunks; k_chunk_write takes its block's offsets as
+// sums of the earlier block totals (a few dozen at 1080p), scans its tiles'
+// counts, and writes the descriptors (tile, begin, end, count << 16 | index)
+// and each chunk's dispatch position.
 __global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restrict__ ranges, int num_tiles,
-                                                          uint32_t chunk, uint32_t* __restrict__ block_extra) {
-    __shared__ uint32_t lds[kThreads / 64];
+                                                          uint32_t chunk, uint32_t* __restrict__ block_extra,
+                                                          uint32_t* __restrict__ block_full) {
+    __shared__ uint32_t lds[2][kThreads / 64];
     const int t = blockIdx.x * kThreads + threadIdx.x;
-    uint32_t e = t < num_tiles ? chunks_of(ranges[t], chunk) - 1u : 0u;
+    const uint2 r = t < num_tiles ? ranges[t] : make_uint2(0u, 0u);
+    uint32_t e = t < num_tiles ? chunks_of(r, chunk) - 1u : 0u;
+    uint32_t f = full_chunks_of(r, chunk);
     e = wave_reduce_sum(e);
-    if (__lane_id() == 0) lds[threadIdx.x >> 6] = e;
+    f = wave_reduce_sum(f);
+    if (__lane_id() == 0) {
+        lds[0][threadIdx.x >> 6] = e;
+        lds[1][threadIdx.x >> 6] = f;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) block_extra[blockIdx.x] = lds[0] + lds[1] + lds[2] + lds[3];
+    if (threadIdx.x == 0) {
+        block_extra[blockIdx.x] = lds[0][0] + lds[0][1] + lds[0][2] + lds[0][3];
+        block_full[blockIdx.x] = lds[1][0] + lds[1][1] + lds[1][2] + lds[1][3];
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restrict__ ranges, int num_tiles,
                                                           uint32_t chunk, const uint32_t* __restrict__ block_extra,
+                                                          const uint32_t* __restrict__ block_full,
                                                           uint32_t* __restrict__ chunk_cnt,
                                                           uint32_t* __restrict__ chunk_base,
                                                           uint32_t* __restrict__ n_extra_dev,
-                                                          uint4* __restrict__ desc, float4* __restrict__ tmax) {
-    __shared__ uint32_t lds[kThreads / 64];
-    __shared__ uint32_t s_prefix;
+                                                          uint4* __restrict__ desc, uint32_t* __restrict__ order,
+                                                          float4* __restrict__ tmax) {
+    __shared__ uint32_t lds[2][kThreads / 64];
+    __shared__ uint32_t s_prefix, s_full_prefix, s_full_total;
     const int t = blockIdx.x * kThreads + threadIdx.x;
-    if (threadIdx.x < 64) {  // wave 0: offset of this block = sum of the earlier blocks' totals
-        uint32_t p = 0;
-        for (uint32_t b = __lane_id(); b < blockIdx.x; b += 64) p += block_extra[b];
+    if (threadIdx.x < 64) {  // wave 0: offsets of this block = sums of the earlier blocks' totals
+        uint32_t p = 0, pf = 0, tf = 0;
+        for (uint32_t b = __lane_id(); b < gridDim.x; b += 64) {
+            const uint32_t f = block_full[b];
+            if (b < blockIdx.x) {
+                p += block_extra[b];
+                pf += f;
+            }
+            tf += f;
+        }
         p = wave_reduce_sum(p);
-        if (__lane_id() == 0) s_prefix = p;
+        pf = wave_reduce_sum(pf);
+        tf = wave_reduce_sum(tf);
+        if (__lane_id() == 0) {
+            s_prefix = p;
+            s_full_prefix = pf;
+            s_full_total = tf;
+        }
     }
     const uint2 r = t < num_tiles ? ranges[t] : make_uint2(0u, 0u);
     const uint32_t cnt = chunks_of(r, chunk);
+    const uint32_t full = full_chunks_of(r, chunk);
     const uint32_t mine = t < num_tiles ? cnt - 1u : 0u;
-    uint32_t total;
-    const uint32_t excl = block_exclusive<kThreads>(mine, lds, total);  // (its barrier also publishes s_prefix)
+    uint32_t total, total_f;
+    const uint32_t excl = block_exclusive<kThreads>(mine, lds[0], total);  // (its barrier also publishes s_*)
+    const uint32_t excl_f = block_exclusive<kThreads>(full, lds[1], total_f);
     const uint32_t extra = s_prefix + excl;
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_extra_dev = s_prefix + total;
-    if (t >= num_tiles) return;
+    const bool valid = t < num_tiles;
     const uint32_t base = (uint32_t)num_tiles + extra;
-    chunk_cnt[t] = cnt;
-    chunk_base[t] = base;
-    for (uint32_t j = 0; j < cnt; ++j) {
-        const uint32_t b = r.x + j * chunk;
-        const uint32_t e = min(r.y, b + chunk);
-        const uint32_t slot = j == 0 ? (uint32_t)t : base + j - 1;
-        desc[slot] = make_uint4((uint32_t)t, b, e, (cnt << 16) | j);
-        if (tmax && cnt > 1) tmax[slot] = make_float4(1.f, 1.f, 1.f, 1.f);  // nothing composited yet
+    // dispatch positions: full chunks in tile order, then the partial ones
+    // (at most one per tile: chunks before this tile minus full ones before it)
+    const uint32_t full_before = s_full_prefix + excl_f;
+    const uint32_t part_pos = s_full_total + ((uint32_t)t + extra - full_before);
+    // chunk j of this tile: descriptor, dispatch position, published maxima
+    auto emit = [&](uint32_t tt, uint32_t rx, uint32_t ry, uint32_t c, uint32_t f, uint32_t bs, uint32_t fb,
+                    uint32_t pp, uint32_t j) {
+        const uint32_t b = rx + j * chunk;
+        const uint32_t e = min(ry, b + chunk);
+        const uint32_t slot = j == 0 ? tt : bs + j - 1;
+        desc[slot] = make_uint4(tt, b, e, (c << 16) | j);
+        order[j < f ? fb + j : pp] = slot;
+        if (tmax && c > 1) tmax[slot] = make_float4(1.f, 1.f, 1.f, 1.f);  // nothing composited yet
+    };
+    if (valid) {
+        chunk_cnt[t] = cnt;
+        chunk_base[t] = base;
+        emit((uint32_t)t, r.x, r.y, cnt, full, base, full_before, part_pos, 0u);
+    }
+    // chunks j >= 1 of the multi-chunk tiles: the whole wave writes one tile's
+    // at a time (a deep tile has ~200 chunks: one lane storing them all would
+    // wait on its own outstanding stores)
+    uint64_t multi = __ballot(valid && cnt > 1);
+    while (multi) {
+        const int src = (int)__builtin_ctzll(multi);
+        multi &= multi - 1;
+        const uint32_t tt = __shfl((uint32_t)t, src, 64), rx = __shfl(r.x, src, 64), ry = __shfl(r.y, src, 64);
+        const uint32_t c = __shfl(cnt, src, 64), f = __shfl(full, src, 64), bs = __shfl(base, src, 64);
+        const uint32_t fb = __shfl(full_before, src, 64), pp = __shfl(part_pos, src, 64);
+        for (uint32_t j = 1 + __lane_id(); j < c; j += 64) emit(tt, rx, ry, c, f, bs, fb, pp, j);
     }
 }
 
@@ -301,12 +377,17 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
 #pragma unroll
     for (int k = 0; k < 4; ++k) pyw[k] = (float)(a.height - 1 - (row_base + 4 * k + lrow)) + 0.5f;
 
-    float T[4], cr[4], cg[4], cb[4];
+    // per slice: (r, g) and (b, T), updated with packed FMAs (v_pk_fma_f32:
+    // one issue slot for two channels)
+    f32x2 rg[4], bt[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        T[k] = 1.f;
-        cr[k] = cg[k] = cb[k] = 0.f;
+        rg[k] = f32x2{0.f, 0.f};
+        bt[k] = f32x2{0.f, 1.f};
     }
+    // transmittance coefficient of the packed (b, T) update: T -= 0.99 w in
+    // interval form (the 0.99 of the alpha), T -= w otherwise
+    const float kT = FRAG == kFragGauss ? -0.99f : -1.0f;
     const float t_min = a.t_min;
     const bool track = (nchunks > 1) && (t_min > 0.f);
     uint32_t* my_sat = sat + (size_t)tile * 4;
@@ -365,18 +446,24 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
 #endif
     for (uint32_t b = begin; b < end && live; b += kBatch) {
         __builtin_amdgcn_wave_barrier();
+        // sb[k] bit j: record j of the batch touches 16x4 slice k (and the
+        // slice is live): one ballot per slice and batch instead of a
+        // readfirstlane of a slice mask per record
+        uint64_t sb[4];
         {
             // Tile-relative coverage of this lane's record, computed once per
             // record (not per pixel): .w of q0 = 16-bit column mask | 16-bit
-            // row mask << 16, .w of q1 = mask of the 16x4 slices it touches.
+            // row mask << 16.
             const uint32_t xs = __float_as_uint(f0.w), ys = __float_as_uint(f1.w);
             const uint32_t covx = span_bits16((int)(xs & 0xffffu) - col_base, (int)(xs >> 16) - col_base);
             const uint32_t covy = span_bits16((int)(ys & 0xffffu) - row_base, (int)(ys >> 16) - row_base);
-            const uint32_t sl = (uint32_t)((covy & 0x000fu) != 0) | ((uint32_t)((covy & 0x00f0u) != 0) << 1) |
-                                ((uint32_t)((covy & 0x0f00u) != 0) << 2) | ((uint32_t)((covy & 0xf000u) != 0) << 3);
+            // LDS record: (cx, cy, opacity, coverage), (qa, qb, qc, mid), (r, g, b, T coefficient)
             my[lane * 3 + 0] = make_float4(f0.x, f0.y, f0.z, __uint_as_float(covx | (covy << 16)));
-            my[lane * 3 + 1] = make_float4(f1.x, f1.y, f1.z, __uint_as_float(sl));
-            my[lane * 3 + 2] = f2;
+            my[lane * 3 + 1] = make_float4(f1.x, f1.y, f1.z, f2.w);
+            my[lane * 3 + 2] = make_float4(f2.x, f2.y, f2.z, kT);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                sb[k] = ((live >> k) & 1u) ? (uint64_t)__ballot(((covy >> (4 * k)) & 0xfu) != 0u) : 0ull;
         }
         __builtin_amdgcn_wave_barrier();
 #ifdef GSR_COMP_BOUND
@@ -400,31 +487,19 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
             if (i2 < end) idx_next = list[i2];
         }
         const int nb = __builtin_amdgcn_readfirstlane((int)min((uint32_t)kBatch, end - b));
-#ifdef GSR_COMP_LDSPIPE
-        float4 n0 = my[0], n1 = my[1], n2 = my[2];
-#endif
+        // (not unrolled: unrolled by 2, the register allocator copies every
+        // packed accumulator at each slice branch and needs 128 VGPRs)
+#pragma unroll 1
         for (int j = 0; j < nb; ++j) {
-#ifdef GSR_COMP_LDSPIPE
-            const float4 q0 = n0, q1 = n1, q2 = n2;
-            {
-                const int jn = min(j + 1, kBatch - 1);
-                n0 = my[jn * 3 + 0];
-                n1 = my[jn * 3 + 1];
-                n2 = my[jn * 3 + 2];
-            }
-#else
-            const float4 q0 = my[j * 3 + 0];  // cx cy opacity xspan
-            const float4 q1 = my[j * 3 + 1];  // qa qb qc yspan
-            const float4 q2 = my[j * 3 + 2];  // r g b -
-#endif
-            // scalar mask of the 16x4 slices the splat touches (and still live)
-            const uint32_t smask = __builtin_amdgcn_readfirstlane(__float_as_uint(q1.w)) & live;
+            const float4 q0 = my[j * 3 + 0];  // cx cy opacity coverage
+            const float4 q1 = my[j * 3 + 1];  // qa qb qc mid
+            const float4 q2 = my[j * 3 + 2];  // r g b kT
 #ifdef GSR_COMP_STATS
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if ((smask >> k) & 1u) {
+                if ((sb[k] >> j) & 1ull) {
                     st_evals += 1;
-                    if (!__any(T[k] >= t_min)) st_wasted += 1;
+                    if (!__any(bt[k].y >= t_min)) st_wasted += 1;
                 }
             st_records += 1;
 #endif
@@ -435,26 +510,29 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
             // power*log2(e) = qa dx^2 + qb dx dy + qc dy^2 in pixel units
             // (gau_frag.glsl:37 with coordxy's scale folded in by the preprocess)
             const float dx = px - q0.x;
-            // kFragGauss: q2.w = mid, and p0 is shifted by it (interval form, SplatRec)
-            const float mid = FRAG == kFragGauss ? q2.w : 0.f;
+            // kFragGauss: q1.w = mid, and p0 is shifted by it (interval form, SplatRec)
+            const float mid = FRAG == kFragGauss ? q1.w : 0.f;
             const float p0 = FRAG == kFragGauss ? fmaf(q1.x * dx, dx, -mid) : q1.x * dx * dx;
             const float p1 = q1.y * dx;
             const float c2 = q1.z;
+            // K m (1 + 2^-22) of the keep test (kKeepScale)
+            const float km = FRAG == kFragGauss ? -mid * kKeepScaleWide : 0.f;
+            const f32x2 c_rg = f32x2{q2.x, q2.y};
+            const f32x2 c_bt = f32x2{q2.z, q2.w};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-#ifndef GSR_COMP_NOSKIP
-                if (!((smask >> k) & 1u)) continue;
-#endif
+                if (!((sb[k] >> j) & 1ull)) continue;
                 // opacity where the pixel is covered, +0 elsewhere (bit mask, no compare)
                 const uint32_t covk = (uint32_t)__builtin_amdgcn_sbfe((int)rb, 4 * k, 1);
-                float alpha, fr = q2.x, fg = q2.y, fb = q2.z;
+                float alpha;
+                f32x2 crg = c_rg, cbt = c_bt;
                 if (FRAG == kFragGauss) {
                     // pw' = pw - mid; keep <=> |pw'| <= -mid; alpha / 0.99 = clamp(s * 2^pw')
                     const float dy = pyw[k] - q0.y;
                     const float pw = (c2 * dy + p1) * dy + p0;
                     const float e = __builtin_amdgcn_exp2f(pw);
                     const float a1 = __builtin_amdgcn_fmed3f(__uint_as_float(covk & __float_as_uint(q0.z)) * e, 0.f, 1.f);
-                    alpha = (fabsf(pw) <= -mid) ? a1 : 0.0f;
+                    alpha = __builtin_amdgcn_fmed3f(fmaf(-kKeepScale, fabsf(pw), km), 0.f, a1);
                 } else if (FRAG == kFragBillboard) {
                     alpha = __uint_as_float(covk & 0x3f800000u);  // 1.0 or 0.0
                 } else {
@@ -466,21 +544,17 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                     alpha = ((pw > 0.0f) | (alpha < (1.0f / 255.0f))) ? 0.0f : alpha;
                     if (FRAG == kFragFlatBall || FRAG == kFragGaussBall) alpha = (alpha > 0.22f) ? 1.0f : 0.0f;
                     if (FRAG == kFragGaussBall) {
-                        fr = fminf(fmaxf(fr * e, 0.f), 1.f);
-                        fg = fminf(fmaxf(fg * e, 0.f), 1.f);
-                        fb = fminf(fmaxf(fb * e, 0.f), 1.f);
+                        crg = f32x2{fminf(fmaxf(q2.x * e, 0.f), 1.f), fminf(fmaxf(q2.y * e, 0.f), 1.f)};
+                        cbt = f32x2{fminf(fmaxf(q2.z * e, 0.f), 1.f), q2.w};
                     }
                 }
-#ifdef GSR_COMP_NOSKIP
-                alpha = (smask & (1u << k)) ? alpha : 0.0f;
-#endif
-                // alpha == 0 leaves (C, T) bit-identical: a discarded fragment
-                const float w = alpha * T[k];
-                cr[k] += fr * w;
-                cg[k] += fg * w;
-                cb[k] += fb * w;
-                // kFragGauss: alpha = 0.99 * a1 (the colour already carries its 0.99)
-                T[k] = FRAG == kFragGauss ? fmaf(w, -0.99f, T[k]) : T[k] - w;
+                // alpha == 0 leaves (C, T) bit-identical: a discarded fragment.
+                // C += c w, T += kT w with w = alpha T (kFragGauss: alpha =
+                // 0.99 a1, the colour already carries its 0.99)
+                const float w = alpha * bt[k].y;
+                const f32x2 ww = f32x2{w, w};
+                rg[k] = __builtin_elementwise_fma(crg, ww, rg[k]);
+                bt[k] = __builtin_elementwise_fma(cbt, ww, bt[k]);
             }
         }
         if (t_min > 0.f) {
@@ -490,7 +564,7 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                 // publish this chunk's slice maxima, then test bound * max against t_min
                 float m[4], B[4] = {1.f, 1.f, 1.f, 1.f};
 #pragma unroll
-                for (int k = 0; k < 4; ++k) m[k] = uniform_f(wave_max(T[k]));
+                for (int k = 0; k < 4; ++k) m[k] = uniform_f(wave_max(bt[k].y));
                 if (lane < 4) {
                     const float mine = lane == 0 ? m[0] : lane == 1 ? m[1] : lane == 2 ? m[2] : m[3];
                     __hip_atomic_store(my_tmax + lane, __float_as_uint(mine), __ATOMIC_RELAXED,
@@ -506,7 +580,7 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                 // stop a slice when every pixel's chunk-local T is below t_min
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    if (__any(T[k] >= t_min)) still |= 1u << k;
+                    if (__any(bt[k].y >= t_min)) still |= 1u << k;
             }
             const uint32_t newly = live & ~still;
             if (track && newly && lane == 0) {
@@ -539,7 +613,7 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         // partial (C, T) per pixel, folded by k_merge; layout [slot][k][lane]
         float4* p = partial + (size_t)slot * 256;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) p[k * 64 + lane] = make_float4(cr[k], cg[k], cb[k], T[k]);
+        for (int k = 0; k < 4; ++k) p[k * 64 + lane] = make_float4(rg[k].x, rg[k].y, bt[k].x, bt[k].y);
         return;
     }
     if (x >= a.width) return;
@@ -548,9 +622,10 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
     for (int k = 0; k < 4; ++k) {
         const int row = row_base + 4 * k + lrow;
         if (row >= a.height) continue;
-        const float r = cr[k] + T[k] * a.bg[0];
-        const float g = cg[k] + T[k] * a.bg[1];
-        const float b = cb[k] + T[k] * a.bg[2];
+        const float T = bt[k].y;
+        const float r = rg[k].x + T * a.bg[0];
+        const float g = rg[k].y + T * a.bg[1];
+        const float b = bt[k].x + T * a.bg[2];
         const size_t pidx = (size_t)row * a.width + x;
         if (a.out_layout == 0) {
             out[pidx] = r;
@@ -569,13 +644,15 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
 __device__ uint4 g_comp_trace[2 * kTraceMax];
 #endif
 
-#ifdef GSR_COMP_WPE
-#define GSR_COMP_OCC __attribute__((amdgpu_waves_per_eu(GSR_COMP_WPE, 8)))
-#else
-#define GSR_COMP_OCC
+// 8 waves per SIMD: the compiler's own choice is 65 VGPRs (7 waves); held to
+// 64 it spills one 8-byte value outside the record loop
+#ifndef GSR_COMP_WPE
+#define GSR_COMP_WPE 8
 #endif
+#define GSR_COMP_OCC __attribute__((amdgpu_waves_per_eu(GSR_COMP_WPE, 8)))
 template <int FRAG>
 __global__ __launch_bounds__(kThreads) GSR_COMP_OCC void k_composite(const uint4* __restrict__ desc,
+                                                        const uint32_t* __restrict__ order,
                                                         const uint32_t* __restrict__ n_chunks_dev,
                                                         const uint32_t* __restrict__ list,
                                                         const SplatRec* __restrict__ recs, CompositeArgs a,
@@ -583,8 +660,9 @@ __global__ __launch_bounds__(kThreads) GSR_COMP_OCC void k_composite(const uint4
                                                         uint32_t* __restrict__ sat, float4* __restrict__ tmax) {
     __shared__ float4 lds[kThreads / 64][kBatch * 3];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t slot = blockIdx.x * (kThreads / 64) + wave;
-    if (slot >= (uint32_t)a.num_tiles + n_chunks_dev[0]) return;  // device count of extra chunks
+    const uint32_t pos = blockIdx.x * (kThreads / 64) + wave;
+    if (pos >= (uint32_t)a.num_tiles + n_chunks_dev[0]) return;  // device count of extra chunks
+    const uint32_t slot = order[pos];
 #ifdef GSR_COMP_TRACE
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -738,22 +816,27 @@ static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float*
     return a;
 }
 
+size_t chunk_cnt_elems(int num_tiles) { return (size_t)num_tiles + 2 * ((size_t)num_tiles / kThreads + 1); }
+
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t* chunk_cnt, uint32_t* chunk_base,
-                  uint32_t* n_extra_dev, uint4* desc, float4* tmax, hipStream_t s) {
+                  uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax, hipStream_t s) {
 #ifndef GSR_COMP_BOUND
     tmax = nullptr;  // the published maxima are only read by the bound variant
 #endif
     const unsigned g = (unsigned)((num_tiles + kThreads - 1) / kThreads);
     // the per-block totals live in chunk_cnt past its num_tiles entries
-    k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_cnt + num_tiles);
+    uint32_t* block_extra = chunk_cnt + num_tiles;
+    uint32_t* block_full = block_extra + g;
+    k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, block_extra, block_full);
     GSR_LAUNCH_CHECK("chunk_count");
-    k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, chunk_cnt + num_tiles, chunk_cnt, chunk_base,
-                                         n_extra_dev, desc, tmax);
+    k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, block_extra, block_full, chunk_cnt, chunk_base,
+                                         n_extra_dev, desc, order, tmax);
     GSR_LAUNCH_CHECK("chunk_write");
     return GSR_OK;
 }
 
-int launch_composite(const uint4* desc, const uint32_t* n_chunks_dev, uint32_t max_chunks, const uint32_t* chunk_cnt,
+int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n_chunks_dev, uint32_t max_chunks,
+                     const uint32_t* chunk_cnt,
                      const uint32_t* chunk_base, uint32_t* sat, const uint32_t* tile_vals, const SplatRec* recs,
                      const FrameUniforms& u, int frag_class, float t_min, const float* bg, int out_layout, float* out,
                      float4* partial, float4* tmax, hipStream_t s) {
@@ -761,19 +844,19 @@ int launch_composite(const uint4* desc, const uint32_t* n_chunks_dev, uint32_t m
     const unsigned grid = (unsigned)((max_chunks + 3) / 4);
     switch (frag_class) {
         case kFragGauss:
-            k_composite<kFragGauss><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial, sat,
+            k_composite<kFragGauss><<<grid, kThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial, sat,
                                                               tmax);
             break;
         case kFragBillboard:
-            k_composite<kFragBillboard><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial,
+            k_composite<kFragBillboard><<<grid, kThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
                                                                   sat, tmax);
             break;
         case kFragFlatBall:
-            k_composite<kFragFlatBall><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial,
+            k_composite<kFragFlatBall><<<grid, kThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
                                                                  sat, tmax);
             break;
         default:
-            k_composite<kFragGaussBall><<<grid, kThreads, 0, s>>>(desc, n_chunks_dev, tile_vals, recs, a, out, partial,
+            k_composite<kFragGaussBall><<<grid, kThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
                                                                   sat, tmax);
             break;
     }

@@ -218,10 +218,13 @@ int launch_binning(const uint32_t* sorted_ids, const uint2* trect, uint32_t n_vi
                    hipStream_t s);
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
                        hipStream_t s);
-// chunk_cnt must hold num_tiles + num_tiles / 256 + 1 entries (block totals after the tiles)
+// chunk_cnt must hold chunk_cnt_elems(num_tiles) entries (block totals after the tiles);
+// order: one entry per chunk (dispatch position -> chunk slot)
+size_t chunk_cnt_elems(int num_tiles);
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t* chunk_cnt,
-                  uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, float4* tmax, hipStream_t s);
-int launch_composite(const uint4* desc, const uint32_t* n_chunks_dev, uint32_t max_chunks,
+                  uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
+                  hipStream_t s);
+int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n_chunks_dev, uint32_t max_chunks,
                      const uint32_t* chunk_cnt, const uint32_t* chunk_base, uint32_t* sat,
                      const uint32_t* tile_vals, const SplatRec* recs, const FrameUniforms& u,
                      int frag_class, float t_min, const float* bg, int out_layout, float* out,
