@@ -96,8 +96,8 @@ struct gsr_context {
     gsr::DevBuf<uint32_t> chunk_order;            // per chunk: dispatch position -> chunk slot
     gsr::DevBuf<float4> partial;                  // per chunk x 256 px (multi-chunk tiles)
     gsr::DevBuf<float4> tmax;                     // per chunk: published slice maxima of local T
-    uint32_t chunk = 128;                         // instances per compositing chunk (swept: 128 best latency;
-                                                  // 4-view throughput flat over 128..384)
+    uint32_t chunk = 192;                         // instances per compositing chunk (swept, 4 views in flight:
+                                                  // 192-256 best throughput (fewer partials), 128 best latency)
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
     uint32_t seq = 0;                       // frame sequence number the host waits for
     uint32_t* host_counters_dev = nullptr;  // its device address

@@ -18,6 +18,8 @@
 #pragma clang fp contract(off)
 #include "gsr_internal.h"
 
+#include <algorithm>
+
 namespace gsr {
 namespace {
 
@@ -491,13 +493,19 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess(const float
                                                          uint32_t* __restrict__ host_counters, uint32_t seq,
                                                          int32_t* __restrict__ radii) {
     __shared__ uint32_t s_cnt[kThreads / 64];
-    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    const uint64_t m = (i < n) ? vis_mask[i >> 6] : 0ull;
-    const bool vis = (m >> __lane_id()) & 1ull;
     uint32_t tiles = 0;
-    if (vis) tiles = preprocess_one<DEG>(pos_op, rot, scale, sh, n, u, m, i, wave_off, n_vis_dev, recs, depth_keys, trect,
-                                    radii);
-    else if (i < n && radii) radii[i] = 0;
+    // Grid-stride over blocks of kThreads Gaussians with a grid of ~4 blocks per
+    // CU: the waves drift out of phase, so one wave's loads overlap another's
+    // arithmetic.  (With one block per 256 Gaussians the resident waves ran in
+    // lock-step rounds of load-then-compute: 67 -> 63.5 us at 1M.)
+    for (int64_t i0 = (int64_t)blockIdx.x * kThreads; i0 < n; i0 += (int64_t)gridDim.x * kThreads) {
+        const int64_t i = i0 + threadIdx.x;
+        const uint64_t m = (i < n) ? vis_mask[i >> 6] : 0ull;
+        const bool vis = (m >> __lane_id()) & 1ull;
+        if (vis) tiles += preprocess_one<DEG>(pos_op, rot, scale, sh, n, u, m, i, wave_off, n_vis_dev, recs, depth_keys,
+                                             trect, radii);
+        else if (i < n && radii) radii[i] = 0;
+    }
     // instance total for the frame (sizes the tile sort without waiting for it)
     const uint32_t ws = wave_reduce_sum(tiles);
     if (__lane_id() == 0) s_cnt[threadIdx.x >> 6] = ws;
@@ -547,7 +555,14 @@ int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_
                       const uint32_t* wave_off, const uint32_t* n_vis_dev, SplatRec* recs, uint32_t* depth_keys,
                       uint2* trect, uint32_t* counters, unsigned long long* done_ctr, uint32_t* host_counters,
                       uint32_t seq, int32_t* radii, hipStream_t s) {
-    const unsigned grid = (unsigned)((sd.n + kThreads - 1) / kThreads);
+    static const unsigned max_grid = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return 4u * (unsigned)cus;  // ~4 resident blocks per CU (92 VGPRs: 5 waves/SIMD fit)
+    }();
+    const unsigned grid = std::min((unsigned)((sd.n + kThreads - 1) / kThreads), max_grid);
     // effective SH degree: the gates of gau_vert.glsl:289-313; -1 = colour not from SH
     const int m = u.render_mod;
     int deg = (u.sh_dim > 27 && m >= 3) ? 3 : (u.sh_dim > 12 && m >= 2) ? 2 : (u.sh_dim > 3 && m >= 1) ? 1 : 0;
