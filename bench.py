@@ -149,10 +149,17 @@ def main():
     ap.add_argument("--t-min", type=float, default=1e-4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=4,
-                    help="independent views in flight per GPU (own stream and context each, pipelined with "
-                         "gsr_render_begin/finish); 1 = one at a time")
+    ap.add_argument("--inflight", type=int, default=16,
+                    help="independent views in flight per GPU (own context each, pipelined with "
+                         "gsr_render_begin[_views]/finish); 1 = one at a time")
+    ap.add_argument("--share", type=int, default=None,
+                    help="views per shared scene pass (gsr_render_begin_views): the views in flight form "
+                         "inflight/share groups, one stream each, whose cull + preprocess read the scene once "
+                         "per group; 1 = off (one stream per view).  Default: 4 when --inflight is a multiple of 4 "
+                         "and >= 8, else 1")
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage HIP events")
+    ap.add_argument("--render-mod", type=int, default=6,
+                    help="render_mod uniform (experiments; 6 = SH:0~3, the reference default)")
     ap.add_argument("--box", default="none", choices=["none", "aabb", "obb"],
                     help="boundary-box cull (SURVEY.md 8d C5): aabb = compute_aabb min/max x 0.5 around "
                          "points_center; obb = euler(30, 15, 0) deg, +-1.5")
@@ -161,7 +168,11 @@ def main():
     # One hardware queue per in-flight view stream (+ torch's own): HIP maps
     # streams round-robin onto GPU_MAX_HW_QUEUES queues (4 by default), and two
     # view streams sharing a queue serialise.  Must be set before HIP starts.
-    want_q = min(32, max(8, args.inflight + 2))
+    share = args.share if args.share is not None else (4 if args.inflight % 4 == 0 and args.inflight >= 8 else 1)
+    share = max(1, share)
+    if args.inflight % share:
+        ap.error("--inflight must be a multiple of --share")
+    want_q = min(32, max(8, args.inflight // share + 2))  # one stream per view (share 1) or per group
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < want_q:
         os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
 
@@ -177,7 +188,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from gsviewer_amd import _lib
-    from gsviewer_amd.multiview import ViewPipeline, broadcast_scene, timed_region, view_of
+    from gsviewer_amd.multiview import ViewBatchPipeline, ViewPipeline, broadcast_scene, timed_region, view_of
     from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into
 
     _lib.load()
@@ -197,6 +208,7 @@ def main():
     cam = view_of(rank, H, W)
     camc = camera_from(cam)
     st = RenderSettings(t_min=args.t_min, out_layout=0)
+    st.render_mod = args.render_mod
     if args.box != "none":
         box = box_settings(g, args.box) if rank == 0 else None
         if world > 1:
@@ -215,12 +227,17 @@ def main():
     cams = [cam] + [view_of(rank + world * j, H, W) for j in range(1, K)]
     camcs = [camera_from(c) for c in cams]
     ctx = ctxs[0]
-    pipe = ViewPipeline(ctxs, streams, scene, camcs, st, outs)
+    if share == 1:
+        pipe = ViewPipeline(ctxs, streams, scene, camcs, st, outs)
+    else:
+        groups = [(ctxs[g:g + share], camcs[g:g + share], outs[g:g + share], streams[g])
+                  for g in range(0, K, share)]
+        pipe = ViewBatchPipeline(groups, scene, st)
 
     def serial_frame():
         render_into(ctx, scene, camc, st, outs[0])
 
-    for _ in range(max(args.warmup, K)):
+    for _ in range(max(args.warmup // share, 2 * K // share)):
         pipe.step()
     pipe.drain()
     torch.cuda.synchronize()
@@ -233,7 +250,13 @@ def main():
             pipe.step()
         pipe.drain()
 
-    elapsed = timed_region(lambda: pipelined(args.steps), 1, dev)
+    if share == 1:
+        elapsed = timed_region(lambda: pipelined(args.steps), 1, dev)
+    else:
+        # a step renders a group of `share` frames: time whole steps covering
+        # args.steps frames, normalised to args.steps frames
+        calls = (args.steps + share - 1) // share
+        elapsed = timed_region(lambda: pipelined(calls), 1, dev) * args.steps / (calls * share)
     # single-view latency: the same number of frames of view 0, one at a time
     latency = timed_region(serial_frame, args.steps, dev) if K > 1 else elapsed
 
@@ -334,7 +357,9 @@ def main():
                    "views": f"view v = default camera yawed v*45 deg; rank r renders v = r + {world}*j, j < {K}, "
                             f"round-robin, one stream per view",
                    "t_min": args.t_min,
-                   "parallelism": f"replicated scene, {world * K} independent views ({K} per GPU in flight)"},
+                   "parallelism": f"replicated scene, {world * K} independent views ({K} per GPU in flight)"
+                                  + (f", cull + preprocess shared by groups of {share} views (one scene pass "
+                                     f"per group)" if share > 1 else "")},
         "frame_stats": stats,
         "stage_ms": stage,
         "roofline": roof,

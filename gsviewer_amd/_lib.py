@@ -99,6 +99,10 @@ SIGNATURES = {
     "gsr_render": (ctypes.c_int, [_P, _P, ctypes.POINTER(GsrCamera), ctypes.POINTER(GsrSettings), _P, _P, _P]),
     "gsr_render_begin": (ctypes.c_int, [_P, _P, ctypes.POINTER(GsrCamera), ctypes.POINTER(GsrSettings), _P, _P, _P]),
     "gsr_render_finish": (ctypes.c_int, [_P, _P]),
+    "gsr_render_begin_views": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int32, _P, ctypes.POINTER(GsrCamera),
+                                              ctypes.POINTER(GsrSettings), ctypes.POINTER(_P), ctypes.POINTER(_P),
+                                              _P]),
+    "gsr_render_begin_sort": (ctypes.c_int, [_P, _P]),
     "gsr_context_stats": (ctypes.c_int, [_P, ctypes.POINTER(GsrFrameStats)]),
     "gsr_sort_depth": (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_float * 16), _P, _P]),
     "gsr_debug_host_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
@@ -120,7 +124,8 @@ STAGES = ["cull", "preprocess", "depth_sort", "binning", "tile_sort", "tile_rang
 
 GSR_DEBUG_RECORDS, GSR_DEBUG_DEPTH_ORDER, GSR_DEBUG_TILE_RANGES, GSR_DEBUG_TILE_LIST = 0, 1, 2, 3
 
-ABI_VERSION = 2
+ABI_VERSION = 3
+MAX_VIEWS = 8  # GSR_MAX_VIEWS (include/gsr.h)
 
 _lib = None
 _lock = threading.Lock()

@@ -75,6 +75,7 @@ struct PendingFrame {
     size_t n = 0;
     int slot = 0;
     uint32_t *ka = nullptr, *va = nullptr, *kb = nullptr, *vb = nullptr;  // depth sort buffers (result in ka/va)
+    bool sort_ready = false;  // gsr_render_begin_views done, gsr_render_begin_sort not yet
 };
 }  // namespace gsr
 
@@ -433,7 +434,8 @@ int gsr_context_stats(const gsr_context* c, gsr_frame_stats* out) {
 int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, float* out,
                      int32_t* radii, void* stream) {
     if (!c || !sc || !cam || !st || !out) return set_error(GSR_ERR_INVALID, "null argument");
-    if (c->pend.active) return set_error(GSR_ERR_INVALID, "render_begin: the previous frame was not finished");
+    if (c->pend.active || c->pend.sort_ready)
+        return set_error(GSR_ERR_INVALID, "render_begin: the previous frame was not finished");
     hipStream_t s = (hipStream_t)stream;
     const auto h0 = std::chrono::steady_clock::now();
     FrameUniforms u;
@@ -495,6 +497,92 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
     f.n = n;
     f.slot = slot;
     c->host_ms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+    return GSR_OK;
+}
+
+int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene* sc, const gsr_camera* cams,
+                           const gsr_settings* st, float* const* outs, int32_t* const* radii, void* stream) {
+    if (!ctxs || !sc || !cams || !st || !outs) return set_error(GSR_ERR_INVALID, "null argument");
+    if (k < 1 || k > GSR_MAX_VIEWS) return set_error(GSR_ERR_INVALID, "render_begin_views: k out of range");
+    for (int v = 0; v < k; ++v) {
+        if (!ctxs[v] || !outs[v]) return set_error(GSR_ERR_INVALID, "null argument");
+        if (ctxs[v]->pend.active || ctxs[v]->pend.sort_ready)
+            return set_error(GSR_ERR_INVALID, "render_begin_views: a view's previous frame was not finished");
+        if (ctxs[v]->prof_on) return set_error(GSR_ERR_INVALID, "render_begin_views: stage profiling is per view only");
+        for (int w = 0; w < v; ++w)
+            if (ctxs[w] == ctxs[v]) return set_error(GSR_ERR_INVALID, "render_begin_views: contexts must differ");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const size_t n = (size_t)sc->d.n;
+    FrameUniforms u[GSR_MAX_VIEWS];
+    ViewCullArgs cull[GSR_MAX_VIEWS];
+    ViewPreArgs pre[GSR_MAX_VIEWS];
+    int rc;
+    for (int v = 0; v < k; ++v) {
+        gsr_context* c = ctxs[v];
+        const auto h0 = std::chrono::steady_clock::now();
+        if ((rc = build_uniforms(sc, &cams[v], st, u[v]))) return rc;
+        const int num_tiles = u[v].tiles_x * u[v].tiles_y;
+        if ((rc = ensure_scene_buffers(c, n))) return rc;
+        const ZeroLayout zl(num_tiles);
+        if ((rc = c->zero.ensure(zl.total, "zero block"))) return rc;
+        uint32_t* counters = c->zero.p + zl.counters;
+        c->stats = gsr_frame_stats{};
+        c->stats.n_gaussians = (int64_t)n;
+        c->stats.tiles_x = u[v].tiles_x;
+        c->stats.tiles_y = u[v].tiles_y;
+        c->last_depth_order = c->last_tile_list = nullptr;
+        c->last_tiles = num_tiles;
+        c->last_ranges = reinterpret_cast<uint2*>(c->zero.p + zl.ranges);
+        if (n == 0) GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * zl.total, s));
+        cull[v] = ViewCullArgs{&u[v], c->vis_mask.p, c->wave_counts.p, c->block_ranges.p, c->zero.p + zl.cleared,
+                               (uint32_t)(zl.total - zl.cleared)};
+        pre[v] = ViewPreArgs{&u[v], c->vis_mask.p, c->wave_counts.p, counters + 0, c->recs.p, c->keys_a.p,
+                             c->trect.p, counters, c->done_ctr.p, c->host_counters_dev, radii ? radii[v] : nullptr,
+                             ++c->seq};
+        PendingFrame& f = c->pend;
+        f.u = u[v];
+        f.t_min = st->t_min;
+        std::memcpy(f.bg, st->bg, sizeof(f.bg));
+        f.out_layout = st->out_layout;
+        f.out = outs[v];
+        f.n = n;
+        f.slot = (int)(c->frame_idx & 1);
+        c->host_ms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+    }
+    if (n > 0) {
+        if ((rc = launch_cull_views(sc->d, cull, k, s))) return rc;
+        const size_t nw = (n + 63) / 64;
+        for (int v = 0; v < k; ++v) {
+            gsr_context* c = ctxs[v];
+            const ZeroLayout zl(u[v].tiles_x * u[v].tiles_y);
+            // visible-compaction offsets + V, and the frame's depth-key range
+            if ((rc = scan_exclusive(c->wave_counts.p, c->wave_counts.p, nw, c->scan_tmp.p, c->zero.p + zl.counters, s,
+                                     c->block_ranges.p, (n + kCullBlock - 1) / kCullBlock, c->zero.p + zl.key_range)))
+                return rc;
+        }
+        if ((rc = launch_preprocess_views(sc->d, pre, k, s))) return rc;
+    }
+    for (int v = 0; v < k; ++v) ctxs[v]->pend.sort_ready = true;
+    return GSR_OK;
+}
+
+int gsr_render_begin_sort(gsr_context* c, void* stream) {
+    if (!c) return set_error(GSR_ERR_INVALID, "null argument");
+    PendingFrame& f = c->pend;
+    if (!f.sort_ready) return set_error(GSR_ERR_INVALID, "render_begin_sort: no gsr_render_begin_views frame");
+    hipStream_t s = (hipStream_t)stream;
+    const ZeroLayout zl(f.u.tiles_x * f.u.tiles_y);
+    uint32_t* counters = c->zero.p + zl.counters;
+    // depth sort over the upper bound N; the device count V bounds the work
+    f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
+    int rc;
+    if (f.n > 0 && (rc = sort_pairs(c, &f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters + 0, 32, kDepthPasses,
+                                    c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s)))
+        return rc;
+    f.sort_ready = false;
+    f.active = true;
+    f.stream = s;
     return GSR_OK;
 }
 

@@ -210,6 +210,33 @@ int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_
                       int32_t* radii, hipStream_t s);
 int launch_depth_keys_all(const SceneData& sd, const float* V, uint32_t* keys, hipStream_t s);
 
+// Several views of one scene (gsr_render_begin_views): one pass over the scene.
+constexpr int kMaxViews = GSR_MAX_VIEWS;
+struct ViewCullArgs {
+    const FrameUniforms* u;
+    uint64_t* vis_mask;
+    uint32_t* wave_counts;
+    uint2* block_ranges;
+    uint32_t* zero_words;
+    uint32_t n_zero;
+};
+struct ViewPreArgs {
+    const FrameUniforms* u;
+    const uint64_t* vis_mask;
+    const uint32_t* wave_off;
+    const uint32_t* n_vis_dev;
+    SplatRec* recs;
+    uint32_t* depth_keys;
+    uint2* trect;
+    uint32_t* counters;
+    unsigned long long* done_ctr;
+    uint32_t* host_counters;
+    int32_t* radii;
+    uint32_t seq;
+};
+int launch_cull_views(const SceneData& sd, const ViewCullArgs* views, int k, hipStream_t s);
+int launch_preprocess_views(const SceneData& sd, const ViewPreArgs* views, int k, hipStream_t s);
+
 // composite.hip
 size_t bin_tmp_elems(size_t n_vis);
 // trect_sorted: n_vis uint2 of scratch (the rects in depth order)

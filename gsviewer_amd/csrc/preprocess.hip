@@ -147,23 +147,15 @@ __device__ __forceinline__ uint32_t float_order_key(float f) {
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
-// Also clears the frame's zero block (tile ranges, saturation words): they
-// are first used several launches later, so no memset launch is needed.
-__global__ __launch_bounds__(kThreads) void k_cull(const float4* __restrict__ pos_op, int64_t n, FrameUniforms u,
-                                                   uint64_t* __restrict__ vis_mask, uint32_t* __restrict__ wave_counts,
-                                                   uint2* __restrict__ block_ranges, uint32_t* __restrict__ zero_words,
-                                                   uint32_t n_zero) {
-    static_assert(kThreads == kCullBlock, "one key range per cull block");
-    __shared__ uint2 s_kr[kThreads / 64];
-    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    // write-through (sc1) stores: several of these words are later updated by
-    // atomics, which act at the coherence point, not in this XCD's L2
-    for (int64_t z = i; z < (int64_t)n_zero; z += (int64_t)gridDim.x * kThreads)
-        __hip_atomic_store(zero_words + z, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// One view's visibility of the block's Gaussians: the wave's ballot and
+// count, and the block's depth-key range {~kmin, kmax} of its visible ones.
+// Ends with a barrier, so s_kr can be reused by the next view.
+__device__ __forceinline__ void cull_view(const float4 p, bool in_range, int64_t i, const FrameUniforms& u,
+                                          uint64_t* __restrict__ vis_mask, uint32_t* __restrict__ wave_counts,
+                                          uint2* __restrict__ block_ranges, uint2* s_kr) {
     bool vis = false;
     uint32_t key = 0;
-    if (i < n) {
-        const float4 p = pos_op[i];
+    if (in_range) {
         const Projected pr = project(p.x, p.y, p.z, u);
         vis = pr.vis;
         key = float_order_key(-pr.pv[2]);  // the depth key k_preprocess writes
@@ -188,6 +180,55 @@ __global__ __launch_bounds__(kThreads) void k_cull(const float4* __restrict__ po
         for (int w = 1; w < kThreads / 64; ++w) r = make_uint2(max(r.x, s_kr[w].x), max(r.y, s_kr[w].y));
         block_ranges[blockIdx.x] = r;
     }
+    __syncthreads();
+}
+
+// write-through (sc1) stores: several of these words are later updated by
+// atomics, which act at the coherence point, not in this XCD's L2
+__device__ __forceinline__ void clear_words(uint32_t* zero_words, uint32_t n_zero) {
+    for (int64_t z = (int64_t)blockIdx.x * kThreads + threadIdx.x; z < (int64_t)n_zero;
+         z += (int64_t)gridDim.x * kThreads)
+        __hip_atomic_store(zero_words + z, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Also clears the frame's zero block (tile ranges, saturation words): they
+// are first used several launches later, so no memset launch is needed.
+__global__ __launch_bounds__(kThreads) void k_cull(const float4* __restrict__ pos_op, int64_t n, FrameUniforms u,
+                                                   uint64_t* __restrict__ vis_mask, uint32_t* __restrict__ wave_counts,
+                                                   uint2* __restrict__ block_ranges, uint32_t* __restrict__ zero_words,
+                                                   uint32_t n_zero) {
+    static_assert(kThreads == kCullBlock, "one key range per cull block");
+    __shared__ uint2 s_kr[kThreads / 64];
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    clear_words(zero_words, n_zero);
+    const float4 p = i < n ? pos_op[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    cull_view(p, i < n, i, u, vis_mask, wave_counts, block_ranges, s_kr);
+}
+
+// Several views of one scene (gsr_render_begin_views): each position is read
+// once for all of them.
+struct ViewCull {
+    FrameUniforms u;
+    uint64_t* vis_mask;
+    uint32_t* wave_counts;
+    uint2* block_ranges;
+    uint32_t* zero_words;
+    uint32_t n_zero;
+};
+struct ViewsCull {
+    ViewCull v[kMaxViews];
+    int32_t k;
+};
+static_assert(sizeof(ViewsCull) <= 3584, "kernel argument size");
+
+__global__ __launch_bounds__(kThreads) void k_cull_views(const float4* __restrict__ pos_op, int64_t n, ViewsCull vc) {
+    __shared__ uint2 s_kr[kThreads / 64];
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    for (int v = 0; v < vc.k; ++v) clear_words(vc.v[v].zero_words, vc.v[v].n_zero);
+    const float4 p = i < n ? pos_op[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+    for (int v = 0; v < vc.k; ++v)
+        cull_view(p, i < n, i, vc.v[v].u, vc.v[v].vis_mask, vc.v[v].wave_counts, vc.v[v].block_ranges, s_kr);
 }
 
 struct V3 {
@@ -283,6 +324,42 @@ __device__ __forceinline__ V3 sh_color(const float (&f)[48], float x, float y, f
 
 __device__ __forceinline__ float clamp01(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
 
+// The scene data of one Gaussian at effective SH degree DEG.
+template <int DEG>
+struct GaussLoad {
+    float4 po, q1, sc4;
+    float f[48];
+};
+
+// Issue every load of Gaussian i (all unconditional at this DEG), the ones
+// needed first first: vmcnt waits are in issue order.
+template <int DEG>
+__device__ __forceinline__ void load_gaussian(GaussLoad<DEG>& g, const float4* __restrict__ pos_op,
+                                              const float4* __restrict__ rot, const float4* __restrict__ scale,
+                                              const float4* __restrict__ sh, int64_t n, int64_t i) {
+    g.po = pos_op[i];
+    g.q1 = rot[i];
+    g.sc4 = scale[i];
+#pragma unroll
+    for (int p = 0; p < 12; ++p) {
+        if (p < sh_planes_for<DEG>()) {
+            const float4 t = load_plane(sh, n, p, i);
+            g.f[4 * p + 0] = t.x;
+            g.f[4 * p + 1] = t.y;
+            g.f[4 * p + 2] = t.z;
+            g.f[4 * p + 3] = t.w;
+        } else {
+            g.f[4 * p + 0] = g.f[4 * p + 1] = g.f[4 * p + 2] = g.f[4 * p + 3] = 0.f;
+        }
+    }
+}
+
+template <int DEG>
+__device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, const FrameUniforms& u, uint64_t m,
+                                                       int64_t i, uint32_t slot_base, SplatRec* __restrict__ recs,
+                                                       uint32_t* __restrict__ depth_keys, uint2* __restrict__ trect,
+                                                       int32_t* __restrict__ radii);
+
 // Per-Gaussian body of k_preprocess for a visible lane; returns the number of
 // 16x16 tiles its covered pixel rectangle touches.
 template <int DEG>
@@ -293,29 +370,25 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
                                                   const uint32_t* __restrict__ n_vis_dev, SplatRec* __restrict__ recs,
                                                   uint32_t* __restrict__ depth_keys, uint2* __restrict__ trect,
                                                   int32_t* __restrict__ radii) {
-    // issue every load of this Gaussian up front (all unconditional at this
-    // DEG), the ones needed first first: vmcnt waits are in issue order
-    const float4 po = pos_op[i];
-    const float4 q1 = rot[i];
-    const float4 sc4 = scale[i];
-    float f[48];
-#pragma unroll
-    for (int p = 0; p < 12; ++p) {
-        if (p < sh_planes_for<DEG>()) {
-            const float4 t = load_plane(sh, n, p, i);
-            f[4 * p + 0] = t.x;
-            f[4 * p + 1] = t.y;
-            f[4 * p + 2] = t.z;
-            f[4 * p + 3] = t.w;
-        } else {
-            f[4 * p + 0] = f[4 * p + 1] = f[4 * p + 2] = f[4 * p + 3] = 0.f;
-        }
-    }
+    GaussLoad<DEG> g;
+    load_gaussian<DEG>(g, pos_op, rot, scale, sh, n, i);
     const uint32_t slot_base = n_vis_dev[0] - 1u - wave_off[i >> 6];
     // keep the compiler from sinking the loads below the arithmetic (it would
     // otherwise wait for pos/rot/scale before issuing the SH planes: two
     // dependent memory round trips per wave instead of one)
     __builtin_amdgcn_sched_barrier(0);
+    return preprocess_compute<DEG>(g, u, m, i, slot_base, recs, depth_keys, trect, radii);
+}
+
+// Everything after the loads: the vertex stage of one view for a visible lane.
+template <int DEG>
+__device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, const FrameUniforms& u, uint64_t m,
+                                                       int64_t i, uint32_t slot_base, SplatRec* __restrict__ recs,
+                                                       uint32_t* __restrict__ depth_keys, uint2* __restrict__ trect,
+                                                       int32_t* __restrict__ radii) {
+    const float4 po = g.po;
+    const float4 q1 = g.q1;
+    const float4 sc4 = g.sc4;
     const float x = po.x, y = po.y, z = po.z;
     const Projected pr = project(x, y, z, u);
 
@@ -436,7 +509,7 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
         if (mode == -1) nrm = normalize3(nrm.x, nrm.y, nrm.z);
         col = V3{0.5f * (nrm.x + 1.0f), 0.5f * (nrm.y + 1.0f), 0.5f * (nrm.z + 1.0f)};
     } else {
-        col = sh_color<DEG < 0 ? 0 : DEG>(f, x, y, z, u);
+        col = sh_color<DEG < 0 ? 0 : DEG>(g.f, x, y, z, u);
     }
     if (mode != -6) {  // unorm target clamps the fragment colour
         col.x = clamp01(col.x);
@@ -533,6 +606,79 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess(const float
 }
 
 
+// Several views of one scene (gsr_render_begin_views): each Gaussian's scene
+// data is loaded once and run through the vertex stage of every view it is
+// visible in.  Per view, the same outputs, slots and publication protocol as
+// k_preprocess.
+struct ViewPre {
+    FrameUniforms u;
+    const uint64_t* vis_mask;
+    const uint32_t* wave_off;
+    const uint32_t* n_vis_dev;
+    SplatRec* recs;
+    uint32_t* depth_keys;
+    uint2* trect;
+    uint32_t* counters;
+    unsigned long long* done_ctr;
+    uint32_t* host_counters;
+    int32_t* radii;
+    uint32_t seq;
+};
+struct ViewsPre {
+    ViewPre v[kMaxViews];
+    int32_t k;
+};
+static_assert(sizeof(ViewsPre) <= 3584, "kernel argument size");
+
+template <int DEG>
+__global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_views(const float4* __restrict__ pos_op,
+                                                                           const float4* __restrict__ rot,
+                                                                           const float4* __restrict__ scale,
+                                                                           const float4* __restrict__ sh, int64_t n,
+                                                                           ViewsPre vs) {
+    __shared__ uint32_t s_cnt[kMaxViews][kThreads / 64];
+    const int wave = threadIdx.x >> 6;
+    const int lane = __lane_id();
+    if (threadIdx.x < kMaxViews * (kThreads / 64)) s_cnt[threadIdx.x / (kThreads / 64)][threadIdx.x % (kThreads / 64)] = 0u;
+    __syncthreads();
+    for (int64_t i0 = (int64_t)blockIdx.x * kThreads; i0 < n; i0 += (int64_t)gridDim.x * kThreads) {
+        const int64_t i = i0 + threadIdx.x;
+        bool any = false;
+        for (int v = 0; v < vs.k; ++v) any |= i < n && ((vs.v[v].vis_mask[i >> 6] >> lane) & 1ull);
+        GaussLoad<DEG> g;
+        if (any) load_gaussian<DEG>(g, pos_op, rot, scale, sh, n, i);
+#pragma unroll 1
+        for (int v = 0; v < vs.k; ++v) {
+            const ViewPre& V = vs.v[v];
+            const uint64_t m = i < n ? V.vis_mask[i >> 6] : 0ull;
+            uint32_t tiles = 0;
+            if ((m >> lane) & 1ull) {
+                const uint32_t slot_base = V.n_vis_dev[0] - 1u - V.wave_off[i >> 6];
+                tiles = preprocess_compute<DEG>(g, V.u, m, i, slot_base, V.recs, V.depth_keys, V.trect, V.radii);
+            } else if (i < n && V.radii) {
+                V.radii[i] = 0;
+            }
+            const uint32_t ws = wave_reduce_sum(tiles);
+            if (lane == 0) s_cnt[v][wave] += ws;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)vs.k) {  // one thread per view: k_preprocess's completion protocol
+        const ViewPre& V = vs.v[threadIdx.x];
+        const uint32_t b = s_cnt[threadIdx.x][0] + s_cnt[threadIdx.x][1] + s_cnt[threadIdx.x][2] + s_cnt[threadIdx.x][3];
+        const unsigned long long old = atomicAdd(V.done_ctr, (1ull << 40) | (unsigned long long)b);
+        if ((old >> 40) == (unsigned long long)(gridDim.x - 1)) {
+            const uint32_t n_dup = (uint32_t)(old & ((1ull << 40) - 1)) + b;
+            const uint32_t n_vis = V.n_vis_dev[0];
+            V.counters[1] = n_dup;
+            __hip_atomic_store(V.host_counters + 0, n_vis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(V.host_counters + 1, n_dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(V.host_counters + 2, V.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(V.done_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void k_depth_keys_all(const float4* __restrict__ pos_op, int64_t n, float v8,
                                                              float v9, float v10, float v11, uint32_t* __restrict__ keys) {
     const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -542,6 +688,25 @@ __global__ __launch_bounds__(kThreads) void k_depth_keys_all(const float4* __res
 }
 
 }  // namespace
+
+static unsigned preprocess_grid(int64_t n) {
+    static const unsigned max_grid = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return 4u * (unsigned)cus;  // ~4 resident blocks per CU (92 VGPRs: 5 waves/SIMD fit)
+    }();
+    return std::max(1u, std::min((unsigned)((n + kThreads - 1) / kThreads), max_grid));
+}
+
+static int effective_deg(const FrameUniforms& u) {
+    // effective SH degree: the gates of gau_vert.glsl:289-313; -1 = colour not from SH
+    const int m = u.render_mod;
+    int deg = (u.sh_dim > 27 && m >= 3) ? 3 : (u.sh_dim > 12 && m >= 2) ? 2 : (u.sh_dim > 3 && m >= 1) ? 1 : 0;
+    if (m == -3 || m == -2 || m == -1) deg = -1;
+    return deg;
+}
 
 int launch_cull(const SceneData& sd, const FrameUniforms& u, uint64_t* vis_mask, uint32_t* wave_counts,
                 uint2* block_ranges, uint32_t* zero_words, uint32_t n_zero, hipStream_t s) {
@@ -555,18 +720,8 @@ int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_
                       const uint32_t* wave_off, const uint32_t* n_vis_dev, SplatRec* recs, uint32_t* depth_keys,
                       uint2* trect, uint32_t* counters, unsigned long long* done_ctr, uint32_t* host_counters,
                       uint32_t seq, int32_t* radii, hipStream_t s) {
-    static const unsigned max_grid = [] {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        return 4u * (unsigned)cus;  // ~4 resident blocks per CU (92 VGPRs: 5 waves/SIMD fit)
-    }();
-    const unsigned grid = std::min((unsigned)((sd.n + kThreads - 1) / kThreads), max_grid);
-    // effective SH degree: the gates of gau_vert.glsl:289-313; -1 = colour not from SH
-    const int m = u.render_mod;
-    int deg = (u.sh_dim > 27 && m >= 3) ? 3 : (u.sh_dim > 12 && m >= 2) ? 2 : (u.sh_dim > 3 && m >= 1) ? 1 : 0;
-    if (m == -3 || m == -2 || m == -1) deg = -1;
+    const unsigned grid = preprocess_grid(sd.n);
+    const int deg = effective_deg(u);
 #define GSR_PRE(D)                                                                                                  \
     k_preprocess<D><<<grid, kThreads, 0, s>>>(sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, u, vis_mask, wave_off,    \
                                               n_vis_dev, recs, depth_keys, trect, counters, done_ctr,            \
@@ -580,6 +735,45 @@ int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_
     }
 #undef GSR_PRE
     GSR_LAUNCH_CHECK("preprocess");
+    return GSR_OK;
+}
+
+int launch_cull_views(const SceneData& sd, const ViewCullArgs* views, int k, hipStream_t s) {
+    if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "cull_views: view count out of range");
+    ViewsCull vc{};
+    vc.k = k;
+    for (int v = 0; v < k; ++v) {
+        const ViewCullArgs& a = views[v];
+        vc.v[v] = ViewCull{*a.u, a.vis_mask, a.wave_counts, a.block_ranges, a.zero_words, a.n_zero};
+    }
+    const unsigned grid = (unsigned)((sd.n + kThreads - 1) / kThreads);
+    k_cull_views<<<grid, kThreads, 0, s>>>(sd.pos_op, sd.n, vc);
+    GSR_LAUNCH_CHECK("cull_views");
+    return GSR_OK;
+}
+
+int launch_preprocess_views(const SceneData& sd, const ViewPreArgs* views, int k, hipStream_t s) {
+    if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "preprocess_views: view count out of range");
+    ViewsPre vp{};
+    vp.k = k;
+    const int deg = effective_deg(*views[0].u);
+    for (int v = 0; v < k; ++v) {
+        const ViewPreArgs& a = views[v];
+        if (effective_deg(*a.u) != deg) return set_error(GSR_ERR_INVALID, "preprocess_views: views differ in SH degree");
+        vp.v[v] = ViewPre{*a.u, a.vis_mask, a.wave_off, a.n_vis_dev, a.recs, a.depth_keys, a.trect,
+                          a.counters, a.done_ctr, a.host_counters, a.radii, a.seq};
+    }
+    const unsigned grid = preprocess_grid(sd.n);
+#define GSR_PREV(D) k_preprocess_views<D><<<grid, kThreads, 0, s>>>(sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, vp)
+    switch (deg) {
+        case -1: GSR_PREV(-1); break;
+        case 0: GSR_PREV(0); break;
+        case 1: GSR_PREV(1); break;
+        case 2: GSR_PREV(2); break;
+        default: GSR_PREV(3); break;
+    }
+#undef GSR_PREV
+    GSR_LAUNCH_CHECK("preprocess_views");
     return GSR_OK;
 }
 

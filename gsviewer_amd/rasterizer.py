@@ -234,6 +234,36 @@ def render_finish(ctx: HipContext, stream=None):
     _lib.check(_lib.load().gsr_render_finish(ctx.handle, _stream_handle(stream)), "gsr_render_finish")
 
 
+def render_begin_views(ctxs, scene: HipScene, cams, settings: RenderSettings, outs, radii=None, stream=None):
+    """gsr_render_begin_views: the cull and preprocess of several views of one
+    scene in one pass over it, enqueued on `stream`.  Then, per view, make its
+    own stream wait for `stream` and call render_begin_sort(ctx, its stream),
+    and later render_finish(ctx, its stream)."""
+    k = len(ctxs)
+    if not (1 <= k <= _lib.MAX_VIEWS) or len(cams) != k or len(outs) != k:
+        raise RuntimeError(f"render_begin_views: 1..{_lib.MAX_VIEWS} views with one camera and output each")
+    for cam, out in zip(cams, outs):
+        if not (out.is_cuda and out.dtype == torch.float32 and out.is_contiguous()):
+            raise RuntimeError("out must be a contiguous float32 CUDA tensor")
+        if out.numel() != 3 * cam.width * cam.height:
+            raise RuntimeError("out has the wrong number of elements")
+    P = ctypes.c_void_p
+    ctx_arr = (P * k)(*[c.handle for c in ctxs])
+    cam_arr = (_lib.GsrCamera * k)(*cams)
+    out_arr = (P * k)(*[o.data_ptr() for o in outs])
+    rad_arr = (P * k)(*[(r.data_ptr() if r is not None else None) for r in radii]) if radii is not None else None
+    st = settings.to_c()
+    _lib.check(_lib.load().gsr_render_begin_views(ctx_arr, k, scene.handle, cam_arr, ctypes.byref(st), out_arr,
+                                                  rad_arr, _stream_handle(stream)), "gsr_render_begin_views")
+    return outs
+
+
+def render_begin_sort(ctx: HipContext, stream=None):
+    """gsr_render_begin_sort: the depth sort of a view begun by
+    render_begin_views, on the view's own stream."""
+    _lib.check(_lib.load().gsr_render_begin_sort(ctx.handle, _stream_handle(stream)), "gsr_render_begin_sort")
+
+
 _default_ctx = {}
 
 

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 2
+#define GSR_ABI_VERSION 3
 
 typedef enum gsr_status {
     GSR_OK = 0,
@@ -145,6 +145,21 @@ int gsr_render_begin(gsr_context* ctx, const gsr_scene* scene, const gsr_camera*
                      const gsr_settings* settings, float* out_image_dev, int32_t* radii_dev,
                      void* stream);
 int gsr_render_finish(gsr_context* ctx, void* stream);
+
+/* Several views of ONE scene begun together (stereo, multi-camera capture, a
+ * batch of views in flight): the cull and preprocess of all k views
+ * (k <= GSR_MAX_VIEWS, one context each, same settings) read the scene once,
+ * in one pass enqueued on `stream`.  Then, per view, after its own stream has
+ * been made to wait for `stream` (an event), gsr_render_begin_sort(ctx, its
+ * stream) enqueues the depth sort, and gsr_render_finish(ctx, its stream)
+ * completes the frame as for gsr_render_begin.  Results are identical to
+ * rendering each view alone.  cams[k], outs[k], radii[k] (radii may be NULL,
+ * or hold NULL entries). */
+#define GSR_MAX_VIEWS 8
+int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene* scene,
+                           const gsr_camera* cams, const gsr_settings* settings,
+                           float* const* out_images_dev, int32_t* const* radii_dev, void* stream);
+int gsr_render_begin_sort(gsr_context* ctx, void* stream);
 
 int gsr_context_stats(const gsr_context* ctx, gsr_frame_stats* out);
 

@@ -93,3 +93,72 @@ def test_contexts_share_one_scene_concurrently(gpu):
     for c in ctxs + [ref]:
         c.close()
     scene.close()
+
+
+def test_shared_scene_pass_matches_serial_renders(gpu):
+    """gsr_render_begin_views (one cull + preprocess pass over the scene for a
+    group of views) through ViewBatchPipeline with two groups: images, radii
+    and counts identical to each view rendered alone."""
+    import torch
+
+    from gsviewer_amd.multiview import ViewBatchPipeline
+    from gsviewer_amd.rasterizer import HipContext, render_into
+    K, G = 3, 2
+    scene, st, cams, ctxs, streams, outs = _setup(K * G)
+    want, want_stats = [], []
+    ref_ctx = HipContext()
+    for k in range(K * G):
+        o = torch.empty_like(outs[k])
+        render_into(ref_ctx, scene, cams[k], st, o)
+        torch.cuda.synchronize()
+        want.append(o)
+        want_stats.append(ref_ctx.stats())
+    groups = [(ctxs[g * K:(g + 1) * K], cams[g * K:(g + 1) * K], outs[g * K:(g + 1) * K], streams[g])
+              for g in range(G)]
+    pipe = ViewBatchPipeline(groups, scene, st)
+    for _ in range(3 * G + 1):  # every group several times, one group a step ahead
+        pipe.step()
+    pipe.drain()
+    torch.cuda.synchronize()
+    for k in range(K * G):
+        np.testing.assert_array_equal(outs[k].cpu().numpy(), want[k].cpu().numpy(), err_msg=f"view {k}")
+        got = ctxs[k].stats()
+        for f in ("n_visible", "n_instances"):
+            assert got[f] == want_stats[k][f], (k, f)
+    for c in ctxs + [ref_ctx]:
+        c.close()
+    scene.close()
+
+
+def test_shared_scene_pass_radii_and_errors(gpu):
+    import torch
+
+    from gsviewer_amd.rasterizer import (HipContext, render_begin_sort, render_begin_views, render_finish,
+                                         render_into)
+    scene, st, cams, ctxs, streams, outs = _setup(2, n=5000)
+    n = 5000
+    radii = [torch.full((n,), -7, dtype=torch.int32, device="cuda") for _ in range(2)]
+    with pytest.raises(RuntimeError, match="no gsr_render_begin_views frame"):
+        render_begin_sort(ctxs[0], streams[0])
+    with pytest.raises(RuntimeError, match="contexts must differ"):
+        render_begin_views([ctxs[0], ctxs[0]], scene, cams[:2], st, outs[:2])
+    s = torch.cuda.Stream()
+    render_begin_views(ctxs, scene, cams[:2], st, outs, radii=radii, stream=s)
+    with pytest.raises(RuntimeError, match="not finished"):
+        render_begin_views(ctxs, scene, cams[:2], st, outs, stream=s)
+    s.synchronize()
+    for c, vs in zip(ctxs, streams):
+        render_begin_sort(c, vs)
+        render_finish(c, vs)
+    torch.cuda.synchronize()
+    ref = HipContext()
+    for k in range(2):
+        o = torch.empty_like(outs[k])
+        r = torch.empty_like(radii[k])
+        render_into(ref, scene, cams[k], st, o, r)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(outs[k].cpu().numpy(), o.cpu().numpy())
+        np.testing.assert_array_equal(radii[k].cpu().numpy(), r.cpu().numpy())
+    for c in ctxs + [ref]:
+        c.close()
+    scene.close()
