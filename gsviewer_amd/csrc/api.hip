@@ -586,6 +586,37 @@ int gsr_render_begin_sort(gsr_context* c, void* stream) {
     return GSR_OK;
 }
 
+int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream) {
+    if (!ctxs) return set_error(GSR_ERR_INVALID, "null argument");
+    if (k < 1 || k > GSR_MAX_VIEWS) return set_error(GSR_ERR_INVALID, "render_begin_sorts: k out of range");
+    hipStream_t s = (hipStream_t)stream;
+    RadixViewArgs views[GSR_MAX_VIEWS];
+    size_t n = 0;
+    for (int v = 0; v < k; ++v) {
+        gsr_context* c = ctxs[v];
+        if (!c) return set_error(GSR_ERR_INVALID, "null argument");
+        PendingFrame& f = c->pend;
+        if (!f.sort_ready) return set_error(GSR_ERR_INVALID, "render_begin_sorts: no gsr_render_begin_views frame");
+        if (v == 0) n = f.n;
+        if (f.n != n) return set_error(GSR_ERR_INVALID, "render_begin_sorts: views of different scenes");
+        for (int w = 0; w < v; ++w)
+            if (ctxs[w] == c) return set_error(GSR_ERR_INVALID, "render_begin_sorts: contexts must differ");
+        const ZeroLayout zl(f.u.tiles_x * f.u.tiles_y);
+        f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
+        views[v] = RadixViewArgs{&f.ka, &f.va, &f.kb, &f.vb, c->zero.p + zl.counters, c->zero.p + zl.key_range,
+                                 c->radix_tmp.p, c->zero.p + zl.totals_depth};
+    }
+    int rc;
+    if (n > 0 && (rc = radix_sort_pairs_views(views, k, true, n, 32, kDepthPasses, s))) return rc;
+    for (int v = 0; v < k; ++v) {
+        PendingFrame& f = ctxs[v]->pend;
+        f.sort_ready = false;
+        f.active = true;
+        f.stream = s;
+    }
+    return GSR_OK;
+}
+
 int gsr_render_finish(gsr_context* c, void* stream) {
     if (!c) return set_error(GSR_ERR_INVALID, "null argument");
     PendingFrame& f = c->pend;

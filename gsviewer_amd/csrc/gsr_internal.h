@@ -12,6 +12,7 @@
 namespace gsr {
 
 constexpr int kTile = 16;              // composite tile edge (pixels)
+constexpr int kMaxViews = GSR_MAX_VIEWS;  // views of one scene begun together (gsr_render_begin_views)
 constexpr int kWave = 64;              // CDNA wavefront
 
 // One visible splat after preprocess: 48 bytes = exactly three float4, so the
@@ -179,6 +180,21 @@ int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
 // identity_vals: vals = 0..n-1 (vals_io not read).  n_dev (nullable):
 // device-side element count <= n (grids are sized by n).  tmp holds
 // radix_tmp_elems(n) uint32, totals radix_totals_elems() uint32.
+// The same sort for several views at once (one launch per step for all of
+// them, view = blockIdx.y); every view sorts n_host keys (its device count
+// n_dev bounds the work), same bits/passes; each has its own buffers.
+struct RadixViewArgs {
+    uint32_t** keys_io;
+    uint32_t** vals_io;
+    uint32_t** keys_alt;
+    uint32_t** vals_alt;
+    const uint32_t* n_dev;
+    const uint32_t* key_range;
+    uint32_t* tmp;
+    uint32_t* totals;
+};
+int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
+                           hipStream_t s);
 size_t radix_tmp_elems(size_t n);
 size_t radix_totals_elems();
 int radix_passes_for(int bits);
@@ -211,7 +227,6 @@ int launch_preprocess(const SceneData& sd, const FrameUniforms& u, const uint64_
 int launch_depth_keys_all(const SceneData& sd, const float* V, uint32_t* keys, hipStream_t s);
 
 // Several views of one scene (gsr_render_begin_views): one pass over the scene.
-constexpr int kMaxViews = GSR_MAX_VIEWS;
 struct ViewCullArgs {
     const FrameUniforms* u;
     uint64_t* vis_mask;

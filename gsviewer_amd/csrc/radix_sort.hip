@@ -84,15 +84,15 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t digit, uint32_t w, bool
 }
 
 template <int kR>
-__global__ __launch_bounds__(kThreads) void k_rs_upsweep(const uint32_t* __restrict__ keys,
-                                                         const uint32_t* __restrict__ n_dev, uint32_t n_host,
-                                                         PassArgs pa, uint32_t* __restrict__ hist, uint32_t ntiles) {
+__device__ __forceinline__ void rs_upsweep(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ n_dev,
+                                           uint32_t n_host, const PassArgs& pa, uint32_t* __restrict__ hist,
+                                           uint32_t ntiles, uint32_t tile) {
     constexpr int kTileItems = kThreads * kR;
     __shared__ uint16_t h[kWaves][kMaxRadix];  // per-wave counts (<= 64*kR each)
     const Digit dg = digit_params(pa);
     const uint32_t radix = dg.mask + 1u;
     const uint32_t n = count_of(n_dev, n_host);
-    const uint32_t tile0 = blockIdx.x * kTileItems;
+    const uint32_t tile0 = tile * kTileItems;
     for (uint32_t i = threadIdx.x; i < kWaves * radix; i += kThreads) h[i / radix][i % radix] = 0u;
     const int w = threadIdx.x >> 6;
     const uint32_t base = tile0 + w * (kTileItems / kWaves) + __lane_id();
@@ -117,15 +117,21 @@ __global__ __launch_bounds__(kThreads) void k_rs_upsweep(const uint32_t* __restr
         uint32_t s = 0;
 #pragma unroll
         for (int q = 0; q < kWaves; ++q) s += h[q][d];
-        hist[(size_t)d * ntiles + blockIdx.x] = s;
+        hist[(size_t)d * ntiles + tile] = s;
     }
 }
 
+template <int kR>
+__global__ __launch_bounds__(kThreads) void k_rs_upsweep(const uint32_t* __restrict__ keys,
+                                                         const uint32_t* __restrict__ n_dev, uint32_t n_host,
+                                                         PassArgs pa, uint32_t* __restrict__ hist, uint32_t ntiles) {
+    rs_upsweep<kR>(keys, n_dev, n_host, pa, hist, ntiles, blockIdx.x);
+}
+
 // One wave per digit d: exclusive scan of row d (ntiles counts) in place; row total out.
-__global__ __launch_bounds__(64) void k_rs_offsets(uint32_t* __restrict__ hist, uint32_t ntiles, PassArgs pa,
-                                                   uint32_t* __restrict__ totals) {
+__device__ __forceinline__ void rs_offsets(uint32_t* __restrict__ hist, uint32_t ntiles, const PassArgs& pa,
+                                           uint32_t* __restrict__ totals, uint32_t d) {
     const Digit dg = digit_params(pa);
-    const uint32_t d = blockIdx.x;
     if (d > dg.mask) return;
     uint32_t* row = hist + (size_t)d * ntiles;
     const uint32_t per = (ntiles + 63) / 64;
@@ -143,12 +149,18 @@ __global__ __launch_bounds__(64) void k_rs_offsets(uint32_t* __restrict__ hist, 
     if (__lane_id() == 63) totals[d] = inc;
 }
 
+__global__ __launch_bounds__(64) void k_rs_offsets(uint32_t* __restrict__ hist, uint32_t ntiles, PassArgs pa,
+                                                   uint32_t* __restrict__ totals) {
+    rs_offsets(hist, ntiles, pa, totals, blockIdx.x);
+}
+
 template <int kR>
-__global__ __launch_bounds__(kThreads) void k_rs_scatter(
-    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, bool identity_vals,
-    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ n_dev,
-    uint32_t n_host, PassArgs pa, const uint32_t* __restrict__ hist_off, const uint32_t* __restrict__ totals,
-    uint32_t ntiles) {
+__device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
+                                           bool identity_vals, uint32_t* __restrict__ keys_out,
+                                           uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ n_dev,
+                                           uint32_t n_host, const PassArgs& pa,
+                                           const uint32_t* __restrict__ hist_off,
+                                           const uint32_t* __restrict__ totals, uint32_t ntiles, uint32_t tile) {
     constexpr int kTileItems = kThreads * kR;
     __shared__ uint32_t s_keys[kTileItems];
     __shared__ uint32_t s_vals[kTileItems];
@@ -158,7 +170,7 @@ __global__ __launch_bounds__(kThreads) void k_rs_scatter(
     __shared__ uint32_t wsum[2][kWaves];
 
     const uint32_t n = count_of(n_dev, n_host);
-    const uint32_t tile0 = blockIdx.x * kTileItems;
+    const uint32_t tile0 = tile * kTileItems;
     if (tile0 >= n) return;
     const Digit dg = digit_params(pa);
     const uint32_t radix = dg.mask + 1u;
@@ -171,7 +183,7 @@ __global__ __launch_bounds__(kThreads) void k_rs_scatter(
         const uint32_t d = d0 + j;
         const bool mine = j < (int)q && d < radix;
         gt[j] = mine ? totals[d] : 0u;
-        ho[j] = mine ? hist_off[(size_t)d * ntiles + blockIdx.x] : 0u;
+        ho[j] = mine ? hist_off[(size_t)d * ntiles + tile] : 0u;
     }
     for (uint32_t i = threadIdx.x; i < kWaves * radix; i += kThreads) wcnt[i / radix][i % radix] = 0u;
 
@@ -261,6 +273,51 @@ __global__ __launch_bounds__(kThreads) void k_rs_scatter(
     }
 }
 
+template <int kR>
+__global__ __launch_bounds__(kThreads) void k_rs_scatter(
+    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, bool identity_vals,
+    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ n_dev,
+    uint32_t n_host, PassArgs pa, const uint32_t* __restrict__ hist_off, const uint32_t* __restrict__ totals,
+    uint32_t ntiles) {
+    rs_scatter<kR>(keys_in, vals_in, identity_vals, keys_out, vals_out, n_dev, n_host, pa, hist_off, totals, ntiles,
+                   blockIdx.x);
+}
+
+// Batched: the sorts of several views in one launch per step, view =
+// blockIdx.y (gsr_render_begin_sorts: the depth sorts of a group of views).
+struct SortView {
+    const uint32_t* keys_in;
+    const uint32_t* vals_in;
+    uint32_t* keys_out;
+    uint32_t* vals_out;
+    const uint32_t* n_dev;
+    uint32_t* hist;
+    uint32_t* totals;
+    PassArgs pa;
+};
+struct SortViews {
+    SortView v[kMaxViews];
+};
+
+template <int kR>
+__global__ __launch_bounds__(kThreads) void k_rs_upsweep_views(SortViews sv, uint32_t n_host, uint32_t ntiles) {
+    const SortView& v = sv.v[blockIdx.y];
+    rs_upsweep<kR>(v.keys_in, v.n_dev, n_host, v.pa, v.hist, ntiles, blockIdx.x);
+}
+
+__global__ __launch_bounds__(64) void k_rs_offsets_views(SortViews sv, uint32_t ntiles) {
+    const SortView& v = sv.v[blockIdx.y];
+    rs_offsets(v.hist, ntiles, v.pa, v.totals, blockIdx.x);
+}
+
+template <int kR>
+__global__ __launch_bounds__(kThreads) void k_rs_scatter_views(SortViews sv, bool identity_vals, uint32_t n_host,
+                                                               uint32_t ntiles) {
+    const SortView& v = sv.v[blockIdx.y];
+    rs_scatter<kR>(v.keys_in, v.vals_in, identity_vals, v.keys_out, v.vals_out, v.n_dev, n_host, v.pa, v.hist,
+                   v.totals, ntiles, blockIdx.x);
+}
+
 }  // namespace
 
 size_t radix_tmp_elems(size_t n) {
@@ -295,6 +352,47 @@ static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_a
         t = *vals_io; *vals_io = *vals_alt; *vals_alt = t;
     }
     return GSR_OK;
+}
+
+template <int kR>
+static int sort_passes_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
+                             hipStream_t s) {
+    constexpr int kTileItems = kThreads * kR;
+    const uint32_t nt = (uint32_t)((n + kTileItems - 1) / kTileItems);
+    const uint32_t radix_max = 1u << ((bits + passes - 1) / passes);
+    bool ident = identity_vals;
+    for (int p = 0; p < passes; ++p) {
+        SortViews sv{};
+        for (int v = 0; v < k; ++v) {
+            RadixViewArgs& a = views[v];
+            sv.v[v] = SortView{*a.keys_io, *a.vals_io, *a.keys_alt, *a.vals_alt, a.n_dev, a.tmp, a.totals,
+                               PassArgs{a.key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p}};
+        }
+        k_rs_upsweep_views<kR><<<dim3(nt, k), kThreads, 0, s>>>(sv, (uint32_t)n, nt);
+        GSR_LAUNCH_CHECK("rs_upsweep_views");
+        k_rs_offsets_views<<<dim3(radix_max, k), 64, 0, s>>>(sv, nt);
+        GSR_LAUNCH_CHECK("rs_offsets_views");
+        k_rs_scatter_views<kR><<<dim3(nt, k), kThreads, 0, s>>>(sv, ident, (uint32_t)n, nt);
+        GSR_LAUNCH_CHECK("rs_scatter_views");
+        ident = false;
+        for (int v = 0; v < k; ++v) {
+            RadixViewArgs& a = views[v];
+            uint32_t* t = *a.keys_io; *a.keys_io = *a.keys_alt; *a.keys_alt = t;
+            t = *a.vals_io; *a.vals_io = *a.vals_alt; *a.vals_alt = t;
+        }
+    }
+    return GSR_OK;
+}
+
+int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
+                           hipStream_t s) {
+    if (n == 0 || passes == 0) return GSR_OK;
+    if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "radix sort: view count out of range");
+    if (n > 0xffffffffull - 4 * kMinTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
+    if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
+        return set_error(GSR_ERR_INVALID, "radix sort: digit width out of range");
+    if ((bits + passes - 1) / passes <= 8) return sort_passes_views<16>(views, k, identity_vals, n, bits, passes, s);
+    return sort_passes_views<8>(views, k, identity_vals, n, bits, passes, s);
 }
 
 int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,

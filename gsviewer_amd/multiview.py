@@ -150,15 +150,16 @@ class ViewBatchPipeline:
     the next group's pending frames (gsr_render_finish per view: the host
     waits for the view's counts, then enqueues its binning, tile sort and
     compositing), then begins the group's next frames: the shared cull +
-    preprocess of its k views, then each view's depth sort
-    (gsr_render_begin_sort).  The groups' streams overlap one another, as the
+    preprocess of its k views, then their depth sorts, batched into one launch
+    per radix step (gsr_render_begin_sorts).  The groups' streams overlap one another, as the
     views of ViewPipeline do.  drain() finishes every pending frame.  Images
     are identical to rendering each view alone (tests/test_gpu_multiview.py)."""
 
-    def __init__(self, groups, scene, settings):
+    def __init__(self, groups, scene, settings, batched_sorts=True):
         assert len(groups) >= 1
         self.groups = groups
         self.scene, self.settings = scene, settings
+        self.batched_sorts = batched_sorts  # the group's depth sorts in one launch per radix step
         self.pending = [False] * len(groups)
         self.next = 0
 
@@ -174,15 +175,18 @@ class ViewBatchPipeline:
         self.pending[gi] = False
 
     def step(self):
-        from .rasterizer import render_begin_sort, render_begin_views
+        from .rasterizer import render_begin_sort, render_begin_sorts, render_begin_views
         gi = self.next
         self.next = (gi + 1) % len(self.groups)
         ctxs, cams, outs, stream = self.groups[gi]
         if self.pending[gi]:
             self._finish(gi)
         render_begin_views(ctxs, self.scene, cams, self.settings, outs, stream=stream)
-        for c in ctxs:
-            render_begin_sort(c, stream)
+        if self.batched_sorts:
+            render_begin_sorts(ctxs, stream)
+        else:
+            for c in ctxs:
+                render_begin_sort(c, stream)
         self.pending[gi] = True
 
     def drain(self):

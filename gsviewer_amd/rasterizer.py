@@ -264,6 +264,15 @@ def render_begin_sort(ctx: HipContext, stream=None):
     _lib.check(_lib.load().gsr_render_begin_sort(ctx.handle, _stream_handle(stream)), "gsr_render_begin_sort")
 
 
+def render_begin_sorts(ctxs, stream=None):
+    """gsr_render_begin_sorts: the depth sorts of the views of one
+    render_begin_views call, batched into one launch per radix step on
+    `stream`; finish each view with render_finish(ctx, stream)."""
+    k = len(ctxs)
+    arr = (ctypes.c_void_p * k)(*[c.handle for c in ctxs])
+    _lib.check(_lib.load().gsr_render_begin_sorts(arr, k, _stream_handle(stream)), "gsr_render_begin_sorts")
+
+
 _default_ctx = {}
 
 

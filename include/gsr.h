@@ -160,6 +160,10 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
                            const gsr_camera* cams, const gsr_settings* settings,
                            float* const* out_images_dev, int32_t* const* radii_dev, void* stream);
 int gsr_render_begin_sort(gsr_context* ctx, void* stream);
+/* The depth sorts of k views begun by one gsr_render_begin_views, in one
+ * launch per radix step on `stream` (which then also takes their
+ * gsr_render_finish). */
+int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream);
 
 int gsr_context_stats(const gsr_context* ctx, gsr_frame_stats* out);
 

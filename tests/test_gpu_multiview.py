@@ -95,7 +95,8 @@ def test_contexts_share_one_scene_concurrently(gpu):
     scene.close()
 
 
-def test_shared_scene_pass_matches_serial_renders(gpu):
+@pytest.mark.parametrize("batched_sorts", [True, False])
+def test_shared_scene_pass_matches_serial_renders(gpu, batched_sorts):
     """gsr_render_begin_views (one cull + preprocess pass over the scene for a
     group of views) through ViewBatchPipeline with two groups: images, radii
     and counts identical to each view rendered alone."""
@@ -115,7 +116,7 @@ def test_shared_scene_pass_matches_serial_renders(gpu):
         want_stats.append(ref_ctx.stats())
     groups = [(ctxs[g * K:(g + 1) * K], cams[g * K:(g + 1) * K], outs[g * K:(g + 1) * K], streams[g])
               for g in range(G)]
-    pipe = ViewBatchPipeline(groups, scene, st)
+    pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=batched_sorts)
     for _ in range(3 * G + 1):  # every group several times, one group a step ahead
         pipe.step()
     pipe.drain()
@@ -142,6 +143,9 @@ def test_shared_scene_pass_radii_and_errors(gpu):
         render_begin_sort(ctxs[0], streams[0])
     with pytest.raises(RuntimeError, match="contexts must differ"):
         render_begin_views([ctxs[0], ctxs[0]], scene, cams[:2], st, outs[:2])
+    from gsviewer_amd.rasterizer import render_begin_sorts
+    with pytest.raises(RuntimeError, match="no gsr_render_begin_views frame"):
+        render_begin_sorts(ctxs, streams[0])
     s = torch.cuda.Stream()
     render_begin_views(ctxs, scene, cams[:2], st, outs, radii=radii, stream=s)
     with pytest.raises(RuntimeError, match="not finished"):
