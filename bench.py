@@ -159,6 +159,9 @@ def main():
                          "and >= 8, else 1")
     ap.add_argument("--no-batched-sorts", action="store_true",
                     help="with --share > 1: one depth sort per view instead of one batched sort per group")
+    ap.add_argument("--no-batched-finish", action="store_true",
+                    help="with --share > 1: finish each view's frame alone instead of one launch per stage "
+                         "for the group")
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage HIP events")
     ap.add_argument("--render-mod", type=int, default=6,
                     help="render_mod uniform (experiments; 6 = SH:0~3, the reference default)")
@@ -234,7 +237,8 @@ def main():
     else:
         groups = [(ctxs[g:g + share], camcs[g:g + share], outs[g:g + share], streams[g])
                   for g in range(0, K, share)]
-        pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=not args.no_batched_sorts)
+        pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=not args.no_batched_sorts,
+                                 batched_finish=not args.no_batched_finish)
 
     def serial_frame():
         render_into(ctx, scene, camc, st, outs[0])

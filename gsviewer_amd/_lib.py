@@ -104,6 +104,7 @@ SIGNATURES = {
                                               _P]),
     "gsr_render_begin_sort": (ctypes.c_int, [_P, _P]),
     "gsr_render_begin_sorts": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int32, _P]),
+    "gsr_render_finish_views": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int32, _P]),
     "gsr_context_stats": (ctypes.c_int, [_P, ctypes.POINTER(GsrFrameStats)]),
     "gsr_sort_depth": (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_float * 16), _P, _P]),
     "gsr_debug_host_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
@@ -125,7 +126,7 @@ STAGES = ["cull", "preprocess", "depth_sort", "binning", "tile_sort", "tile_rang
 
 GSR_DEBUG_RECORDS, GSR_DEBUG_DEPTH_ORDER, GSR_DEBUG_TILE_RANGES, GSR_DEBUG_TILE_LIST = 0, 1, 2, 3
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_VIEWS = 8  # GSR_MAX_VIEWS (include/gsr.h)
 
 _lib = None

@@ -705,6 +705,115 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     return GSR_OK;
 }
 
+// The second halves of a group of frames in one set of launches (view =
+// blockIdx.y in every kernel): binning, tile sort, ranges, chunks, composite
+// and merge are each one launch for the group instead of one per view.
+int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
+    if (!ctxs) return set_error(GSR_ERR_INVALID, "null argument");
+    if (k < 1 || k > GSR_MAX_VIEWS) return set_error(GSR_ERR_INVALID, "render_finish_views: k out of range");
+    hipStream_t s = (hipStream_t)stream;
+    gsr_context* c0 = ctxs[0];
+    if (!c0) return set_error(GSR_ERR_INVALID, "null argument");
+    for (int v = 0; v < k; ++v) {
+        gsr_context* c = ctxs[v];
+        if (!c) return set_error(GSR_ERR_INVALID, "null argument");
+        const PendingFrame& f = c->pend;
+        const PendingFrame& f0 = c0->pend;
+        if (!f.active) return set_error(GSR_ERR_INVALID, "render_finish_views: no frame was begun");
+        if (f.stream != s) return set_error(GSR_ERR_INVALID, "render_finish_views: not the frames' stream");
+        if (c->prof_on) return set_error(GSR_ERR_INVALID, "render_finish_views: profiling is per view");
+        for (int w = 0; w < v; ++w)
+            if (ctxs[w] == c) return set_error(GSR_ERR_INVALID, "render_finish_views: contexts must differ");
+        if (f.u.width != f0.u.width || f.u.height != f0.u.height || f.t_min != f0.t_min || f.bg[0] != f0.bg[0] ||
+            f.bg[1] != f0.bg[1] || f.bg[2] != f0.bg[2] || f.out_layout != f0.out_layout ||
+            frag_class_of(f.u.render_mod) != frag_class_of(f0.u.render_mod) || c->chunk != c0->chunk)
+            return set_error(GSR_ERR_INVALID, "render_finish_views: views differ in frame size or settings");
+    }
+    const FrameUniforms& u0 = c0->pend.u;
+    const int num_tiles = u0.tiles_x * u0.tiles_y;
+    const ZeroLayout zl(num_tiles);
+    FinishView fv[GSR_MAX_VIEWS];
+    RadixViewArgs rv[GSR_MAX_VIEWS];
+    uint32_t *tka[GSR_MAX_VIEWS], *tkb[GSR_MAX_VIEWS], *tva[GSR_MAX_VIEWS], *tvb[GSR_MAX_VIEWS];
+    uint32_t n_vis_max = 0, n_dup_max = 0;
+    size_t max_chunks = 0;
+    int rc;
+    const auto h1 = std::chrono::steady_clock::now();
+    // the frames' counts (published together by the shared preprocess, or one by one)
+    for (int v = 0; v < k; ++v)
+        if (ctxs[v]->pend.n > 0 && (rc = wait_counts(ctxs[v], s))) return rc;
+    const auto h2 = std::chrono::steady_clock::now();
+    for (int v = 0; v < k; ++v) {
+        gsr_context* c = ctxs[v];
+        PendingFrame& f = c->pend;
+        f.active = false;
+        const uint32_t n_vis = f.n > 0 ? __atomic_load_n(&c->host_counters[0], __ATOMIC_ACQUIRE) : 0u;
+        const uint32_t n_dup = f.n > 0 ? __atomic_load_n(&c->host_counters[1], __ATOMIC_ACQUIRE) : 0u;
+        n_vis_max = std::max(n_vis_max, n_vis);
+        n_dup_max = std::max(n_dup_max, n_dup);
+        if (n_vis > 0) c->last_depth_order = f.va;
+        if (n_dup > 0) {
+            if ((rc = c->tkeys_a.ensure(n_dup, "tile_keys"))) return rc;
+            if ((rc = c->tkeys_b.ensure(n_dup, "tile_keys"))) return rc;
+            if ((rc = c->tvals_a.ensure(n_dup, "tile_vals"))) return rc;
+            if ((rc = c->tvals_b.ensure(n_dup, "tile_vals"))) return rc;
+        }
+        const size_t mc = (size_t)num_tiles + n_dup / c->chunk + 1;
+        max_chunks = std::max(max_chunks, mc);
+        if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
+        if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
+        if ((rc = c->chunk_desc.ensure(mc, "chunk_desc"))) return rc;
+        if ((rc = c->chunk_order.ensure(mc, "chunk_order"))) return rc;
+        if ((rc = c->partial.ensure(mc * 256, "partial"))) return rc;
+        if ((rc = c->tmax.ensure(mc, "tmax"))) return rc;
+        uint32_t* counters = c->zero.p + zl.counters;
+        tka[v] = c->tkeys_a.p, tkb[v] = c->tkeys_b.p, tva[v] = c->tvals_a.p, tvb[v] = c->tvals_b.p;
+        fv[v] = FinishView{f.va, c->trect.p, n_vis, n_dup, c->bin_tmp.p, c->trect_sorted.p, tka[v], tva[v],
+                           reinterpret_cast<uint2*>(c->zero.p + zl.ranges), c->chunk_cnt.p, c->chunk_base.p,
+                           counters + 2, c->chunk_desc.p, c->chunk_order.p, c->tmax.p, c->zero.p + zl.sat,
+                           c->recs.p, f.out, c->partial.p};
+        rv[v] = RadixViewArgs{&tka[v], &tva[v], &tkb[v], &tvb[v], counters + 1, nullptr, c->radix_tmp.p,
+                              c->zero.p + zl.totals_tile};
+    }
+    // every view's sort temporaries cover the largest view (the grids do)
+    for (int v = 0; v < k && n_dup_max > 0; ++v) {
+        gsr_context* c = ctxs[v];
+        if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(n_dup_max), radix_tmp_elems(c->pend.n)),
+                                      "radix_tmp")))
+            return rc;
+        rv[v].tmp = c->radix_tmp.p;
+    }
+    if (n_vis_max > 0 && (rc = launch_binning_views(fv, k, u0.tiles_x, s))) return rc;
+    const int tbits = bits_for((uint32_t)num_tiles);
+    if (n_dup_max > 0 && tbits > 0 &&
+        (rc = radix_sort_pairs_views(rv, k, false, n_dup_max, tbits, radix_passes_for(tbits), s)))
+        return rc;
+    for (int v = 0; v < k; ++v) {
+        fv[v].tile_keys = tka[v];
+        fv[v].tile_vals = tva[v];
+        if (fv[v].n_dup > 0) ctxs[v]->last_tile_list = tva[v];
+    }
+    if ((rc = launch_tile_ranges_views(fv, k, s))) return rc;
+    if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk, s))) return rc;
+    const PendingFrame& f0 = c0->pend;
+    if ((rc = launch_composite_views(fv, k, (uint32_t)max_chunks, u0, frag_class_of(u0.render_mod), f0.t_min, f0.bg,
+                                     f0.out_layout, s)))
+        return rc;
+    if ((rc = launch_merge_views(fv, k, u0, f0.t_min, f0.bg, f0.out_layout, s))) return rc;
+    const auto h3 = std::chrono::steady_clock::now();
+    using ms = std::chrono::duration<double, std::milli>;
+    for (int v = 0; v < k; ++v) {
+        gsr_context* c = ctxs[v];
+        c->host_ms[1] += ms(h2 - h1).count() / k;
+        c->host_ms[2] += ms(h3 - h2).count() / k;
+        c->host_frames += 1;
+        c->frame_idx += 1;
+        c->stats.n_visible = fv[v].n_vis;
+        c->stats.n_instances = fv[v].n_dup;
+    }
+    return GSR_OK;
+}
+
 int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, float* out,
                int32_t* radii, void* stream) {
     int rc = gsr_render_begin(c, sc, cam, st, out, radii, stream);

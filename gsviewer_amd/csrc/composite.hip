@@ -14,6 +14,8 @@
 // workgroup barriers; a wave retires as soon as all its 256 pixels are
 // saturated (transmittance < t_min).  Slices a splat's row span misses are
 // skipped with a scalar branch.
+#include <algorithm>
+
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -34,12 +36,10 @@ __device__ __forceinline__ uint32_t rect_tiles(uint2 tr) {
 
 // Also writes the gathered rects in depth order (trect_sorted), so that
 // k_bin_write reads them coalesced instead of gathering them a second time.
-__global__ __launch_bounds__(kThreads) void k_bin_reduce(const uint32_t* __restrict__ sorted_ids,
-                                                         const uint2* __restrict__ trect, uint32_t n_vis,
-                                                         uint32_t* __restrict__ block_sums,
-                                                         uint2* __restrict__ trect_sorted) {
-    __shared__ uint32_t lds[kThreads / 64];
-    const uint32_t base = blockIdx.x * kBinBlock + threadIdx.x;
+__device__ __forceinline__ void bin_reduce(const uint32_t* __restrict__ sorted_ids, const uint2* __restrict__ trect,
+                                           uint32_t n_vis, uint32_t* __restrict__ block_sums,
+                                           uint2* __restrict__ trect_sorted, uint32_t blk, uint32_t* lds) {
+    const uint32_t base = blk * kBinBlock + threadIdx.x;
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
@@ -55,18 +55,25 @@ __global__ __launch_bounds__(kThreads) void k_bin_reduce(const uint32_t* __restr
     s = wave_reduce_sum(s);
     if (__lane_id() == 0) lds[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) block_sums[blockIdx.x] = lds[0] + lds[1] + lds[2] + lds[3];
+    if (threadIdx.x == 0) block_sums[blk] = lds[0] + lds[1] + lds[2] + lds[3];
+}
+
+__global__ __launch_bounds__(kThreads) void k_bin_reduce(const uint32_t* __restrict__ sorted_ids,
+                                                         const uint2* __restrict__ trect, uint32_t n_vis,
+                                                         uint32_t* __restrict__ block_sums,
+                                                         uint2* __restrict__ trect_sorted) {
+    __shared__ uint32_t lds[kThreads / 64];
+    bin_reduce(sorted_ids, trect, n_vis, block_sums, trect_sorted, blockIdx.x, lds);
 }
 
 // Exclusive offsets of the block's splats (block prefix + in-block scan), then
 // one (tile key, record slot) instance per covered tile, row-major.
-__global__ __launch_bounds__(kThreads) void k_bin_write(const uint32_t* __restrict__ sorted_ids,
-                                                        const uint2* __restrict__ trect_sorted, uint32_t n_vis,
-                                                        const uint32_t* __restrict__ block_off, int tiles_x,
-                                                        uint32_t* __restrict__ tile_keys,
-                                                        uint32_t* __restrict__ tile_vals) {
-    __shared__ uint32_t lds[kThreads / 64];
-    const uint32_t base = blockIdx.x * kBinBlock + threadIdx.x * kBinItems;  // 4 consecutive per thread
+__device__ __forceinline__ void bin_write(const uint32_t* __restrict__ sorted_ids,
+                                          const uint2* __restrict__ trect_sorted, uint32_t n_vis,
+                                          const uint32_t* __restrict__ block_off, int tiles_x,
+                                          uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ tile_vals,
+                                          uint32_t blk, uint32_t* lds) {
+    const uint32_t base = blk * kBinBlock + threadIdx.x * kBinItems;  // 4 consecutive per thread
     uint32_t id[kBinItems];
     uint2 tr[kBinItems];
 #pragma unroll
@@ -84,7 +91,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_write(const uint32_t* __restri
     const uint32_t inc = wave_inclusive_scan(s);
     if (__lane_id() == 63) lds[w] = inc;
     __syncthreads();
-    uint32_t o = block_off[blockIdx.x] + inc - s;
+    uint32_t o = block_off[blk] + inc - s;
 #pragma unroll
     for (int k = 0; k < kThreads / 64; ++k) o += (k < w) ? lds[k] : 0u;
 #pragma unroll
@@ -100,13 +107,65 @@ __global__ __launch_bounds__(kThreads) void k_bin_write(const uint32_t* __restri
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_tile_ranges(const uint32_t* __restrict__ keys, uint32_t n,
-                                                          uint2* __restrict__ ranges) {
-    const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+__global__ __launch_bounds__(kThreads) void k_bin_write(const uint32_t* __restrict__ sorted_ids,
+                                                        const uint2* __restrict__ trect_sorted, uint32_t n_vis,
+                                                        const uint32_t* __restrict__ block_off, int tiles_x,
+                                                        uint32_t* __restrict__ tile_keys,
+                                                        uint32_t* __restrict__ tile_vals) {
+    __shared__ uint32_t lds[kThreads / 64];
+    bin_write(sorted_ids, trect_sorted, n_vis, block_off, tiles_x, tile_keys, tile_vals, blockIdx.x, lds);
+}
+
+// Views of a group (blockIdx.y = view); the grid covers the largest view.
+struct BinView {
+    const uint32_t* sorted_ids;
+    const uint2* trect;
+    uint2* trect_sorted;
+    uint32_t* block_sums;
+    uint32_t* tile_keys;
+    uint32_t* tile_vals;
+    uint32_t n_vis;
+};
+struct BinViews {
+    BinView v[kMaxViews];
+};
+
+__global__ __launch_bounds__(kThreads) void k_bin_reduce_views(BinViews vs) {
+    __shared__ uint32_t lds[kThreads / 64];
+    const BinView& v = vs.v[blockIdx.y];
+    if (blockIdx.x * kBinBlock >= v.n_vis) return;
+    bin_reduce(v.sorted_ids, v.trect, v.n_vis, v.block_sums, v.trect_sorted, blockIdx.x, lds);
+}
+
+__global__ __launch_bounds__(kThreads) void k_bin_write_views(BinViews vs, int tiles_x) {
+    __shared__ uint32_t lds[kThreads / 64];
+    const BinView& v = vs.v[blockIdx.y];
+    if (blockIdx.x * kBinBlock >= v.n_vis) return;
+    bin_write(v.sorted_ids, v.trect_sorted, v.n_vis, v.block_sums, tiles_x, v.tile_keys, v.tile_vals, blockIdx.x, lds);
+}
+
+__device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, uint32_t n, uint2* __restrict__ ranges,
+                                            uint32_t i) {
     if (i >= n) return;
     const uint32_t k = keys[i];
     if (i == 0 || keys[i - 1] != k) ranges[k].x = i;
     if (i == n - 1 || keys[i + 1] != k) ranges[k].y = i + 1;
+}
+
+__global__ __launch_bounds__(kThreads) void k_tile_ranges(const uint32_t* __restrict__ keys, uint32_t n,
+                                                          uint2* __restrict__ ranges) {
+    tile_ranges(keys, n, ranges, blockIdx.x * kThreads + threadIdx.x);
+}
+
+struct RangeViews {
+    const uint32_t* keys[kMaxViews];
+    uint2* ranges[kMaxViews];
+    uint32_t n[kMaxViews];
+};
+
+__global__ __launch_bounds__(kThreads) void k_tile_ranges_views(RangeViews vs) {
+    const int v = blockIdx.y;
+    tile_ranges(vs.keys[v], vs.n[v], vs.ranges[v], blockIdx.x * kThreads + threadIdx.x);
 }
 
 struct CompositeArgs {
@@ -171,10 +230,9 @@ __device__ __forceinline__ uint32_t full_chunks_of(uint2 r, uint32_t chunk) { re
 // sums of the earlier block totals (a few dozen at 1080p), scans its tiles'
 // counts, and writes the descriptors (tile, begin, end, count << 16 | index)
 // and each chunk's dispatch position.
-__global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restrict__ ranges, int num_tiles,
-                                                          uint32_t chunk, uint32_t* __restrict__ block_extra,
-                                                          uint32_t* __restrict__ block_full) {
-    __shared__ uint32_t lds[2][kThreads / 64];
+__device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
+                                            uint32_t* __restrict__ block_extra, uint32_t* __restrict__ block_full,
+                                            uint32_t (*lds)[kThreads / 64]) {
     const int t = blockIdx.x * kThreads + threadIdx.x;
     const uint2 r = t < num_tiles ? ranges[t] : make_uint2(0u, 0u);
     uint32_t e = t < num_tiles ? chunks_of(r, chunk) - 1u : 0u;
@@ -192,16 +250,21 @@ __global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restric
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restrict__ ranges, int num_tiles,
-                                                          uint32_t chunk, const uint32_t* __restrict__ block_extra,
-                                                          const uint32_t* __restrict__ block_full,
-                                                          uint32_t* __restrict__ chunk_cnt,
-                                                          uint32_t* __restrict__ chunk_base,
-                                                          uint32_t* __restrict__ n_extra_dev,
-                                                          uint4* __restrict__ desc, uint32_t* __restrict__ order,
-                                                          float4* __restrict__ tmax) {
+__global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restrict__ ranges, int num_tiles,
+                                                          uint32_t chunk, uint32_t* __restrict__ block_extra,
+                                                          uint32_t* __restrict__ block_full) {
     __shared__ uint32_t lds[2][kThreads / 64];
-    __shared__ uint32_t s_prefix, s_full_prefix, s_full_total;
+    chunk_count(ranges, num_tiles, chunk, block_extra, block_full, lds);
+}
+
+__device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
+                                            const uint32_t* __restrict__ block_extra,
+                                            const uint32_t* __restrict__ block_full, uint32_t* __restrict__ chunk_cnt,
+                                            uint32_t* __restrict__ chunk_base, uint32_t* __restrict__ n_extra_dev,
+                                            uint4* __restrict__ desc, uint32_t* __restrict__ order,
+                                            float4* __restrict__ tmax, uint32_t (*lds)[kThreads / 64],
+                                            uint32_t* s_sh) {
+    uint32_t &s_prefix = s_sh[0], &s_full_prefix = s_sh[1], &s_full_total = s_sh[2];
     const int t = blockIdx.x * kThreads + threadIdx.x;
     if (threadIdx.x < 64) {  // wave 0: offsets of this block = sums of the earlier blocks' totals
         uint32_t p = 0, pf = 0, tf = 0;
@@ -264,6 +327,49 @@ __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restric
         const uint32_t fb = __shfl(full_before, src, 64), pp = __shfl(part_pos, src, 64);
         for (uint32_t j = 1 + __lane_id(); j < c; j += 64) emit(tt, rx, ry, c, f, bs, fb, pp, j);
     }
+}
+
+__global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restrict__ ranges, int num_tiles,
+                                                          uint32_t chunk, const uint32_t* __restrict__ block_extra,
+                                                          const uint32_t* __restrict__ block_full,
+                                                          uint32_t* __restrict__ chunk_cnt,
+                                                          uint32_t* __restrict__ chunk_base,
+                                                          uint32_t* __restrict__ n_extra_dev,
+                                                          uint4* __restrict__ desc, uint32_t* __restrict__ order,
+                                                          float4* __restrict__ tmax) {
+    __shared__ uint32_t lds[2][kThreads / 64];
+    __shared__ uint32_t s_sh[3];
+    chunk_write(ranges, num_tiles, chunk, block_extra, block_full, chunk_cnt, chunk_base, n_extra_dev, desc, order,
+                tmax, lds, s_sh);
+}
+
+struct ChunkView {
+    const uint2* ranges;
+    uint32_t* chunk_cnt;  // block totals after its num_tiles entries
+    uint32_t* chunk_base;
+    uint32_t* n_extra_dev;
+    uint4* desc;
+    uint32_t* order;
+    float4* tmax;
+};
+struct ChunkViews {
+    ChunkView v[kMaxViews];
+};
+
+__global__ __launch_bounds__(kThreads) void k_chunk_count_views(ChunkViews vs, int num_tiles, uint32_t chunk) {
+    __shared__ uint32_t lds[2][kThreads / 64];
+    const ChunkView& v = vs.v[blockIdx.y];
+    uint32_t* block_extra = v.chunk_cnt + num_tiles;
+    chunk_count(v.ranges, num_tiles, chunk, block_extra, block_extra + gridDim.x, lds);
+}
+
+__global__ __launch_bounds__(kThreads) void k_chunk_write_views(ChunkViews vs, int num_tiles, uint32_t chunk) {
+    __shared__ uint32_t lds[2][kThreads / 64];
+    __shared__ uint32_t s_sh[3];
+    const ChunkView& v = vs.v[blockIdx.y];
+    const uint32_t* block_extra = v.chunk_cnt + num_tiles;
+    chunk_write(v.ranges, num_tiles, chunk, block_extra, block_extra + gridDim.x, v.chunk_cnt, v.chunk_base,
+                v.n_extra_dev, v.desc, v.order, v.tmax, lds, s_sh);
 }
 
 // Bits [lo, hi] of a 16-bit mask, clamped to [0, 15]; 0 if the range is empty.
@@ -679,6 +785,35 @@ __global__ __launch_bounds__(kThreads) GSR_COMP_OCC void k_composite(const uint4
 #endif
 }
 
+// The composite of a group of views: blockIdx.y = view, each view's chunks in
+// its own dispatch order; a view's waves past its chunk count exit.
+struct CompView {
+    const uint4* desc;
+    const uint32_t* order;
+    const uint32_t* n_chunks_dev;
+    const uint32_t* list;
+    const SplatRec* recs;
+    float* out;
+    float4* partial;
+    uint32_t* sat;
+    float4* tmax;
+};
+struct CompViews {
+    CompView v[kMaxViews];
+};
+
+template <int FRAG>
+__global__ __launch_bounds__(kThreads) GSR_COMP_OCC void k_composite_views(CompViews vs, CompositeArgs a) {
+    __shared__ float4 lds[kThreads / 64][kBatch * 3];
+    const CompView& v = vs.v[blockIdx.y];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t pos = blockIdx.x * (kThreads / 64) + wave;
+    if (pos >= (uint32_t)a.num_tiles + v.n_chunks_dev[0]) return;
+    const uint32_t slot = v.order[pos];
+    const uint4 d = v.desc[slot];
+    composite_chunk<FRAG>(d, slot, lds[wave], v.list, v.recs, a, v.out, v.partial, v.sat, v.tmax);
+}
+
 // Fold the partial results of multi-chunk tiles in depth order: one block of
 // 16 waves per tile; wave w folds slice (w & 3) over the w >> 2 quarter of the
 // tile's chunks (up to the saturating chunk, if any) with 16 partial loads in
@@ -689,12 +824,11 @@ constexpr int kMergeThreads = 1024;
 constexpr int kMergeParts = kMergeThreads / 64 / 4;  // 4
 constexpr int kMergeDepth = 16;
 
-__global__ __launch_bounds__(kMergeThreads) void k_merge(const uint32_t* __restrict__ chunk_cnt,
-                                                         const uint32_t* __restrict__ chunk_base,
-                                                         const float4* __restrict__ partial,
-                                                         const uint32_t* __restrict__ sat, CompositeArgs a,
-                                                         float* __restrict__ out) {
-    __shared__ float4 part[kMergeParts][4][64];
+__device__ __forceinline__ void merge_tile(const uint32_t* __restrict__ chunk_cnt,
+                                           const uint32_t* __restrict__ chunk_base,
+                                           const float4* __restrict__ partial, const uint32_t* __restrict__ sat,
+                                           const CompositeArgs& a, float* __restrict__ out,
+                                           float4 (*part)[4][64]) {
     const int tile = blockIdx.x;
     const uint32_t cnt = chunk_cnt[tile];
     if (cnt <= 1) return;
@@ -757,6 +891,32 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(const uint32_t* __restr
         out[3 * pidx + 1] = g;
         out[3 * pidx + 2] = b;
     }
+}
+
+__global__ __launch_bounds__(kMergeThreads) void k_merge(const uint32_t* __restrict__ chunk_cnt,
+                                                         const uint32_t* __restrict__ chunk_base,
+                                                         const float4* __restrict__ partial,
+                                                         const uint32_t* __restrict__ sat, CompositeArgs a,
+                                                         float* __restrict__ out) {
+    __shared__ float4 part[kMergeParts][4][64];
+    merge_tile(chunk_cnt, chunk_base, partial, sat, a, out, part);
+}
+
+struct MergeView {
+    const uint32_t* chunk_cnt;
+    const uint32_t* chunk_base;
+    const float4* partial;
+    const uint32_t* sat;
+    float* out;
+};
+struct MergeViews {
+    MergeView v[kMaxViews];
+};
+
+__global__ __launch_bounds__(kMergeThreads) void k_merge_views(MergeViews vs, CompositeArgs a) {
+    __shared__ float4 part[kMergeParts][4][64];
+    const MergeView& v = vs.v[blockIdx.y];
+    merge_tile(v.chunk_cnt, v.chunk_base, v.partial, v.sat, a, v.out, part);
 }
 
 }  // namespace
@@ -869,6 +1029,95 @@ int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const fl
     const CompositeArgs a = make_args(u, t_min, bg, out_layout);
     k_merge<<<(unsigned)a.num_tiles, kMergeThreads, 0, s>>>(chunk_cnt, chunk_base, partial, sat, a, out);
     GSR_LAUNCH_CHECK("merge");
+    return GSR_OK;
+}
+
+// ------------------------------------------------------------ groups of views
+int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s) {
+    BinViews bv{};
+    uint32_t* arrays[kMaxViews];
+    uint32_t nb[kMaxViews];
+    uint32_t nb_max = 0;
+    for (int i = 0; i < k; ++i) {
+        const FinishView& f = views[i];
+        bv.v[i] = BinView{f.sorted_ids, f.trect, f.trect_sorted, f.bin_tmp, f.tile_keys, f.tile_vals, f.n_vis};
+        arrays[i] = f.bin_tmp;
+        nb[i] = (f.n_vis + kBinBlock - 1) / kBinBlock;
+        nb_max = std::max(nb_max, nb[i]);
+    }
+    if (nb_max == 0) return GSR_OK;
+    k_bin_reduce_views<<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv);
+    GSR_LAUNCH_CHECK("bin_reduce_views");
+    int rc = scan_single_views(arrays, nb, k, s);
+    if (rc) return rc;
+    k_bin_write_views<<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x);
+    GSR_LAUNCH_CHECK("bin_write_views");
+    return GSR_OK;
+}
+
+int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s) {
+    RangeViews rv{};
+    uint32_t n_max = 0;
+    for (int i = 0; i < k; ++i) {
+        rv.keys[i] = views[i].tile_keys;
+        rv.ranges[i] = views[i].ranges;
+        rv.n[i] = views[i].n_dup;
+        n_max = std::max(n_max, views[i].n_dup);
+    }
+    if (n_max == 0) return GSR_OK;
+    k_tile_ranges_views<<<dim3((n_max + kThreads - 1) / kThreads, (unsigned)k), kThreads, 0, s>>>(rv);
+    GSR_LAUNCH_CHECK("tile_ranges_views");
+    return GSR_OK;
+}
+
+int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, hipStream_t s) {
+    ChunkViews cv{};
+    for (int i = 0; i < k; ++i) {
+        const FinishView& f = views[i];
+#ifdef GSR_COMP_BOUND
+        float4* tmax = f.tmax;
+#else
+        float4* tmax = nullptr;  // the published maxima are only read by the bound variant
+#endif
+        cv.v[i] = ChunkView{f.ranges, f.chunk_cnt, f.chunk_base, f.n_extra_dev, f.desc, f.order, tmax};
+    }
+    const dim3 grid((unsigned)((num_tiles + kThreads - 1) / kThreads), (unsigned)k);
+    k_chunk_count_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk);
+    GSR_LAUNCH_CHECK("chunk_count_views");
+    k_chunk_write_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk);
+    GSR_LAUNCH_CHECK("chunk_write_views");
+    return GSR_OK;
+}
+
+int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, const FrameUniforms& u, int frag_class,
+                           float t_min, const float* bg, int out_layout, hipStream_t s) {
+    const CompositeArgs a = make_args(u, t_min, bg, out_layout);
+    CompViews cv{};
+    for (int i = 0; i < k; ++i) {
+        const FinishView& f = views[i];
+        cv.v[i] = CompView{f.desc, f.order, f.n_extra_dev, f.tile_vals, f.recs, f.out, f.partial, f.sat, f.tmax};
+    }
+    const dim3 grid((unsigned)((max_chunks + 3) / 4), (unsigned)k);
+    switch (frag_class) {
+        case kFragGauss: k_composite_views<kFragGauss><<<grid, kThreads, 0, s>>>(cv, a); break;
+        case kFragBillboard: k_composite_views<kFragBillboard><<<grid, kThreads, 0, s>>>(cv, a); break;
+        case kFragFlatBall: k_composite_views<kFragFlatBall><<<grid, kThreads, 0, s>>>(cv, a); break;
+        default: k_composite_views<kFragGaussBall><<<grid, kThreads, 0, s>>>(cv, a); break;
+    }
+    GSR_LAUNCH_CHECK("composite_views");
+    return GSR_OK;
+}
+
+int launch_merge_views(FinishView* views, int k, const FrameUniforms& u, float t_min, const float* bg,
+                       int out_layout, hipStream_t s) {
+    const CompositeArgs a = make_args(u, t_min, bg, out_layout);
+    MergeViews mv{};
+    for (int i = 0; i < k; ++i) {
+        const FinishView& f = views[i];
+        mv.v[i] = MergeView{f.chunk_cnt, f.chunk_base, f.partial, f.sat, f.out};
+    }
+    k_merge_views<<<dim3((unsigned)a.num_tiles, (unsigned)k), kMergeThreads, 0, s>>>(mv, a);
+    GSR_LAUNCH_CHECK("merge_views");
     return GSR_OK;
 }
 

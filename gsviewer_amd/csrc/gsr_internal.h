@@ -275,6 +275,43 @@ int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n
 int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const float4* partial, const uint32_t* sat,
                  const FrameUniforms& u, float t_min, const float* bg, int out_layout, float* out, hipStream_t s);
 
+// The second half of a group of views' frames (gsr_render_finish_views): each
+// stage is one launch for the whole group (view = blockIdx.y); grids cover the
+// largest view and the blocks past a view's own size exit.  All views share
+// the frame size, t_min, background, output layout and chunk length.
+struct FinishView {
+    // binning (n_vis, n_dup: this view's exact counts)
+    const uint32_t* sorted_ids;
+    const uint2* trect;
+    uint32_t n_vis, n_dup;
+    uint32_t* bin_tmp;
+    uint2* trect_sorted;
+    uint32_t* tile_keys;  // tile-sorted (keys, vals) after the tile sort
+    uint32_t* tile_vals;
+    // chunks, composite, merge
+    uint2* ranges;
+    uint32_t* chunk_cnt;
+    uint32_t* chunk_base;
+    uint32_t* n_extra_dev;
+    uint4* desc;
+    uint32_t* order;
+    float4* tmax;
+    uint32_t* sat;
+    const SplatRec* recs;
+    float* out;
+    float4* partial;
+};
+// binning: scan_tmp of each view is its bin_tmp (block sums scanned in place)
+int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s);
+int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s);
+int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, hipStream_t s);
+int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, const FrameUniforms& u, int frag_class,
+                           float t_min, const float* bg, int out_layout, hipStream_t s);
+int launch_merge_views(FinishView* views, int k, const FrameUniforms& u, float t_min, const float* bg,
+                       int out_layout, hipStream_t s);
+// scan.hip: in-place exclusive scans of k small arrays (each n <= 131072), one launch
+int scan_single_views(uint32_t* const* arrays, const uint32_t* n, int k, hipStream_t s);
+
 }  // namespace gsr
 
 struct gsr_scene {

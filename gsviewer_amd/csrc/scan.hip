@@ -132,14 +132,8 @@ __global__ __launch_bounds__(kThreads) void k_scan_final(const uint32_t* __restr
 // for the small arrays of a frame (wave counts, tiles, block sums).  The array
 // is walked in 4096-element chunks: coalesced dwordx4 loads (next chunk
 // prefetched), a block scan per chunk, a running carry.
-__global__ __launch_bounds__(kPartialThreads) void k_scan_single(const uint32_t* __restrict__ in,
-                                                                 uint32_t* __restrict__ out, size_t n,
-                                                                 uint32_t* __restrict__ total_dev,
-                                                                 const uint2* __restrict__ kr_in, size_t n_kr,
-                                                                 uint32_t* __restrict__ kr_out) {
-    __shared__ uint32_t lds[2][kPartialThreads / 64];
-    __shared__ uint2 lds_kr[kPartialThreads / 64];
-    if (kr_in) reduce_ranges(kr_in, n_kr, kr_out, lds_kr);
+__device__ __forceinline__ void scan_single(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t n,
+                                            uint32_t* __restrict__ total_dev, uint32_t (*lds)[kPartialThreads / 64]) {
     constexpr size_t kChunk = 4 * kPartialThreads;
     const bool aligned = (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
     auto load4 = [&](size_t c, uint32_t (&v)[4]) {
@@ -179,6 +173,29 @@ __global__ __launch_bounds__(kPartialThreads) void k_scan_single(const uint32_t*
     if (threadIdx.x == 0 && total_dev) *total_dev = carry;
 }
 
+__global__ __launch_bounds__(kPartialThreads) void k_scan_single(const uint32_t* __restrict__ in,
+                                                                 uint32_t* __restrict__ out, size_t n,
+                                                                 uint32_t* __restrict__ total_dev,
+                                                                 const uint2* __restrict__ kr_in, size_t n_kr,
+                                                                 uint32_t* __restrict__ kr_out) {
+    __shared__ uint32_t lds[2][kPartialThreads / 64];
+    __shared__ uint2 lds_kr[kPartialThreads / 64];
+    if (kr_in) reduce_ranges(kr_in, n_kr, kr_out, lds_kr);
+    scan_single(in, out, n, total_dev, lds);
+}
+
+// In-place scans of up to kMaxViews small arrays, one workgroup each (blockIdx.y).
+struct ScanViews {
+    uint32_t* a[kMaxViews];
+    uint32_t n[kMaxViews];
+};
+
+__global__ __launch_bounds__(kPartialThreads) void k_scan_single_views(ScanViews v) {
+    __shared__ uint32_t lds[2][kPartialThreads / 64];
+    const int i = blockIdx.y;
+    scan_single(v.a[i], v.a[i], v.n[i], nullptr, lds);
+}
+
 }  // namespace
 
 size_t scan_tmp_elems(size_t n) {
@@ -206,6 +223,19 @@ int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
     GSR_LAUNCH_CHECK("scan_partials");
     k_scan_final<<<dim3((unsigned)nb), dim3(kThreads), 0, s>>>(in, out, n, tmp);
     GSR_LAUNCH_CHECK("scan_final");
+    return GSR_OK;
+}
+
+int scan_single_views(uint32_t* const* arrays, const uint32_t* n, int k, hipStream_t s) {
+    if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "scan: view count out of range");
+    ScanViews v{};
+    for (int i = 0; i < k; ++i) {
+        if (n[i] > kSingleMax) return set_error(GSR_ERR_INVALID, "scan: array too long for a single-workgroup scan");
+        v.a[i] = arrays[i];
+        v.n[i] = n[i];
+    }
+    k_scan_single_views<<<dim3(1, (unsigned)k), kPartialThreads, 0, s>>>(v);
+    GSR_LAUNCH_CHECK("scan_single_views");
     return GSR_OK;
 }
 

@@ -147,19 +147,21 @@ class ViewBatchPipeline:
     `groups`: list of (ctxs, cams, outs, stream), k views each.  Everything of
     a group runs on the group's stream, so no cross-stream event is needed
     (each costs the frame ~50 us here: tools/event_cost.py): step() finishes
-    the next group's pending frames (gsr_render_finish per view: the host
-    waits for the view's counts, then enqueues its binning, tile sort and
-    compositing), then begins the group's next frames: the shared cull +
-    preprocess of its k views, then their depth sorts, batched into one launch
-    per radix step (gsr_render_begin_sorts).  The groups' streams overlap one another, as the
-    views of ViewPipeline do.  drain() finishes every pending frame.  Images
+    the next group's pending frames (gsr_render_finish_views: the host waits
+    for the views' counts, then enqueues their binning, tile sort and
+    compositing, one launch per stage for the group), then begins the group's
+    next frames: the shared cull + preprocess of its k views, then their depth
+    sorts, batched into one launch per radix step (gsr_render_begin_sorts).
+    The groups' streams overlap one another, as the views of ViewPipeline do.
+    batched_sorts / batched_finish=False use the per-view calls instead.  drain() finishes every pending frame.  Images
     are identical to rendering each view alone (tests/test_gpu_multiview.py)."""
 
-    def __init__(self, groups, scene, settings, batched_sorts=True):
+    def __init__(self, groups, scene, settings, batched_sorts=True, batched_finish=True):
         assert len(groups) >= 1
         self.groups = groups
         self.scene, self.settings = scene, settings
         self.batched_sorts = batched_sorts  # the group's depth sorts in one launch per radix step
+        self.batched_finish = batched_finish  # the group's second halves in one launch per stage
         self.pending = [False] * len(groups)
         self.next = 0
 
@@ -168,10 +170,13 @@ class ViewBatchPipeline:
         return len(self.groups[self.next][0])
 
     def _finish(self, gi):
-        from .rasterizer import render_finish
+        from .rasterizer import render_finish, render_finish_views
         ctxs, _, _, stream = self.groups[gi]
-        for c in ctxs:
-            render_finish(c, stream)
+        if self.batched_finish:
+            render_finish_views(ctxs, stream)
+        else:
+            for c in ctxs:
+                render_finish(c, stream)
         self.pending[gi] = False
 
     def step(self):

@@ -273,6 +273,15 @@ def render_begin_sorts(ctxs, stream=None):
     _lib.check(_lib.load().gsr_render_begin_sorts(arr, k, _stream_handle(stream)), "gsr_render_begin_sorts")
 
 
+def render_finish_views(ctxs, stream=None):
+    """gsr_render_finish_views: completes the pending frames of `ctxs` (all
+    begun on `stream`) with one launch per stage for the group; identical
+    to render_finish on each."""
+    k = len(ctxs)
+    arr = (ctypes.c_void_p * k)(*[c.handle for c in ctxs])
+    _lib.check(_lib.load().gsr_render_finish_views(arr, k, _stream_handle(stream)), "gsr_render_finish_views")
+
+
 _default_ctx = {}
 
 

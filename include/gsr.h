@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 3
+#define GSR_ABI_VERSION 4
 
 typedef enum gsr_status {
     GSR_OK = 0,
@@ -164,6 +164,12 @@ int gsr_render_begin_sort(gsr_context* ctx, void* stream);
  * launch per radix step on `stream` (which then also takes their
  * gsr_render_finish). */
 int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream);
+/* gsr_render_finish for k begun frames pending on the same `stream` (e.g. the
+ * views of one gsr_render_begin_sorts): binning, tile sort, compositing and
+ * merge run as one launch per step for all k.  The views must share frame
+ * size, t_min, background, output layout, fragment mode and chunk length.
+ * Results are identical to k gsr_render_finish calls. */
+int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream);
 
 int gsr_context_stats(const gsr_context* ctx, gsr_frame_stats* out);
 

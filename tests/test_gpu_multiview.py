@@ -95,8 +95,8 @@ def test_contexts_share_one_scene_concurrently(gpu):
     scene.close()
 
 
-@pytest.mark.parametrize("batched_sorts", [True, False])
-def test_shared_scene_pass_matches_serial_renders(gpu, batched_sorts):
+@pytest.mark.parametrize("batched_sorts,batched_finish", [(True, True), (True, False), (False, False)])
+def test_shared_scene_pass_matches_serial_renders(gpu, batched_sorts, batched_finish):
     """gsr_render_begin_views (one cull + preprocess pass over the scene for a
     group of views) through ViewBatchPipeline with two groups: images, radii
     and counts identical to each view rendered alone."""
@@ -116,7 +116,7 @@ def test_shared_scene_pass_matches_serial_renders(gpu, batched_sorts):
         want_stats.append(ref_ctx.stats())
     groups = [(ctxs[g * K:(g + 1) * K], cams[g * K:(g + 1) * K], outs[g * K:(g + 1) * K], streams[g])
               for g in range(G)]
-    pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=batched_sorts)
+    pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=batched_sorts, batched_finish=batched_finish)
     for _ in range(3 * G + 1):  # every group several times, one group a step ahead
         pipe.step()
     pipe.drain()
@@ -166,3 +166,56 @@ def test_shared_scene_pass_radii_and_errors(gpu):
     for c in ctxs + [ref]:
         c.close()
     scene.close()
+
+
+def test_finish_views_mixed_frames(gpu):
+    """gsr_render_finish_views over frames begun one by one (gsr_render_begin)
+    on one stream, of two different scenes, one of them with no visible
+    Gaussian: identical to finishing each alone; protocol errors."""
+    import torch
+
+    from gsviewer_amd.rasterizer import HipContext, HipScene, render_begin, render_finish_views, render_into
+    scene, st, cams, ctxs, streams, outs = _setup(3)
+    g = garden_standin(3000, seed=5, sh_degree=3)
+    g.xyz = g.xyz + np.float32(1e8)  # beyond the far plane: nothing visible
+    far = HipScene.from_gaussian_data(g)
+    scenes = [scene, far, scene]
+    s = torch.cuda.Stream()
+    with pytest.raises(RuntimeError, match="no frame was begun"):
+        render_finish_views(ctxs, s)
+    for _ in range(2):  # twice: buffers sized by the first frames are reused
+        for k in range(3):
+            render_begin(ctxs[k], scenes[k], cams[k], st, outs[k], stream=s)
+        render_finish_views(ctxs, s)
+    torch.cuda.synchronize()
+    ref = HipContext()
+    for k in range(3):
+        o = torch.empty_like(outs[k])
+        render_into(ref, scenes[k], cams[k], st, o)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(outs[k].cpu().numpy(), o.cpu().numpy(), err_msg=f"view {k}")
+        want = ref.stats()
+        got = ctxs[k].stats()
+        for f in ("n_visible", "n_instances"):
+            assert got[f] == want[f], (k, f)
+    assert ctxs[1].stats()["n_visible"] == 0
+    # misuse: the same context twice; frames of different sizes; another stream
+    render_begin(ctxs[0], scene, cams[0], st, outs[0], stream=s)
+    with pytest.raises(RuntimeError, match="contexts must differ"):
+        render_finish_views([ctxs[0], ctxs[0]], s)
+    with pytest.raises(RuntimeError, match="not the frames' stream"):
+        render_finish_views([ctxs[0]], streams[0])
+    from gsviewer_amd.multiview import view_of
+    from gsviewer_amd.rasterizer import camera_from
+    small = camera_from(view_of(1, 90, 160))
+    o_small = torch.empty((90, 160, 3), dtype=torch.float32, device="cuda")
+    render_begin(ctxs[1], scene, small, st, o_small, stream=s)
+    with pytest.raises(RuntimeError, match="differ in frame size"):
+        render_finish_views([ctxs[0], ctxs[1]], s)
+    render_finish_views([ctxs[0]], s)
+    render_finish_views([ctxs[1]], s)
+    torch.cuda.synchronize()
+    for c in ctxs + [ref]:
+        c.close()
+    scene.close()
+    far.close()
