@@ -75,6 +75,8 @@ struct PendingFrame {
     size_t n = 0;
     int slot = 0;
     uint32_t *ka = nullptr, *va = nullptr, *kb = nullptr, *vb = nullptr;  // depth sort buffers (result in ka/va)
+    uint32_t *pa = nullptr, *pb = nullptr;  // packed tile rects carried by the depth sort (result in pa)
+    bool packed = false;                    // the depth sort carries them (frames of <= 256 x 256 tiles)
     bool sort_ready = false;  // gsr_render_begin_views done, gsr_render_begin_sort not yet
 };
 }  // namespace gsr
@@ -88,6 +90,7 @@ struct gsr_context {
     gsr::DevBuf<uint32_t> keys_a, keys_b, vals_a, vals_b;   // depth sort (capacity N)
     gsr::DevBuf<uint2> trect;                               // per record: packed tile rectangle
     gsr::DevBuf<uint2> trect_sorted;                        // the same, in depth order (binning)
+    gsr::DevBuf<uint32_t> rect4_a, rect4_b;                 // packed rects, depth sort payload
     gsr::DevBuf<uint32_t> bin_tmp;                          // binning block offsets
     gsr::DevBuf<uint32_t> tkeys_a, tkeys_b, tvals_a, tvals_b;  // tile sort (capacity D)
     gsr::DevBuf<uint32_t> radix_tmp;
@@ -212,6 +215,8 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
     if ((rc = c->vals_b.ensure(n, "vals"))) return rc;
     if ((rc = c->trect.ensure(n, "trect"))) return rc;
     if ((rc = c->trect_sorted.ensure(n, "trect_sorted"))) return rc;
+    if ((rc = c->rect4_a.ensure(n, "rect4"))) return rc;
+    if ((rc = c->rect4_b.ensure(n, "rect4"))) return rc;
     if ((rc = c->bin_tmp.ensure(bin_tmp_elems(n), "bin_tmp"))) return rc;
     if ((rc = c->radix_tmp.ensure(radix_tmp_elems(n), "radix_tmp"))) return rc;
     if (!c->done_ctr.p) {
@@ -265,10 +270,31 @@ void prof_accumulate(gsr_context* c, int slot, bool wait) {
 }
 
 // Stable sort of (key, val) pairs; totals = digit-total scratch.
+// The frame's depth sort (pairs (depth key, slot), over the upper bound n; the
+// device count V bounds the work); carries the packed tile rects as payload
+// when the frame's tiles fit 8 bits per coordinate.
+int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const uint32_t* key_range, uint32_t* totals,
+               hipStream_t s);
+
 int sort_pairs(gsr_context* c, uint32_t** ka, uint32_t** va, uint32_t** kb, uint32_t** vb, bool ident, size_t n,
                const uint32_t* n_dev, int bits, int passes, const uint32_t* key_range, uint32_t* totals,
                hipStream_t s) {
     return radix_sort_pairs(ka, va, kb, vb, ident, n, n_dev, bits, passes, key_range, c->radix_tmp.p, totals, s);
+}
+
+bool rects_packable(const FrameUniforms& u) {
+    const bool off = std::getenv("GSR_NO_RECT_PAYLOAD") != nullptr;  // A/B and test knob, read per frame
+    return !off && u.tiles_x <= kPackedRectTiles && u.tiles_y <= kPackedRectTiles;
+}
+
+int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const uint32_t* key_range, uint32_t* totals,
+               hipStream_t s) {
+    f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
+    f.pa = c->rect4_a.p, f.pb = c->rect4_b.p;
+    f.packed = rects_packable(f.u);
+    if (f.n == 0) return GSR_OK;
+    return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32, kDepthPasses, key_range,
+                            c->radix_tmp.p, totals, s, f.packed ? c->trect.p : nullptr, &f.pa, &f.pb);
 }
 
 // Wait until the last preprocess block has stored this frame's (V, D, seq) to
@@ -411,7 +437,7 @@ int gsr_context_destroy(gsr_context* c) {
     c->vis_mask.release(); c->wave_counts.release(); c->scan_tmp.release(); c->recs.release();
     c->block_ranges.release();
     c->keys_a.release(); c->keys_b.release(); c->vals_a.release(); c->vals_b.release();
-    c->trect.release(); c->trect_sorted.release(); c->bin_tmp.release(); c->tkeys_a.release(); c->tkeys_b.release(); c->tvals_a.release();
+    c->trect.release(); c->trect_sorted.release(); c->rect4_a.release(); c->rect4_b.release(); c->bin_tmp.release(); c->tkeys_a.release(); c->tkeys_b.release(); c->tvals_a.release();
     c->tvals_b.release(); c->radix_tmp.release(); c->zero.release();
     c->chunk_cnt.release(); c->chunk_base.release();
     c->chunk_desc.release(); c->chunk_order.release(); c->partial.release();
@@ -482,10 +508,9 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
 
     // depth sort over the upper bound N; the device count V bounds the work
     PendingFrame& f = c->pend;
-    f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
-    if (n > 0 && (rc = sort_pairs(c, &f.ka, &f.va, &f.kb, &f.vb, true, n, counters + 0, 32, kDepthPasses,
-                                  c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s)))
-        return rc;
+    f.n = n;
+    f.u = u;
+    if ((rc = depth_sort(c, f, counters + 0, c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s))) return rc;
     if ((rc = prof_record(c, slot, EV_DSORT, s))) return rc;
     f.active = true;
     f.u = u;
@@ -575,11 +600,8 @@ int gsr_render_begin_sort(gsr_context* c, void* stream) {
     const ZeroLayout zl(f.u.tiles_x * f.u.tiles_y);
     uint32_t* counters = c->zero.p + zl.counters;
     // depth sort over the upper bound N; the device count V bounds the work
-    f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
     int rc;
-    if (f.n > 0 && (rc = sort_pairs(c, &f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters + 0, 32, kDepthPasses,
-                                    c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s)))
-        return rc;
+    if ((rc = depth_sort(c, f, counters + 0, c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s))) return rc;
     f.sort_ready = false;
     f.active = true;
     f.stream = s;
@@ -603,8 +625,13 @@ int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream) {
             if (ctxs[w] == c) return set_error(GSR_ERR_INVALID, "render_begin_sorts: contexts must differ");
         const ZeroLayout zl(f.u.tiles_x * f.u.tiles_y);
         f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
+        f.pa = c->rect4_a.p, f.pb = c->rect4_b.p;
+        f.packed = rects_packable(f.u);
+        if (f.packed != rects_packable(ctxs[0]->pend.u))
+            return set_error(GSR_ERR_INVALID, "render_begin_sorts: views differ in frame size");
         views[v] = RadixViewArgs{&f.ka, &f.va, &f.kb, &f.vb, c->zero.p + zl.counters, c->zero.p + zl.key_range,
-                                 c->radix_tmp.p, c->zero.p + zl.totals_depth};
+                                 c->radix_tmp.p, c->zero.p + zl.totals_depth, f.packed ? c->trect.p : nullptr,
+                                 &f.pa, &f.pb};
     }
     int rc;
     if (n > 0 && (rc = radix_sort_pairs_views(views, k, true, n, 32, kDepthPasses, s))) return rc;
@@ -651,7 +678,7 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         if ((rc = c->tvals_b.ensure(n_dup, "tile_vals"))) return rc;
         if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(n_dup), radix_tmp_elems(n)), "radix_tmp")))
             return rc;
-        if ((rc = launch_binning(f.va, c->trect.p, n_vis, u.tiles_x, c->bin_tmp.p, c->trect_sorted.p, c->tkeys_a.p,
+        if ((rc = launch_binning(f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, u.tiles_x, c->bin_tmp.p, c->trect_sorted.p, c->tkeys_a.p,
                                  c->tvals_a.p, s)))
             return rc;
     }
@@ -768,7 +795,9 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         if ((rc = c->tmax.ensure(mc, "tmax"))) return rc;
         uint32_t* counters = c->zero.p + zl.counters;
         tka[v] = c->tkeys_a.p, tkb[v] = c->tkeys_b.p, tva[v] = c->tvals_a.p, tvb[v] = c->tvals_b.p;
-        fv[v] = FinishView{f.va, c->trect.p, n_vis, n_dup, c->bin_tmp.p, c->trect_sorted.p, tka[v], tva[v],
+        if (f.packed != c0->pend.packed)
+            return set_error(GSR_ERR_INVALID, "render_finish_views: views differ in frame size or settings");
+        fv[v] = FinishView{f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, n_dup, c->bin_tmp.p, c->trect_sorted.p, tka[v], tva[v],
                            reinterpret_cast<uint2*>(c->zero.p + zl.ranges), c->chunk_cnt.p, c->chunk_base.p,
                            counters + 2, c->chunk_desc.p, c->chunk_order.p, c->tmax.p, c->zero.p + zl.sat,
                            c->recs.p, f.out, c->partial.p};

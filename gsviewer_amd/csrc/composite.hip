@@ -34,22 +34,35 @@ __device__ __forceinline__ uint32_t rect_tiles(uint2 tr) {
     return (tx0 <= tx1) ? (tx1 - tx0 + 1) * (ty1 - ty0 + 1) : 0u;
 }
 
+// Packed rectangle (radix_sort_pairs payload, pack_rect) back to the uint2 form.
+__device__ __forceinline__ uint2 unpack_rect(uint32_t p) {
+    return make_uint2((p & 0xffu) | ((p >> 8) & 0xffu) << 16, ((p >> 16) & 0xffu) | (p >> 24) << 16);
+}
+
 // Also writes the gathered rects in depth order (trect_sorted), so that
 // k_bin_write reads them coalesced instead of gathering them a second time.
+// kPacked: the depth sort carried the rects (rect4_sorted, in depth order):
+// nothing is gathered.
+template <bool kPacked>
 __device__ __forceinline__ void bin_reduce(const uint32_t* __restrict__ sorted_ids, const uint2* __restrict__ trect,
-                                           uint32_t n_vis, uint32_t* __restrict__ block_sums,
-                                           uint2* __restrict__ trect_sorted, uint32_t blk, uint32_t* lds) {
+                                           const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
+                                           uint32_t* __restrict__ block_sums, uint2* __restrict__ trect_sorted,
+                                           uint32_t blk, uint32_t* lds) {
     const uint32_t base = blk * kBinBlock + threadIdx.x;
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
         const uint32_t r = base + k * kThreads;
         if (r < n_vis) {
-            const uint32_t id = sorted_ids[r];
-            // (ids are < n_vis by construction)
-            const uint2 tr = id < n_vis ? trect[id] : make_uint2(0xffffu, 0u);
-            trect_sorted[r] = tr;
-            s += rect_tiles(tr);
+            if constexpr (kPacked) {
+                s += rect_tiles(unpack_rect(rect4_sorted[r]));
+            } else {
+                const uint32_t id = sorted_ids[r];
+                // (ids are < n_vis by construction)
+                const uint2 tr = id < n_vis ? trect[id] : make_uint2(0xffffu, 0u);
+                trect_sorted[r] = tr;
+                s += rect_tiles(tr);
+            }
         }
     }
     s = wave_reduce_sum(s);
@@ -58,18 +71,22 @@ __device__ __forceinline__ void bin_reduce(const uint32_t* __restrict__ sorted_i
     if (threadIdx.x == 0) block_sums[blk] = lds[0] + lds[1] + lds[2] + lds[3];
 }
 
+template <bool kPacked>
 __global__ __launch_bounds__(kThreads) void k_bin_reduce(const uint32_t* __restrict__ sorted_ids,
-                                                         const uint2* __restrict__ trect, uint32_t n_vis,
+                                                         const uint2* __restrict__ trect,
+                                                         const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
                                                          uint32_t* __restrict__ block_sums,
                                                          uint2* __restrict__ trect_sorted) {
     __shared__ uint32_t lds[kThreads / 64];
-    bin_reduce(sorted_ids, trect, n_vis, block_sums, trect_sorted, blockIdx.x, lds);
+    bin_reduce<kPacked>(sorted_ids, trect, rect4_sorted, n_vis, block_sums, trect_sorted, blockIdx.x, lds);
 }
 
 // Exclusive offsets of the block's splats (block prefix + in-block scan), then
 // one (tile key, record slot) instance per covered tile, row-major.
+template <bool kPacked>
 __device__ __forceinline__ void bin_write(const uint32_t* __restrict__ sorted_ids,
-                                          const uint2* __restrict__ trect_sorted, uint32_t n_vis,
+                                          const uint2* __restrict__ trect_sorted,
+                                          const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
                                           const uint32_t* __restrict__ block_off, int tiles_x,
                                           uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ tile_vals,
                                           uint32_t blk, uint32_t* lds) {
@@ -84,7 +101,10 @@ __device__ __forceinline__ void bin_write(const uint32_t* __restrict__ sorted_id
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
-        tr[k] = (base + k < n_vis) ? trect_sorted[base + k] : make_uint2(0xffffu, 0u);
+        if constexpr (kPacked)
+            tr[k] = (base + k < n_vis) ? unpack_rect(rect4_sorted[base + k]) : make_uint2(0xffffu, 0u);
+        else
+            tr[k] = (base + k < n_vis) ? trect_sorted[base + k] : make_uint2(0xffffu, 0u);
         s += rect_tiles(tr[k]);
     }
     const int w = threadIdx.x >> 6;
@@ -107,19 +127,23 @@ __device__ __forceinline__ void bin_write(const uint32_t* __restrict__ sorted_id
     }
 }
 
+template <bool kPacked>
 __global__ __launch_bounds__(kThreads) void k_bin_write(const uint32_t* __restrict__ sorted_ids,
-                                                        const uint2* __restrict__ trect_sorted, uint32_t n_vis,
+                                                        const uint2* __restrict__ trect_sorted,
+                                                        const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
                                                         const uint32_t* __restrict__ block_off, int tiles_x,
                                                         uint32_t* __restrict__ tile_keys,
                                                         uint32_t* __restrict__ tile_vals) {
     __shared__ uint32_t lds[kThreads / 64];
-    bin_write(sorted_ids, trect_sorted, n_vis, block_off, tiles_x, tile_keys, tile_vals, blockIdx.x, lds);
+    bin_write<kPacked>(sorted_ids, trect_sorted, rect4_sorted, n_vis, block_off, tiles_x, tile_keys, tile_vals,
+                       blockIdx.x, lds);
 }
 
 // Views of a group (blockIdx.y = view); the grid covers the largest view.
 struct BinView {
     const uint32_t* sorted_ids;
     const uint2* trect;
+    const uint32_t* rect4_sorted;
     uint2* trect_sorted;
     uint32_t* block_sums;
     uint32_t* tile_keys;
@@ -130,18 +154,22 @@ struct BinViews {
     BinView v[kMaxViews];
 };
 
+template <bool kPacked>
 __global__ __launch_bounds__(kThreads) void k_bin_reduce_views(BinViews vs) {
     __shared__ uint32_t lds[kThreads / 64];
     const BinView& v = vs.v[blockIdx.y];
     if (blockIdx.x * kBinBlock >= v.n_vis) return;
-    bin_reduce(v.sorted_ids, v.trect, v.n_vis, v.block_sums, v.trect_sorted, blockIdx.x, lds);
+    bin_reduce<kPacked>(v.sorted_ids, v.trect, v.rect4_sorted, v.n_vis, v.block_sums, v.trect_sorted, blockIdx.x,
+                        lds);
 }
 
+template <bool kPacked>
 __global__ __launch_bounds__(kThreads) void k_bin_write_views(BinViews vs, int tiles_x) {
     __shared__ uint32_t lds[kThreads / 64];
     const BinView& v = vs.v[blockIdx.y];
     if (blockIdx.x * kBinBlock >= v.n_vis) return;
-    bin_write(v.sorted_ids, v.trect_sorted, v.n_vis, v.block_sums, tiles_x, v.tile_keys, v.tile_vals, blockIdx.x, lds);
+    bin_write<kPacked>(v.sorted_ids, v.trect_sorted, v.rect4_sorted, v.n_vis, v.block_sums, tiles_x, v.tile_keys,
+                       v.tile_vals, blockIdx.x, lds);
 }
 
 __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, uint32_t n, uint2* __restrict__ ranges,
@@ -942,15 +970,24 @@ extern "C" int64_t gsr_debug_comp_trace(void* host_dst, int64_t max_entries) {
 
 size_t bin_tmp_elems(size_t n_vis) { return (n_vis + kBinBlock - 1) / kBinBlock + 1; }
 
-int launch_binning(const uint32_t* sorted_ids, const uint2* trect, uint32_t n_vis, int tiles_x, uint32_t* tmp,
-                   uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s) {
+int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted, uint32_t n_vis,
+                   int tiles_x, uint32_t* tmp, uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals,
+                   hipStream_t s) {
     if (n_vis == 0) return GSR_OK;
     const uint32_t nb = (n_vis + kBinBlock - 1) / kBinBlock;
-    k_bin_reduce<<<nb, kThreads, 0, s>>>(sorted_ids, trect, n_vis, tmp, trect_sorted);
+    if (rect4_sorted)
+        k_bin_reduce<true><<<nb, kThreads, 0, s>>>(sorted_ids, trect, rect4_sorted, n_vis, tmp, trect_sorted);
+    else
+        k_bin_reduce<false><<<nb, kThreads, 0, s>>>(sorted_ids, trect, rect4_sorted, n_vis, tmp, trect_sorted);
     GSR_LAUNCH_CHECK("bin_reduce");
     int rc = scan_exclusive(tmp, tmp, nb, nullptr, nullptr, s);
     if (rc) return rc;
-    k_bin_write<<<nb, kThreads, 0, s>>>(sorted_ids, trect_sorted, n_vis, tmp, tiles_x, tile_keys, tile_vals);
+    if (rect4_sorted)
+        k_bin_write<true><<<nb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tmp, tiles_x,
+                                                  tile_keys, tile_vals);
+    else
+        k_bin_write<false><<<nb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tmp, tiles_x,
+                                                   tile_keys, tile_vals);
     GSR_LAUNCH_CHECK("bin_write");
     return GSR_OK;
 }
@@ -1040,17 +1077,27 @@ int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s) {
     uint32_t nb_max = 0;
     for (int i = 0; i < k; ++i) {
         const FinishView& f = views[i];
-        bv.v[i] = BinView{f.sorted_ids, f.trect, f.trect_sorted, f.bin_tmp, f.tile_keys, f.tile_vals, f.n_vis};
+        bv.v[i] = BinView{f.sorted_ids, f.trect, f.rect4_sorted, f.trect_sorted, f.bin_tmp, f.tile_keys, f.tile_vals,
+                          f.n_vis};
+        if ((f.rect4_sorted != nullptr) != (views[0].rect4_sorted != nullptr))
+            return set_error(GSR_ERR_INVALID, "binning: packed rectangles on some views only");
         arrays[i] = f.bin_tmp;
         nb[i] = (f.n_vis + kBinBlock - 1) / kBinBlock;
         nb_max = std::max(nb_max, nb[i]);
     }
     if (nb_max == 0) return GSR_OK;
-    k_bin_reduce_views<<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv);
+    const bool packed = views[0].rect4_sorted != nullptr;
+    if (packed)
+        k_bin_reduce_views<true><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv);
+    else
+        k_bin_reduce_views<false><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv);
     GSR_LAUNCH_CHECK("bin_reduce_views");
     int rc = scan_single_views(arrays, nb, k, s);
     if (rc) return rc;
-    k_bin_write_views<<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x);
+    if (packed)
+        k_bin_write_views<true><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x);
+    else
+        k_bin_write_views<false><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x);
     GSR_LAUNCH_CHECK("bin_write_views");
     return GSR_OK;
 }

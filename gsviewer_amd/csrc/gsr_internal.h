@@ -192,6 +192,9 @@ struct RadixViewArgs {
     const uint32_t* key_range;
     uint32_t* tmp;
     uint32_t* totals;
+    const uint2* rect_in = nullptr;  // payload (see radix_sort_pairs): on every view or none
+    uint32_t** pay_io = nullptr;
+    uint32_t** pay_alt = nullptr;
 };
 int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
                            hipStream_t s);
@@ -201,7 +204,12 @@ int radix_passes_for(int bits);
 int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt,
                      uint32_t** vals_alt, bool identity_vals, size_t n, const uint32_t* n_dev,
                      int bits, int passes, const uint32_t* key_range, uint32_t* tmp,
-                     uint32_t* totals, hipStream_t s);
+                     uint32_t* totals, hipStream_t s, const uint2* rect_in = nullptr,
+                     uint32_t** pay_io = nullptr, uint32_t** pay_alt = nullptr);
+// Payload (rect_in non-null): the tile rectangles rect_in[n] (uint2, in the
+// input order) travel with the pairs packed to 32 bits (pack_rect: frames of
+// at most 256 x 256 tiles); the sorted packed rectangles end in *pay_io.
+constexpr int kPackedRectTiles = 256;
 
 // scene.hip
 int scene_repack_from_fields(SceneData& sd, const float* xyz, const float* rot,
@@ -255,8 +263,10 @@ int launch_preprocess_views(const SceneData& sd, const ViewPreArgs* views, int k
 // composite.hip
 size_t bin_tmp_elems(size_t n_vis);
 // trect_sorted: n_vis uint2 of scratch (the rects in depth order)
-int launch_binning(const uint32_t* sorted_ids, const uint2* trect, uint32_t n_vis, int tiles_x,
-                   uint32_t* tmp, uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals,
+// rect4_sorted (nullable): the packed rects in depth order (the depth sort's
+// payload); else the rects are gathered by id from trect
+int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted, uint32_t n_vis,
+                   int tiles_x, uint32_t* tmp, uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals,
                    hipStream_t s);
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
                        hipStream_t s);
@@ -283,6 +293,7 @@ struct FinishView {
     // binning (n_vis, n_dup: this view's exact counts)
     const uint32_t* sorted_ids;
     const uint2* trect;
+    const uint32_t* rect4_sorted;  // nullable, on every view or none (launch_binning)
     uint32_t n_vis, n_dup;
     uint32_t* bin_tmp;
     uint2* trect_sorted;

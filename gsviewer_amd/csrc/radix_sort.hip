@@ -154,16 +154,31 @@ __global__ __launch_bounds__(64) void k_rs_offsets(uint32_t* __restrict__ hist, 
     rs_offsets(hist, ntiles, pa, totals, blockIdx.x);
 }
 
-template <int kR>
+// Tile rectangle of a splat packed in 32 bits (tx0 | tx1 << 8 | ty0 << 16 |
+// ty1 << 24) for frames of at most 256 x 256 tiles; empty: tx0 > tx1.
+__device__ __forceinline__ uint32_t pack_rect(uint2 tr) {
+    const uint32_t tx0 = tr.x & 0xffffu, tx1 = tr.x >> 16, ty0 = tr.y & 0xffffu, ty1 = tr.y >> 16;
+    return tx0 > tx1 ? 0xffu : (tx0 | tx1 << 8 | ty0 << 16 | ty1 << 24);
+}
+
+// kPay: a 32-bit payload travels with each pair (the packed tile rectangle of
+// the depth sort, so the binning reads it in sorted order instead of
+// gathering it by id).  Its first pass reads the rectangles (rect_in, in
+// input order) and packs them; later passes read pay_in.
+template <int kR, bool kPay>
 __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
                                            bool identity_vals, uint32_t* __restrict__ keys_out,
                                            uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ n_dev,
                                            uint32_t n_host, const PassArgs& pa,
                                            const uint32_t* __restrict__ hist_off,
-                                           const uint32_t* __restrict__ totals, uint32_t ntiles, uint32_t tile) {
+                                           const uint32_t* __restrict__ totals, uint32_t ntiles, uint32_t tile,
+                                           const uint2* __restrict__ rect_in = nullptr,
+                                           const uint32_t* __restrict__ pay_in = nullptr,
+                                           uint32_t* __restrict__ pay_out = nullptr) {
     constexpr int kTileItems = kThreads * kR;
     __shared__ uint32_t s_keys[kTileItems];
     __shared__ uint32_t s_vals[kTileItems];
+    __shared__ uint32_t s_pay[kPay ? kTileItems : 1];
     __shared__ uint16_t wcnt[kWaves][kMaxRadix];  // per-wave digit counts, then per-wave prefixes
     __shared__ uint32_t dbase[kMaxRadix];         // tile-local exclusive digit offsets
     __shared__ uint32_t gbase[kMaxRadix];         // global position of LDS index 0 of digit d's run
@@ -191,13 +206,14 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
     const uint32_t base = tile0 + w * (kTileItems / kWaves) + __lane_id();
     const uint64_t lt = lanemask_lt();
 
-    uint32_t k_reg[kR], v_reg[kR], rank[kR];
+    uint32_t k_reg[kR], v_reg[kR], rank[kR], p_reg[kPay ? kR : 1];
 #pragma unroll
     for (int r = 0; r < kR; ++r) {  // issue every load first
         const uint32_t i = base + r * 64;
         const bool valid = i < n;
         k_reg[r] = valid ? keys_in[i] : 0u;
         v_reg[r] = valid ? (identity_vals ? i : vals_in[i]) : 0u;
+        if constexpr (kPay) p_reg[r] = valid ? (rect_in ? pack_rect(rect_in[i]) : pay_in[i]) : 0u;
     }
     __syncthreads();
 #pragma unroll
@@ -260,6 +276,7 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
             const uint32_t p = dbase[d] + wcnt[w][d] + rank[r];
             s_keys[p] = k_reg[r];
             s_vals[p] = v_reg[r];
+            if constexpr (kPay) s_pay[p] = p_reg[r];
         }
     }
     __syncthreads();
@@ -270,17 +287,19 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
         const uint32_t g = gbase[dg.of(key)] + j;
         keys_out[g] = key;
         vals_out[g] = s_vals[j];
+        if constexpr (kPay) pay_out[g] = s_pay[j];
     }
 }
 
-template <int kR>
+template <int kR, bool kPay>
 __global__ __launch_bounds__(kThreads) void k_rs_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, bool identity_vals,
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ n_dev,
     uint32_t n_host, PassArgs pa, const uint32_t* __restrict__ hist_off, const uint32_t* __restrict__ totals,
-    uint32_t ntiles) {
-    rs_scatter<kR>(keys_in, vals_in, identity_vals, keys_out, vals_out, n_dev, n_host, pa, hist_off, totals, ntiles,
-                   blockIdx.x);
+    uint32_t ntiles, const uint2* __restrict__ rect_in, const uint32_t* __restrict__ pay_in,
+    uint32_t* __restrict__ pay_out) {
+    rs_scatter<kR, kPay>(keys_in, vals_in, identity_vals, keys_out, vals_out, n_dev, n_host, pa, hist_off, totals,
+                         ntiles, blockIdx.x, rect_in, pay_in, pay_out);
 }
 
 // Batched: the sorts of several views in one launch per step, view =
@@ -294,6 +313,9 @@ struct SortView {
     uint32_t* hist;
     uint32_t* totals;
     PassArgs pa;
+    const uint2* rect_in;  // payload (kPay): first pass
+    const uint32_t* pay_in;
+    uint32_t* pay_out;
 };
 struct SortViews {
     SortView v[kMaxViews];
@@ -310,12 +332,12 @@ __global__ __launch_bounds__(64) void k_rs_offsets_views(SortViews sv, uint32_t 
     rs_offsets(v.hist, ntiles, v.pa, v.totals, blockIdx.x);
 }
 
-template <int kR>
+template <int kR, bool kPay>
 __global__ __launch_bounds__(kThreads) void k_rs_scatter_views(SortViews sv, bool identity_vals, uint32_t n_host,
                                                                uint32_t ntiles) {
     const SortView& v = sv.v[blockIdx.y];
-    rs_scatter<kR>(v.keys_in, v.vals_in, identity_vals, v.keys_out, v.vals_out, v.n_dev, n_host, v.pa, v.hist,
-                   v.totals, ntiles, blockIdx.x);
+    rs_scatter<kR, kPay>(v.keys_in, v.vals_in, identity_vals, v.keys_out, v.vals_out, v.n_dev, n_host, v.pa, v.hist,
+                         v.totals, ntiles, blockIdx.x, v.rect_in, v.pay_in, v.pay_out);
 }
 
 }  // namespace
@@ -332,7 +354,8 @@ int radix_passes_for(int bits) { return bits <= 0 ? 0 : (bits + kMaxBits - 1) / 
 template <int kR>
 static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
                        bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
-                       const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s) {
+                       const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s,
+                       const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt) {
     constexpr int kTileItems = kThreads * kR;
     const uint32_t nt = (uint32_t)((n + kTileItems - 1) / kTileItems);
     // upper bound of the radix over the passes (device-chosen widths never exceed it)
@@ -344,12 +367,22 @@ static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_a
         GSR_LAUNCH_CHECK("rs_upsweep");
         k_rs_offsets<<<radix_max, 64, 0, s>>>(tmp, nt, pa, totals);
         GSR_LAUNCH_CHECK("rs_offsets");
-        k_rs_scatter<kR><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev, (uint32_t)n,
-                                                 pa, tmp, totals, nt);
+        if (rect_in) {
+            k_rs_scatter<kR, true><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev,
+                                                           (uint32_t)n, pa, tmp, totals, nt, p == 0 ? rect_in : nullptr,
+                                                           *pay_io, *pay_alt);
+        } else {
+            k_rs_scatter<kR, false><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev,
+                                                            (uint32_t)n, pa, tmp, totals, nt, nullptr, nullptr,
+                                                            nullptr);
+        }
         GSR_LAUNCH_CHECK("rs_scatter");
         ident = false;
         uint32_t* t = *keys_io; *keys_io = *keys_alt; *keys_alt = t;
         t = *vals_io; *vals_io = *vals_alt; *vals_alt = t;
+        if (rect_in) {
+            t = *pay_io; *pay_io = *pay_alt; *pay_alt = t;
+        }
     }
     return GSR_OK;
 }
@@ -366,19 +399,28 @@ static int sort_passes_views(RadixViewArgs* views, int k, bool identity_vals, si
         for (int v = 0; v < k; ++v) {
             RadixViewArgs& a = views[v];
             sv.v[v] = SortView{*a.keys_io, *a.vals_io, *a.keys_alt, *a.vals_alt, a.n_dev, a.tmp, a.totals,
-                               PassArgs{a.key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p}};
+                               PassArgs{a.key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p},
+                               p == 0 ? a.rect_in : nullptr, a.rect_in ? *a.pay_io : nullptr,
+                               a.rect_in ? *a.pay_alt : nullptr};
         }
+        const bool pay = views[0].rect_in != nullptr;  // all views or none (radix_sort_pairs_views)
         k_rs_upsweep_views<kR><<<dim3(nt, k), kThreads, 0, s>>>(sv, (uint32_t)n, nt);
         GSR_LAUNCH_CHECK("rs_upsweep_views");
         k_rs_offsets_views<<<dim3(radix_max, k), 64, 0, s>>>(sv, nt);
         GSR_LAUNCH_CHECK("rs_offsets_views");
-        k_rs_scatter_views<kR><<<dim3(nt, k), kThreads, 0, s>>>(sv, ident, (uint32_t)n, nt);
+        if (pay)
+            k_rs_scatter_views<kR, true><<<dim3(nt, k), kThreads, 0, s>>>(sv, ident, (uint32_t)n, nt);
+        else
+            k_rs_scatter_views<kR, false><<<dim3(nt, k), kThreads, 0, s>>>(sv, ident, (uint32_t)n, nt);
         GSR_LAUNCH_CHECK("rs_scatter_views");
         ident = false;
         for (int v = 0; v < k; ++v) {
             RadixViewArgs& a = views[v];
             uint32_t* t = *a.keys_io; *a.keys_io = *a.keys_alt; *a.keys_alt = t;
             t = *a.vals_io; *a.vals_io = *a.vals_alt; *a.vals_alt = t;
+            if (a.rect_in) {
+                t = *a.pay_io; *a.pay_io = *a.pay_alt; *a.pay_alt = t;
+            }
         }
     }
     return GSR_OK;
@@ -391,13 +433,17 @@ int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size
     if (n > 0xffffffffull - 4 * kMinTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
     if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
         return set_error(GSR_ERR_INVALID, "radix sort: digit width out of range");
+    for (int v = 1; v < k; ++v)
+        if ((views[v].rect_in != nullptr) != (views[0].rect_in != nullptr))
+            return set_error(GSR_ERR_INVALID, "radix sort: payload on some views only");
     if ((bits + passes - 1) / passes <= 8) return sort_passes_views<16>(views, k, identity_vals, n, bits, passes, s);
     return sort_passes_views<8>(views, k, identity_vals, n, bits, passes, s);
 }
 
 int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
                      bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
-                     const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s) {
+                     const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s,
+                     const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt) {
     if (n == 0 || passes == 0) return GSR_OK;
     if (n > 0xffffffffull - 4 * kMinTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
     if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
@@ -405,9 +451,9 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
     // measured on MI355X: 2048-item tiles for wide digits, 4096 for <= 8-bit digits
     if ((bits + passes - 1) / passes <= 8)
         return sort_passes<16>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes, key_range,
-                               tmp, totals, s);
+                               tmp, totals, s, rect_in, pay_io, pay_alt);
     return sort_passes<8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes, key_range, tmp,
-                          totals, s);
+                          totals, s, rect_in, pay_io, pay_alt);
 }
 
 }  // namespace gsr

@@ -140,7 +140,10 @@ int gsr_render(gsr_context* ctx, const gsr_scene* scene, const gsr_camera* cam,
  * host) for the frame's visible/instance counts and enqueues the rest.  A
  * caller begins the next view's frame before finishing this one, so the
  * host never idles while the GPU could take more work.  One frame per
- * context may be pending; _finish takes the same stream. */
+ * context may be pending; _finish takes the same stream.  A context's buffers
+ * belong to the stream of its last frame until that frame completes: before
+ * using the context on another stream, synchronise (or make the new stream
+ * wait for the old one). */
 int gsr_render_begin(gsr_context* ctx, const gsr_scene* scene, const gsr_camera* cam,
                      const gsr_settings* settings, float* out_image_dev, int32_t* radii_dev,
                      void* stream);

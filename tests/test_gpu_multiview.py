@@ -219,3 +219,34 @@ def test_finish_views_mixed_frames(gpu):
         c.close()
     scene.close()
     far.close()
+
+
+def test_rect_payload_matches_gathered_rects(gpu, monkeypatch):
+    """The depth sort carrying the packed tile rectangles (default for frames
+    of <= 256 x 256 tiles) bins exactly as the by-id gather of the rectangles
+    (GSR_NO_RECT_PAYLOAD): same images and counts, single view and a batched
+    group."""
+    import torch
+
+    from gsviewer_amd.multiview import ViewBatchPipeline
+    from gsviewer_amd.rasterizer import render_into
+    scene, st, cams, ctxs, streams, outs = _setup(4)
+    got = {}
+    for mode in ("payload", "gather"):
+        if mode == "gather":
+            monkeypatch.setenv("GSR_NO_RECT_PAYLOAD", "1")
+        o = torch.empty_like(outs[0])
+        render_into(ctxs[0], scene, cams[1], st, o)
+        # the context moves to another stream: its frame on this one must be done
+        torch.cuda.synchronize()
+        pipe = ViewBatchPipeline([(ctxs, cams, outs, streams[0])], scene, st)
+        pipe.step()
+        pipe.drain()
+        torch.cuda.synchronize()
+        got[mode] = ([o.cpu().numpy()] + [x.cpu().numpy() for x in outs], [c.stats() for c in ctxs])
+    for a, b in zip(got["payload"][0], got["gather"][0]):
+        np.testing.assert_array_equal(a, b)
+    assert got["payload"][1] == got["gather"][1]
+    for c in ctxs:
+        c.close()
+    scene.close()
