@@ -842,13 +842,19 @@ __global__ __launch_bounds__(kThreads) GSR_COMP_OCC void k_composite_views(CompV
     composite_chunk<FRAG>(d, slot, lds[wave], v.list, v.recs, a, v.out, v.partial, v.sat, v.tmax);
 }
 
-// Fold the partial results of multi-chunk tiles in depth order: one block of
-// 16 waves per tile; wave w folds slice (w & 3) over the w >> 2 quarter of the
-// tile's chunks (up to the saturating chunk, if any) with 16 partial loads in
-// flight, and the four quarters are combined in order through LDS.  The
-// deepest tiles (~100 chunks) set this kernel's length, so their fold is
-// spread over 4 waves instead of walked by one.
-constexpr int kMergeThreads = 1024;
+// Fold the partial results of multi-chunk tiles in depth order: one block per
+// tile of 4 x P waves (P = kMergeParts); wave w folds slice (w & 3) over the
+// (w >> 2)-th of P parts of the tile's chunks (up to the saturating chunk, if
+// any) with 16 partial loads in flight, and the parts are combined in order
+// through LDS.  Default P = 1 (256 threads): with P = 4 (1024 threads) the
+// deepest tiles' fold was spread over 4 waves, but a 16-wave block waits for
+// a whole CU's worth of free slots while other views' compositors hold the
+// chip: 0.2124 / 0.2126 -> 0.207 / 0.2074 ms per frame in flight with P = 1,
+// and 17.4 -> 14.8 us alone (r1_s10 box).
+#ifndef GSR_MERGE_THREADS
+#define GSR_MERGE_THREADS 256
+#endif
+constexpr int kMergeThreads = GSR_MERGE_THREADS;
 constexpr int kMergeParts = kMergeThreads / 64 / 4;  // 4
 constexpr int kMergeDepth = 16;
 
