@@ -13,6 +13,14 @@ constexpr int kItems = 16;
 constexpr int kTileItems = kThreads * kItems;  // 4096
 constexpr int kPartialThreads = 1024;
 constexpr size_t kSingleMax = 131072;  // single-workgroup scan up to this many elements
+// Short single-workgroup scans (the binning's block sums, ~1000 entries) run as
+// 4-wave blocks: a 16-wave block waits for a whole CU's worth of free slots
+// while other views' compositors hold the chip (in flight,
+// k_scan_single_views averaged 68 us against 4.5 us alone).  Longer ones (the
+// visibility words, ~16k at 1M) keep 16 waves: with 4 the cull stage took
+// 8 us longer alone.
+constexpr int kSingleThreads = 256;
+constexpr size_t kSmallScan = 4 * kSingleThreads;  // one chunk of the 256-thread scan
 
 __device__ __forceinline__ void load16(const uint32_t* in, size_t base, size_t n, uint32_t (&v)[kItems]) {
     if (base + kItems <= n) {
@@ -53,10 +61,11 @@ __global__ __launch_bounds__(kThreads) void k_scan_reduce(const uint32_t* __rest
 // Optional side job of the single-block kernels: componentwise max over n_kr
 // uint2 entries (the per-block depth-key ranges {~kmin, kmax} of k_cull) into
 // kr_out[0..1].
+template <int NT>
 __device__ __forceinline__ void reduce_ranges(const uint2* __restrict__ kr_in, size_t n_kr, uint32_t* __restrict__ kr_out,
                                               uint2* lds) {
     uint2 m = make_uint2(0u, 0u);
-    for (size_t i = threadIdx.x; i < n_kr; i += kPartialThreads) {
+    for (size_t i = threadIdx.x; i < n_kr; i += NT) {
         const uint2 v = kr_in[i];
         m.x = max(m.x, v.x);
         m.y = max(m.y, v.y);
@@ -69,7 +78,7 @@ __device__ __forceinline__ void reduce_ranges(const uint2* __restrict__ kr_in, s
     if (__lane_id() == 0) lds[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < kPartialThreads / 64; ++w) {
+        for (int w = 1; w < NT / 64; ++w) {
             m.x = max(m.x, lds[w].x);
             m.y = max(m.y, lds[w].y);
         }
@@ -84,7 +93,7 @@ __global__ __launch_bounds__(kPartialThreads) void k_scan_partials(uint32_t* __r
                                                                    uint32_t* __restrict__ kr_out) {
     __shared__ uint32_t lds[kPartialThreads / 64];
     __shared__ uint2 lds_kr[kPartialThreads / 64];
-    if (kr_in) reduce_ranges(kr_in, n_kr, kr_out, lds_kr);
+    if (kr_in) reduce_ranges<kPartialThreads>(kr_in, n_kr, kr_out, lds_kr);
     const size_t per = (nb + kPartialThreads - 1) / kPartialThreads;
     const size_t b0 = (size_t)threadIdx.x * per;
     const size_t b1 = (b0 + per < nb) ? b0 + per : nb;
@@ -132,9 +141,10 @@ __global__ __launch_bounds__(kThreads) void k_scan_final(const uint32_t* __restr
 // for the small arrays of a frame (wave counts, tiles, block sums).  The array
 // is walked in 4096-element chunks: coalesced dwordx4 loads (next chunk
 // prefetched), a block scan per chunk, a running carry.
+template <int NT>
 __device__ __forceinline__ void scan_single(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t n,
-                                            uint32_t* __restrict__ total_dev, uint32_t (*lds)[kPartialThreads / 64]) {
-    constexpr size_t kChunk = 4 * kPartialThreads;
+                                            uint32_t* __restrict__ total_dev, uint32_t (*lds)[NT / 64]) {
+    constexpr size_t kChunk = 4 * NT;
     const bool aligned = (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
     auto load4 = [&](size_t c, uint32_t (&v)[4]) {
         const size_t i = c * kChunk + 4 * (size_t)threadIdx.x;
@@ -154,7 +164,7 @@ __device__ __forceinline__ void scan_single(const uint32_t* __restrict__ in, uin
         if (c + 1 < nchunks) load4(c + 1, nxt);
         const uint32_t s = cur[0] + cur[1] + cur[2] + cur[3];
         uint32_t total;
-        uint32_t run = carry + block_exclusive<kPartialThreads>(s, lds[c & 1], total);
+        uint32_t run = carry + block_exclusive<NT>(s, lds[c & 1], total);
         const size_t i = c * kChunk + 4 * (size_t)threadIdx.x;
         uint32_t o[4];
         for (int k = 0; k < 4; ++k) {
@@ -173,15 +183,16 @@ __device__ __forceinline__ void scan_single(const uint32_t* __restrict__ in, uin
     if (threadIdx.x == 0 && total_dev) *total_dev = carry;
 }
 
-__global__ __launch_bounds__(kPartialThreads) void k_scan_single(const uint32_t* __restrict__ in,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_scan_single(const uint32_t* __restrict__ in,
                                                                  uint32_t* __restrict__ out, size_t n,
                                                                  uint32_t* __restrict__ total_dev,
                                                                  const uint2* __restrict__ kr_in, size_t n_kr,
                                                                  uint32_t* __restrict__ kr_out) {
-    __shared__ uint32_t lds[2][kPartialThreads / 64];
-    __shared__ uint2 lds_kr[kPartialThreads / 64];
-    if (kr_in) reduce_ranges(kr_in, n_kr, kr_out, lds_kr);
-    scan_single(in, out, n, total_dev, lds);
+    __shared__ uint32_t lds[2][NT / 64];
+    __shared__ uint2 lds_kr[NT / 64];
+    if (kr_in) reduce_ranges<NT>(kr_in, n_kr, kr_out, lds_kr);
+    scan_single<NT>(in, out, n, total_dev, lds);
 }
 
 // In-place scans of up to kMaxViews small arrays, one workgroup each (blockIdx.y).
@@ -190,10 +201,10 @@ struct ScanViews {
     uint32_t n[kMaxViews];
 };
 
-__global__ __launch_bounds__(kPartialThreads) void k_scan_single_views(ScanViews v) {
-    __shared__ uint32_t lds[2][kPartialThreads / 64];
+__global__ __launch_bounds__(kSingleThreads) void k_scan_single_views(ScanViews v) {
+    __shared__ uint32_t lds[2][kSingleThreads / 64];
     const int i = blockIdx.y;
-    scan_single(v.a[i], v.a[i], v.n[i], nullptr, lds);
+    scan_single<kSingleThreads>(v.a[i], v.a[i], v.n[i], nullptr, lds);
 }
 
 }  // namespace
@@ -211,7 +222,10 @@ int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
         return GSR_OK;
     }
     if (n <= kSingleMax) {
-        k_scan_single<<<1, kPartialThreads, 0, s>>>(in, out, n, total_dev, kr_in, n_kr, kr_out);
+        if (n <= kSmallScan)
+            k_scan_single<kSingleThreads><<<1, kSingleThreads, 0, s>>>(in, out, n, total_dev, kr_in, n_kr, kr_out);
+        else
+            k_scan_single<kPartialThreads><<<1, kPartialThreads, 0, s>>>(in, out, n, total_dev, kr_in, n_kr, kr_out);
         GSR_LAUNCH_CHECK("scan_single");
         return GSR_OK;
     }
@@ -234,7 +248,7 @@ int scan_single_views(uint32_t* const* arrays, const uint32_t* n, int k, hipStre
         v.a[i] = arrays[i];
         v.n[i] = n[i];
     }
-    k_scan_single_views<<<dim3(1, (unsigned)k), kPartialThreads, 0, s>>>(v);
+    k_scan_single_views<<<dim3(1, (unsigned)k), kSingleThreads, 0, s>>>(v);
     GSR_LAUNCH_CHECK("scan_single_views");
     return GSR_OK;
 }
