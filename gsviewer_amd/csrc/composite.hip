@@ -784,17 +784,23 @@ __device__ uint4 g_comp_trace[2 * kTraceMax];
 #define GSR_COMP_WPE 8
 #endif
 #define GSR_COMP_OCC __attribute__((amdgpu_waves_per_eu(GSR_COMP_WPE, 8)))
+// compositing waves per block (each wave takes its own chunk; no block barrier)
+#ifndef GSR_COMP_THREADS
+#define GSR_COMP_THREADS 256
+#endif
+constexpr int kCompThreads = GSR_COMP_THREADS;
+constexpr int kCompWaves = kCompThreads / 64;
 template <int FRAG>
-__global__ __launch_bounds__(kThreads) GSR_COMP_OCC void k_composite(const uint4* __restrict__ desc,
+__global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const uint4* __restrict__ desc,
                                                         const uint32_t* __restrict__ order,
                                                         const uint32_t* __restrict__ n_chunks_dev,
                                                         const uint32_t* __restrict__ list,
                                                         const SplatRec* __restrict__ recs, CompositeArgs a,
                                                         float* __restrict__ out, float4* __restrict__ partial,
                                                         uint32_t* __restrict__ sat, float4* __restrict__ tmax) {
-    __shared__ float4 lds[kThreads / 64][kBatch * 3];
+    __shared__ float4 lds[kCompWaves][kBatch * 3];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t pos = blockIdx.x * (kThreads / 64) + wave;
+    const uint32_t pos = blockIdx.x * kCompWaves + wave;
     if (pos >= (uint32_t)a.num_tiles + n_chunks_dev[0]) return;  // device count of extra chunks
     const uint32_t slot = order[pos];
 #ifdef GSR_COMP_TRACE
@@ -831,11 +837,11 @@ struct CompViews {
 };
 
 template <int FRAG>
-__global__ __launch_bounds__(kThreads) GSR_COMP_OCC void k_composite_views(CompViews vs, CompositeArgs a) {
-    __shared__ float4 lds[kThreads / 64][kBatch * 3];
+__global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite_views(CompViews vs, CompositeArgs a) {
+    __shared__ float4 lds[kCompWaves][kBatch * 3];
     const CompView& v = vs.v[blockIdx.y];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t pos = blockIdx.x * (kThreads / 64) + wave;
+    const uint32_t pos = blockIdx.x * kCompWaves + wave;
     if (pos >= (uint32_t)a.num_tiles + v.n_chunks_dev[0]) return;
     const uint32_t slot = v.order[pos];
     const uint4 d = v.desc[slot];
@@ -1044,22 +1050,22 @@ int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n
                      const FrameUniforms& u, int frag_class, float t_min, const float* bg, int out_layout, float* out,
                      float4* partial, float4* tmax, hipStream_t s) {
     const CompositeArgs a = make_args(u, t_min, bg, out_layout);
-    const unsigned grid = (unsigned)((max_chunks + 3) / 4);
+    const unsigned grid = (unsigned)((max_chunks + kCompWaves - 1) / kCompWaves);
     switch (frag_class) {
         case kFragGauss:
-            k_composite<kFragGauss><<<grid, kThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial, sat,
+            k_composite<kFragGauss><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial, sat,
                                                               tmax);
             break;
         case kFragBillboard:
-            k_composite<kFragBillboard><<<grid, kThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
+            k_composite<kFragBillboard><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
                                                                   sat, tmax);
             break;
         case kFragFlatBall:
-            k_composite<kFragFlatBall><<<grid, kThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
+            k_composite<kFragFlatBall><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
                                                                  sat, tmax);
             break;
         default:
-            k_composite<kFragGaussBall><<<grid, kThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
+            k_composite<kFragGaussBall><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
                                                                   sat, tmax);
             break;
     }
@@ -1150,12 +1156,12 @@ int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, const 
         const FinishView& f = views[i];
         cv.v[i] = CompView{f.desc, f.order, f.n_extra_dev, f.tile_vals, f.recs, f.out, f.partial, f.sat, f.tmax};
     }
-    const dim3 grid((unsigned)((max_chunks + 3) / 4), (unsigned)k);
+    const dim3 grid((unsigned)((max_chunks + kCompWaves - 1) / kCompWaves), (unsigned)k);
     switch (frag_class) {
-        case kFragGauss: k_composite_views<kFragGauss><<<grid, kThreads, 0, s>>>(cv, a); break;
-        case kFragBillboard: k_composite_views<kFragBillboard><<<grid, kThreads, 0, s>>>(cv, a); break;
-        case kFragFlatBall: k_composite_views<kFragFlatBall><<<grid, kThreads, 0, s>>>(cv, a); break;
-        default: k_composite_views<kFragGaussBall><<<grid, kThreads, 0, s>>>(cv, a); break;
+        case kFragGauss: k_composite_views<kFragGauss><<<grid, kCompThreads, 0, s>>>(cv, a); break;
+        case kFragBillboard: k_composite_views<kFragBillboard><<<grid, kCompThreads, 0, s>>>(cv, a); break;
+        case kFragFlatBall: k_composite_views<kFragFlatBall><<<grid, kCompThreads, 0, s>>>(cv, a); break;
+        default: k_composite_views<kFragGaussBall><<<grid, kCompThreads, 0, s>>>(cv, a); break;
     }
     GSR_LAUNCH_CHECK("composite_views");
     return GSR_OK;
