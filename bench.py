@@ -10,12 +10,22 @@ weak scaling, no per-frame collective.
 
 Prints ONE JSON line on rank 0.  Stage timings come from HIP events recorded
 by libgsr on the render stream during the timed region.
+
+Launch: ``python bench.py --gpus N`` with N > 1 and no WORLD_SIZE in the
+environment starts ``torch.distributed.run`` (N ranks, 127.0.0.1) as a CHILD
+process before anything touches the GPU, and exits with its status; under
+torchrun (WORLD_SIZE set) the process is one rank and checks that the world
+size equals --gpus.  ``--dry-run`` runs the same launch, rendezvous, scene
+broadcast, view assignment and max-over-ranks timing on CPU over gloo, with
+no rendering (a CPU test of the launcher: tests/test_bench_launch.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -137,6 +147,60 @@ def valu_issue(kernel, args, ms_per_launch):
             "issue_ns_per_instr": {"valu": VALU_NS, "trans": TRANS_NS}, "source": src}
 
 
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Start n ranks of this script under torch.distributed.run as a child
+    process (one process per GPU, rendezvous on 127.0.0.1) and return its
+    exit status.  Nothing before this touches the GPU, so no process that
+    initialised HIP is ever replaced."""
+    env = dict(os.environ)
+    env["MASTER_ADDR"] = "127.0.0.1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    log("bench.py: launching", n, "ranks:", " ".join(cmd[1:]))
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args):
+    """The multi-rank skeleton of the GPU run, on CPU over gloo: rendezvous,
+    the one scene broadcast, view assignment and the barrier-bracketed
+    max-over-ranks timed region, with a no-op frame.  Rank 0 prints one JSON
+    line listing every rank; nothing is measured."""
+    import torch.distributed as dist
+
+    from gsviewer_amd.multiview import broadcast_scene, gather_objects, timed_region, view_of
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    if world > 1:
+        dist.init_process_group("gloo")
+    _, deg, W, H, desc = CONFIGS[args.config]
+    n = args.n or 1000
+    k_coef = (deg + 1) ** 2
+    g = make_scene(args.config, n, deg)[0] if rank == 0 else None
+    tensors, bcast = broadcast_scene(g, n, k_coef, "cpu")
+    views = [rank + world * j for j in range(max(1, args.inflight))]
+    cam0 = view_of(views[0], H, W)
+    elapsed = timed_region(lambda: None, args.steps, "cpu")
+    me = dict(rank=rank, world=dist.get_world_size() if world > 1 else 1, views=views,
+              view0_row2=[float(x) for x in cam0.get_view_matrix()[2]],
+              scene_sum=float(sum(float(t.double().sum()) for t in tensors)), elapsed=elapsed)
+    ranks = gather_objects(me, world)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "backend": "gloo" if world > 1 else None,
+                          "workload": desc, "n_gaussians": n, "steps": args.steps, "broadcast": bcast,
+                          "ranks": ranks}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -168,7 +232,15 @@ def main():
     ap.add_argument("--box", default="none", choices=["none", "aabb", "obb"],
                     help="boundary-box cull (SURVEY.md 8d C5): aabb = compute_aabb min/max x 0.5 around "
                          "points_center; obb = euler(30, 15, 0) deg, +-1.5")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the multi-rank launch over gloo (no GPU, no rendering)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.dry_run:
+        return dry_run(args)
 
     # One hardware queue per in-flight view stream (+ torch's own): HIP maps
     # streams round-robin onto GPU_MAX_HW_QUEUES queues (4 by default), and two
@@ -187,10 +259,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI on ROCm
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
     from gsviewer_amd import _lib
     from gsviewer_amd.multiview import ViewBatchPipeline, ViewPipeline, broadcast_scene, timed_region, view_of
@@ -256,13 +332,15 @@ def main():
             pipe.step()
         pipe.drain()
 
+    own = []
     if share == 1:
-        elapsed = timed_region(lambda: pipelined(args.steps), 1, dev)
+        elapsed = timed_region(lambda: pipelined(args.steps), 1, dev, own)
     else:
         # a step renders a group of `share` frames: time whole steps covering
         # args.steps frames, normalised to args.steps frames
         calls = (args.steps + share - 1) // share
-        elapsed = timed_region(lambda: pipelined(calls), 1, dev) * args.steps / (calls * share)
+        elapsed = timed_region(lambda: pipelined(calls), 1, dev, own) * args.steps / (calls * share)
+        own[0] *= args.steps / (calls * share)
     # single-view latency: the same number of frames of view 0, one at a time
     latency = timed_region(serial_frame, args.steps, dev) if K > 1 else elapsed
 
@@ -292,6 +370,11 @@ def main():
         stage = {name: ms[i] / max(frames.value, 1) for i, name in enumerate(_lib.STAGES)}
         stage["instrumented_ms_per_frame"] = 1e3 * prof_elapsed / args.steps
 
+    # every rank's own rate (validation of the weak-scaling line; outside the timed regions)
+    from gsviewer_amd.multiview import gather_objects
+    per_rank = gather_objects(dict(rank=rank, local_rank=local, views=[rank + world * j for j in range(K)],
+                                   elapsed_s=own[0], splats_per_s=n * args.steps / own[0],
+                                   n_visible=stats["n_visible"], n_instances=stats["n_instances"]), world)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -371,6 +454,9 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "broadcast": bcast,
+        "process_group": {"backend": dist.get_backend() if world > 1 else None,
+                          "world_size": dist.get_world_size() if world > 1 else 1},
+        "per_rank": per_rank,
         "scene_gen_s": t_gen,
     }
     print(json.dumps(res), flush=True)

@@ -79,6 +79,7 @@ class GsrBox(ctypes.Structure):
     ]
 
 
+GSR_OK, GSR_ERR_INVALID, GSR_ERR_HIP, GSR_ERR_NOMEM, GSR_ERR_OVERFLOW = 0, -1, -2, -3, -4  # gsr_status
 GSR_PLY_BINARY_LE, GSR_PLY_BINARY_BE, GSR_PLY_ASCII = 0, 1, 2
 GSR_BOX_NONE, GSR_BOX_AABB, GSR_BOX_OBB = 0, 1, 2
 
@@ -110,6 +111,7 @@ SIGNATURES = {
     "gsr_debug_host_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "gsr_debug_sort_pairs": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _P, _P, _P]),
     "gsr_debug_copy": (ctypes.c_int64, [_P, ctypes.c_int32, _P, ctypes.c_int64, _P]),
+    "gsr_debug_stall": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "gsr_context_set_profiling": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gsr_context_stage_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     # gsr_io.h

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "gsr_internal.h"
 
@@ -35,25 +36,31 @@ int set_error(int code, const std::string& msg) {
 
 namespace {
 
+// A context-owned device array that grows on demand.  Growth never frees the
+// old allocation: hipFree synchronises the whole device, which would stall
+// every other view in flight, and the context's previous frame may still read
+// the old block.  Retired blocks are freed with the context (release()).
+// gsr_context_reserve sizes everything up front, so a steady state never grows.
 template <typename T>
 struct DevBuf {
     T* p = nullptr;
     size_t cap = 0;  // elements
+    std::vector<void*> retired;
     int ensure(size_t n, const char* what) {
         if (n <= cap && p) return GSR_OK;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
         size_t want = n < 64 ? 64 : n + n / 8;  // 12.5% headroom against regrowth
-        if (hipMalloc(&p, want * sizeof(T)) != hipSuccess) {
-            p = nullptr;
+        T* q = nullptr;
+        if (hipMalloc(&q, want * sizeof(T)) != hipSuccess)
             return set_error(GSR_ERR_NOMEM, std::string("context: hipMalloc failed for ") + what);
-        }
+        if (p) retired.push_back(p);
+        p = q;
         cap = want;
         return GSR_OK;
     }
     void release() {
         if (p) (void)hipFree(p);
+        for (void* r : retired) (void)hipFree(r);
+        retired.clear();
         p = nullptr;
         cap = 0;
     }
@@ -122,6 +129,8 @@ struct gsr_context {
     double host_ms[3] = {};  // host time in gsr_render: enqueue before the wait, the wait, enqueue after
     int64_t host_frames = 0;
     int64_t prof_frames = 0;
+    bool failed = false;           // a wait timed out or the stream faulted: no further frames
+    int64_t wait_timeout_ms = 2000;
 };
 
 namespace gsr {
@@ -130,6 +139,10 @@ namespace {
 int build_uniforms(const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, FrameUniforms& u) {
     if (cam->width <= 0 || cam->height <= 0 || cam->width > 32768 || cam->height > 32768)
         return set_error(GSR_ERR_INVALID, "camera: width/height out of range");
+    if (st->out_layout != 0 && st->out_layout != 1)
+        return set_error(GSR_ERR_INVALID, "settings: out_layout must be 0 ([3,H,W]) or 1 ([H,W,3])");
+    if (!(st->t_min >= 0.f && st->t_min < 1.f))
+        return set_error(GSR_ERR_INVALID, "settings: t_min must be in [0, 1)");
     std::memcpy(u.V, cam->view, sizeof(u.V));
     std::memcpy(u.P, cam->proj, sizeof(u.P));
     std::memcpy(u.hfov, cam->hfovxy_focal, sizeof(u.hfov));
@@ -303,6 +316,11 @@ int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const 
 // a spin far longer than any frame is the stream queried (a query may itself
 // enqueue a marker, i.e. a stall): a stream that stopped making progress (a
 // fault) is then synchronised, which reports the error.
+// The wait has a hard deadline (GSR_WAIT_TIMEOUT_MS, default 2000 ms): a
+// stream that makes no progress for that long (a hung kernel, or work queued
+// ahead of the frame that never finishes) fails the call with GSR_ERR_HIP and
+// marks the context failed instead of spinning forever; a failed context
+// refuses further frames (destroy it).
 int wait_counts(gsr_context* c, hipStream_t s) {
     const uint32_t want = c->seq;
     const auto t0 = std::chrono::steady_clock::now();
@@ -312,11 +330,17 @@ int wait_counts(gsr_context* c, hipStream_t s) {
             const hipError_t q = hipStreamQuery(s);
             if (q == hipSuccess) {  // stream drained: the store must be visible now
                 if (__atomic_load_n(&c->host_counters[2], __ATOMIC_ACQUIRE) == want) return GSR_OK;
+                c->failed = true;
                 return set_error(GSR_ERR_HIP, "render: frame counters were not published");
             }
             if (q != hipErrorNotReady) {
-                GSR_HIP_CHECK(hipStreamSynchronize(s));
+                c->failed = true;
                 return set_error(GSR_ERR_HIP, std::string("render: stream error ") + hipGetErrorString(q));
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(c->wait_timeout_ms)) {
+                c->failed = true;
+                return set_error(GSR_ERR_HIP, "render: timed out waiting for the frame's counts (stream not "
+                                              "progressing); the context is marked failed");
             }
         }
 #if defined(__x86_64__)
@@ -329,6 +353,15 @@ int wait_counts(gsr_context* c, hipStream_t s) {
 }  // namespace gsr
 
 using namespace gsr;
+
+namespace {
+// Test hook: one wave that keeps its stream busy for a bounded time (the
+// deadline of the host wait for a frame's counts is tested against it).
+__global__ void k_stall(uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+}  // namespace
 
 extern "C" {
 
@@ -428,6 +461,10 @@ int gsr_context_create(gsr_context** out) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 16 && v <= (1 << 20)) (*out)->chunk = (uint32_t)v;
     }
+    if (const char* e = std::getenv("GSR_WAIT_TIMEOUT_MS")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 1) (*out)->wait_timeout_ms = v;
+    }
     return GSR_OK;
 }
 
@@ -460,6 +497,7 @@ int gsr_context_stats(const gsr_context* c, gsr_frame_stats* out) {
 int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, float* out,
                      int32_t* radii, void* stream) {
     if (!c || !sc || !cam || !st || !out) return set_error(GSR_ERR_INVALID, "null argument");
+    if (c->failed) return set_error(GSR_ERR_HIP, "render: the context failed earlier (destroy it)");
     if (c->pend.active || c->pend.sort_ready)
         return set_error(GSR_ERR_INVALID, "render_begin: the previous frame was not finished");
     hipStream_t s = (hipStream_t)stream;
@@ -531,6 +569,7 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
     if (k < 1 || k > GSR_MAX_VIEWS) return set_error(GSR_ERR_INVALID, "render_begin_views: k out of range");
     for (int v = 0; v < k; ++v) {
         if (!ctxs[v] || !outs[v]) return set_error(GSR_ERR_INVALID, "null argument");
+        if (ctxs[v]->failed) return set_error(GSR_ERR_HIP, "render: a context failed earlier (destroy it)");
         if (ctxs[v]->pend.active || ctxs[v]->pend.sort_ready)
             return set_error(GSR_ERR_INVALID, "render_begin_views: a view's previous frame was not finished");
         if (ctxs[v]->prof_on) return set_error(GSR_ERR_INVALID, "render_begin_views: stage profiling is per view only");
@@ -875,6 +914,14 @@ int gsr_debug_host_times(const gsr_context* c, double ms_out[3], int64_t* frames
     if (!c || !ms_out) return set_error(GSR_ERR_INVALID, "null argument");
     for (int k = 0; k < 3; ++k) ms_out[k] = c->host_ms[k];
     if (frames_out) *frames_out = c->host_frames;
+    return GSR_OK;
+}
+
+int gsr_debug_stall(void* stream, uint32_t microseconds) {
+    if (microseconds > 5000000u) return set_error(GSR_ERR_INVALID, "debug_stall: at most 5 s");
+    const uint64_t ticks = (uint64_t)microseconds * 100u;  // s_memrealtime runs at 100 MHz
+    k_stall<<<1, 64, 0, (hipStream_t)stream>>>(ticks);
+    GSR_LAUNCH_CHECK("debug_stall");
     return GSR_OK;
 }
 

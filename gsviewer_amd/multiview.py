@@ -65,11 +65,12 @@ def view_of(rank: int, height: int, width: int) -> Camera:
     return view_for_rank(height, width, rank)
 
 
-def timed_region(step: Callable[[], None], steps: int, device) -> float:
+def timed_region(step: Callable[[], None], steps: int, device, local_out: Optional[list] = None) -> float:
     """Time exactly `steps` calls of `step`.
 
     The region is bracketed by a barrier and a device synchronize on both
-    sides.  Returns the MAX elapsed seconds over all ranks.
+    sides.  Returns the MAX elapsed seconds over all ranks (this rank's own
+    time is appended to `local_out` when given).
     """
     world = dist.get_world_size() if dist.is_initialized() else 1
     if world > 1:
@@ -82,6 +83,8 @@ def timed_region(step: Callable[[], None], steps: int, device) -> float:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if local_out is not None:
+        local_out.append(elapsed)
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)

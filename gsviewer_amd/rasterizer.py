@@ -13,6 +13,7 @@ Everything computes on the GPU through ``libgsr.so``; there is no fallback.
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import NamedTuple, Optional
 
 import numpy as np
@@ -32,6 +33,10 @@ def _stream_handle(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+def _sync_stream(stream=None):
+    (stream if stream is not None else torch.cuda.current_stream()).synchronize()
+
+
 def _dev_f32(t: torch.Tensor, name: str, shape_tail=None) -> torch.Tensor:
     if not isinstance(t, torch.Tensor):
         t = torch.as_tensor(np.asarray(t, np.float32))
@@ -49,7 +54,10 @@ class HipScene:
     def __init__(self, xyz, rot, scale, opacity, sh, stream=None):
         lib = _lib.load()
         n = int(xyz.shape[0])
-        sh = sh.reshape(n, -1) if isinstance(sh, torch.Tensor) else np.asarray(sh).reshape(n, -1)
+        if not isinstance(sh, torch.Tensor):
+            sh = np.asarray(sh)
+        sh_dim = int(np.prod(sh.shape[1:])) if sh.ndim > 1 else 1
+        sh = sh.reshape(n, sh_dim)
         self._keep = [_dev_f32(xyz, "xyz", (3,)), _dev_f32(rot, "rot", (4,)), _dev_f32(scale, "scale", (3,)),
                       _dev_f32(opacity, "opacity").reshape(n, 1), _dev_f32(sh, "sh")]
         self.n = n
@@ -58,7 +66,11 @@ class HipScene:
         _lib.check(lib.gsr_scene_create(*[ctypes.c_void_p(t.data_ptr()) for t in self._keep], n, self.sh_dim,
                                         _stream_handle(stream), ctypes.byref(h)), "gsr_scene_create")
         self._h = h
-        self._keep = None  # repack is stream-ordered; torch's caching allocator keeps the memory valid
+        # the repack is ordered on `stream`; scene creation is a load-time
+        # step, so wait for it here: the source tensors may then be freed and
+        # the scene used from any stream
+        _sync_stream(stream)
+        self._keep = None
 
     @classmethod
     def from_gaussian_data(cls, g, stream=None):
@@ -74,6 +86,7 @@ class HipScene:
         _lib.check(lib.gsr_scene_create_flat(ctypes.c_void_p(flat.data_ptr()), obj.n, obj.sh_dim,
                                              _stream_handle(stream), ctypes.byref(h)), "gsr_scene_create_flat")
         obj._h = h
+        _sync_stream(stream)
         obj._keep = None
         return obj
 
@@ -176,6 +189,8 @@ class RenderSettings:
         s.points_center[:] = [float(v) for v in self.points_center]
         s.bg[:] = [float(v) for v in self.bg]
         s.t_min = float(self.t_min)
+        if int(self.out_layout) not in (0, 1):
+            raise RuntimeError(f"out_layout must be 0 ([3,H,W]) or 1 ([H,W,3]), got {self.out_layout}")
         s.out_layout = int(self.out_layout)
         return s
 
@@ -333,16 +348,70 @@ class GaussianRasterizationSettings(NamedTuple):
 
 _FLIP = np.diag([-1.0, 1.0, -1.0, 1.0])
 
+# Host copies of the small per-camera tensors of the settings (viewmatrix,
+# projmatrix, campos, bg), keyed by tensor identity and version: the reference
+# builds them once per camera change (renderer_cuda.py:196-213) and then hands
+# the same tensor objects to a new GaussianRasterizer every frame (:226-228),
+# so after the first frame no device->host copy (a stream sync) remains.
+_host_cache = {}
+
+
+def _host_array(t) -> np.ndarray:
+    if not isinstance(t, torch.Tensor):
+        return np.asarray(t, np.float64)
+    key = id(t)
+    e = _host_cache.get(key)
+    if e is not None and e[0]() is t and e[1] == t._version:
+        return e[2]
+    a = np.array(t.detach().cpu().numpy(), np.float64)
+    _host_cache[key] = (weakref.ref(t, lambda _r, k=key: _host_cache.pop(k, None)), t._version, a)
+    return a
+
 
 def gl_matrices_from_settings(rs: GaussianRasterizationSettings):
     """Invert CUDARenderer's camera conversion (renderer_cuda.py:196-213):
     viewmatrix = V'^T, projmatrix = (P V')^T with V' = diag(-1,1,-1,1) V.
-    Returns the GL-convention (V, P) the OGL shaders use."""
-    Vp = np.asarray(rs.viewmatrix.detach().cpu().numpy(), np.float64).T
-    PVp = np.asarray(rs.projmatrix.detach().cpu().numpy(), np.float64).T
+    Returns the GL-convention (V, P) the OGL shaders use.  V is recovered
+    exactly (a sign flip and a transpose).  P = (P V') V'^-1 in float64, and
+    entries below 2^-20 of their row's largest magnitude (the rounding
+    residue of the float32 product P V' at P's structural zeros) are set to 0."""
+    Vp = _host_array(rs.viewmatrix).T
+    PVp = _host_array(rs.projmatrix).T
     V = _FLIP @ Vp
     P = PVp @ np.linalg.inv(Vp)
+    row_max = np.abs(P).max(axis=1, keepdims=True)
+    P[np.abs(P) < row_max * 2.0 ** -20] = 0.0
     return V.astype(np.float32), P.astype(np.float32)
+
+
+class _SceneCache:
+    """The device scene of the last rasterizer call per device, reused while
+    the five input tensors are the same objects at the same version.  The
+    reference constructs a new GaussianRasterizer per frame
+    (renderer_cuda.py:226-228), so the cache is per process, not per
+    instance: the repack then happens once per update_gaussian_data."""
+
+    def __init__(self):
+        self.entries = {}
+        self.creates = 0
+
+    def get(self, tensors, build):
+        dev = tensors[0].device
+        key = tuple((id(t), t._version, t.data_ptr(), tuple(t.shape)) for t in tensors)
+        e = self.entries.get(dev)
+        if e is not None and e[0] == key and all(r() is t for r, t in zip(e[1], tensors)):
+            return e[2]
+        self.entries.pop(dev, None)  # release the old scene before building the new one
+        scene = build()
+        self.creates += 1
+        self.entries[dev] = (key, [weakref.ref(t) for t in tensors], scene)
+        return scene
+
+    def clear(self):
+        self.entries.clear()
+
+
+scene_cache = _SceneCache()
 
 
 class GaussianRasterizer(torch.nn.Module):
@@ -352,20 +421,14 @@ class GaussianRasterizer(torch.nn.Module):
 
     Arithmetic is the reference OpenGL path's (SURVEY.md Appendix A);
     ``sh_degree`` caps the SH degree like render_mod does in gau_vert.glsl.
-    The static scene is repacked only when an input tensor changes."""
+    The static scene is repacked only when an input tensor changes
+    (``scene_cache``), and the camera tensors are copied to the host only
+    when they change, so a steady-state frame enqueues the render with no
+    host synchronisation."""
 
     def __init__(self, raster_settings: GaussianRasterizationSettings):
         super().__init__()
         self.raster_settings = raster_settings
-        self._scene = None
-        self._scene_key = None
-
-    def _scene_for(self, tensors):
-        key = tuple((t.data_ptr(), tuple(t.shape), t._version) for t in tensors)
-        if key != self._scene_key:
-            self._scene = HipScene(*tensors)
-            self._scene_key = key
-        return self._scene
 
     def forward(self, means3D, means2D=None, opacities=None, shs=None, colors_precomp=None, scales=None,
                 rotations=None, cov3D_precomp=None):
@@ -376,15 +439,15 @@ class GaussianRasterizer(torch.nn.Module):
             raise RuntimeError("means3D, opacities, shs, scales and rotations are required")
         rs = self.raster_settings
         n = means3D.shape[0]
-        scene = self._scene_for([means3D.contiguous(), rotations.contiguous(), scales.contiguous(),
-                                 opacities.contiguous(), shs.reshape(n, -1).contiguous()])
+        src = (means3D, rotations, scales, opacities, shs)
+        scene = scene_cache.get(src, lambda: HipScene(means3D, rotations, scales, opacities, shs.reshape(n, -1)))
         V, P = gl_matrices_from_settings(rs)
-        campos = rs.campos.detach().cpu().numpy()
+        campos = _host_array(rs.campos)
         H, W = int(rs.image_height), int(rs.image_width)
         focal = H / (2.0 * float(rs.tanfovy))
         cam = camera_struct(V, P, campos, [rs.tanfovx, rs.tanfovy, focal], W, H)
         st = RenderSettings(scale_modifier=rs.scale_modifier, render_mod=int(rs.sh_degree),
-                            bg=[float(v) for v in rs.bg.detach().cpu().numpy().reshape(3)], out_layout=0)
+                            bg=[float(v) for v in _host_array(rs.bg).reshape(3)], out_layout=0)
         color = torch.empty((3, H, W), dtype=torch.float32, device=means3D.device)
         radii = torch.empty((n,), dtype=torch.int32, device=means3D.device)
         render_into(_ctx_for_device(), scene, cam, st, color, radii)

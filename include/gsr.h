@@ -207,6 +207,12 @@ int gsr_context_stage_times(gsr_context* ctx, double* ms_out /* [GSR_NUM_STAGES]
  * [2] enqueue after it; *frames_out = number of frames. */
 int gsr_debug_host_times(const gsr_context* ctx, double ms_out[3], int64_t* frames_out);
 
+/* Test hook: keep `stream` busy for `microseconds` (<= 5 s) with one wave
+ * that sleeps until the time has passed (exercises the bounded host wait:
+ * GSR_WAIT_TIMEOUT_MS, default 2000, after which gsr_render_finish returns
+ * GSR_ERR_HIP and the context is marked failed). */
+int gsr_debug_stall(void* stream, uint32_t microseconds);
+
 /* Test hook: copy an internal array of the last gsr_render on `ctx` into
  * dst_dev (device memory, at most max_bytes). Returns the number of bytes
  * copied (>= 0) or a negative gsr_status.  what:

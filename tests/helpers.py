@@ -60,24 +60,78 @@ def gpu_frame(g, cam, settings, with_debug=False, radii=False):
     if radii:
         res["radii"] = rad.cpu().numpy()
     if with_debug:
-        lib = _lib.load()
-        st = res["stats"]
-        nv, nd, nt = st["n_visible"], st["n_instances"], st["tiles_x"] * st["tiles_y"]
-
-        def grab(what, nbytes, dtype):
-            buf = torch.empty(max(nbytes, 4) // 4 + 1, dtype=torch.int32, device="cuda")
-            got = lib.gsr_debug_copy(ctx.handle, what, ctypes.c_void_p(buf.data_ptr()), nbytes, None)
-            assert got >= 0, lib.gsr_last_error()
-            torch.cuda.synchronize()
-            return buf.cpu().numpy().view(np.uint8)[:got].view(dtype)
-
-        res["records"] = grab(_lib.GSR_DEBUG_RECORDS, nv * 48, np.uint8).reshape(nv, 48)
-        res["depth_order"] = grab(_lib.GSR_DEBUG_DEPTH_ORDER, nv * 4, np.uint32)
-        res["ranges"] = grab(_lib.GSR_DEBUG_TILE_RANGES, nt * 8, np.uint32).reshape(nt, 2)
-        res["tile_list"] = grab(_lib.GSR_DEBUG_TILE_LIST, nd * 4, np.uint32)
+        res.update(grab_debug(ctx, res["stats"]))
     scene.close()
     ctx.close()
     return res
+
+
+def grab_debug(ctx, st):
+    """The last frame's internal arrays of a context (gsr_debug_copy)."""
+    import ctypes
+
+    import torch
+
+    from gsviewer_amd import _lib
+    lib = _lib.load()
+    nv, nd, nt = st["n_visible"], st["n_instances"], st["tiles_x"] * st["tiles_y"]
+
+    def grab(what, nbytes, dtype):
+        buf = torch.empty(max(nbytes, 4) // 4 + 1, dtype=torch.int32, device="cuda")
+        got = lib.gsr_debug_copy(ctx.handle, what, ctypes.c_void_p(buf.data_ptr()), nbytes, None)
+        assert got >= 0, lib.gsr_last_error()
+        torch.cuda.synchronize()
+        return buf.cpu().numpy().view(np.uint8)[:got].view(dtype)
+
+    return dict(records=grab(_lib.GSR_DEBUG_RECORDS, nv * 48, np.uint8).reshape(nv, 48),
+                depth_order=grab(_lib.GSR_DEBUG_DEPTH_ORDER, nv * 4, np.uint32),
+                ranges=grab(_lib.GSR_DEBUG_TILE_RANGES, nt * 8, np.uint32).reshape(nt, 2),
+                tile_list=grab(_lib.GSR_DEBUG_TILE_LIST, nd * 4, np.uint32))
+
+
+def batched_frames(scene, cams, settings, group=4, debug_views=()):
+    """Render len(cams) views through the path bench.py times:
+    ViewBatchPipeline (shared cull + preprocess per group, batched depth
+    sorts, batched finish), one stream per group, planar [3,H,W] outputs.
+    Returns per view: image [H,W,3] (numpy), stats, and the debug arrays for
+    the views listed in debug_views."""
+    import torch
+
+    from gsviewer_amd.multiview import ViewBatchPipeline
+    from gsviewer_amd.rasterizer import HipContext, camera_from
+    assert len(cams) % group == 0
+    settings.out_layout = 0
+    ctxs = [HipContext() for _ in cams]
+    outs = [torch.full((3, c.h, c.w), -1.0, dtype=torch.float32, device="cuda") for c in cams]
+    streams = [torch.cuda.Stream() for _ in range(len(cams) // group)]
+    camcs = [camera_from(c) for c in cams]
+    groups = [(ctxs[i:i + group], camcs[i:i + group], outs[i:i + group], streams[i // group])
+              for i in range(0, len(cams), group)]
+    pipe = ViewBatchPipeline(groups, scene, settings)
+    for _ in groups:
+        pipe.step()
+    pipe.drain()
+    torch.cuda.synchronize()
+    res = []
+    for v, (ctx, out) in enumerate(zip(ctxs, outs)):
+        r = {"image": out.permute(1, 2, 0).contiguous().cpu().numpy(), "stats": ctx.stats()}
+        if v in debug_views:
+            r.update(grab_debug(ctx, r["stats"]))
+        res.append(r)
+    for c in ctxs:
+        c.close()
+    return res
+
+
+def error_census(gpu, ref, tol):
+    """Count and locate the channels whose |GPU - oracle| exceeds `tol`."""
+    d = np.abs(gpu.astype(np.float64) - ref.astype(np.float64))
+    bad = d > tol
+    ys, xs, _ = np.nonzero(bad)
+    return dict(max=float(d.max()), mean=float(d.mean()), n_over=int(bad.sum()), channels=int(d.size),
+                frac_over=float(bad.mean()), pixels_over=int(bad.any(axis=2).sum()),
+                over_gt_1e3=int((d > 1e-3).sum()), over_gt_4e3=int((d > 4e-3).sum()),
+                rows=(int(ys.min()), int(ys.max())) if len(ys) else None)
 
 
 def decode_records(raw):

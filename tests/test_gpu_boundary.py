@@ -1,0 +1,327 @@
+"""GPU tests of the reference-facing boundary, driven the way the reference
+drives it (not only through the C ABI):
+
+* ``GaussianRasterizer`` built exactly as ``CUDARenderer`` builds its settings
+  (``renderer_cuda.py:104-120`` init, ``:147-150`` update_gaussian_data,
+  ``:196-213`` update_camera_pose / update_camera_intrin) and called as in
+  ``CUDARenderer.draw`` (``:226-243``): a NEW rasterizer per frame, shs as
+  [N, K, 3], planar color[3,H,W] and radii[N] out;
+* ``HIPRenderer`` through the OpenGLRenderer setter sequence of
+  ``main.py:128-137`` (update_activated_renderer_state) and the appearance
+  setters (``renderer_ogl.py:246-318``);
+* ``HipScene.from_flat`` (the flat() SSBO-0 layout, ``renderer_ogl.py:238``,
+  ``util_gau.py:40-42``) and the planar output layout.
+The oracle is the C restatement of the OGL path (oracle/gl_oracle.c)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from gsviewer_amd.camera import Camera
+from gsviewer_amd.gaussian_data import garden_standin, random_scene
+from oracle import c_oracle as C
+from oracle import gl_oracle as O
+from helpers import TOL_TMIN, compare_images, uniforms_for
+
+pytestmark = pytest.mark.gpu
+
+
+def _cuda_renderer_settings(camera, sh_dim, w, h):
+    """CUDARenderer.raster_settings after __init__ (:106-119),
+    update_gaussian_data (:150), update_camera_pose (:196-203) and
+    update_camera_intrin (:205-213), restated line by line."""
+    rs = {"image_height": int(h), "image_width": int(w), "tanfovx": 1, "tanfovy": 1,
+          "bg": torch.Tensor([0., 0., 0]).float().cuda(), "scale_modifier": 1., "viewmatrix": None,
+          "projmatrix": None, "sh_degree": 3, "campos": None, "prefiltered": False, "debug": False}
+    rs["sh_degree"] = int(np.round(np.sqrt(sh_dim))) - 1
+    view_matrix = camera.get_view_matrix()
+    view_matrix[[0, 2], :] = -view_matrix[[0, 2], :]
+    proj = camera.get_project_matrix() @ view_matrix
+    rs["viewmatrix"] = torch.tensor(view_matrix.T).float().cuda()
+    rs["campos"] = torch.tensor(camera.position).float().cuda()
+    rs["projmatrix"] = torch.tensor(proj.T).float().cuda()
+    view_matrix = camera.get_view_matrix()
+    view_matrix[[0, 2], :] = -view_matrix[[0, 2], :]
+    proj = camera.get_project_matrix() @ view_matrix
+    rs["projmatrix"] = torch.tensor(proj.T).float().cuda()
+    hfovx, hfovy, focal = camera.get_htanfovxy_focal()
+    rs["tanfovx"] = hfovx
+    rs["tanfovy"] = hfovy
+    return rs
+
+
+def _gaus_cuda(g):
+    """gaus_cuda_from_cpu (renderer_cuda.py:92-101): sh reshaped to [N, K, 3]."""
+    t = {f: torch.tensor(getattr(g, f)).float().cuda() for f in ("xyz", "rot", "scale", "opacity", "sh")}
+    t["sh"] = t["sh"].reshape(len(g), -1, 3).contiguous()
+    return t
+
+
+def _draw(rs, gc):
+    """CUDARenderer.draw's rasterizer call (renderer_cuda.py:226-243)."""
+    from gsviewer_amd.rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+    raster_settings = GaussianRasterizationSettings(**rs)
+    rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+    with torch.no_grad():
+        img, radii = rasterizer(means3D=gc["xyz"], means2D=None, shs=gc["sh"], colors_precomp=None,
+                                opacities=gc["opacity"], scales=gc["scale"], rotations=gc["rot"],
+                                cov3D_precomp=None)
+    return img, radii
+
+
+def _oracle(g, U, threads=8):
+    return C.render(g.flat(), g.sh_dim, U, threads=threads)
+
+
+def test_rasterizer_called_like_cuda_renderer(gpu):
+    from gsviewer_amd.rasterizer import gl_matrices_from_settings, scene_cache
+    g = random_scene(20_000, sh_degree=3, seed=21)
+    W, H = 320, 240
+    gc = _gaus_cuda(g)
+    scene_cache.clear()
+    creates0 = scene_cache.creates
+    for yaw in (0.0, 35.0, -70.0):
+        cam = Camera(H, W).yaw(yaw)
+        rs = _cuda_renderer_settings(cam, g.sh.shape[1] // 3, W, H)
+        for _ in range(2):   # a new rasterizer per frame, like draw()
+            img, radii = _draw(rs, gc)
+        torch.cuda.synchronize()
+        assert tuple(img.shape) == (3, H, W) and img.dtype == torch.float32
+        assert tuple(radii.shape) == (len(g),) and radii.dtype == torch.int32
+        # V comes back exactly; P to within the float32 rounding of the product
+        # P V' the reference hands over (its [2,3] entry, -0.002, is recovered from
+        # -5.002 and keeps ~2.4e-7 absolute error: it only moves the z_ndc clip)
+        from gsviewer_amd.rasterizer import GaussianRasterizationSettings
+        V, P = gl_matrices_from_settings(GaussianRasterizationSettings(**rs))
+        np.testing.assert_array_equal(V, cam.get_view_matrix())
+        np.testing.assert_allclose(P, cam.get_project_matrix(), rtol=0, atol=1e-6)
+        P0 = cam.get_project_matrix()
+        np.testing.assert_array_equal(P[:2], P0[:2])          # x/y rows: exact
+        np.testing.assert_array_equal(P[3], P0[3])
+        # image and radii against the oracle given the matrices the GPU received
+        U = O.default_uniforms(V, P, np.asarray([rs["tanfovx"], rs["tanfovy"], H / (2.0 * rs["tanfovy"])],
+                                                np.float32), cam.position, W, H)
+        ref = _oracle(g, U)
+        compare_images(img.permute(1, 2, 0).cpu().numpy(), ref, tol=TOL_TMIN + 2e-5)
+        vs = O.vertex_stage(g.flat(), g.sh_dim, U)
+        np.testing.assert_array_equal(radii.cpu().numpy(), O.radii(vs))
+        # and against the oracle on the camera's own matrices (the OGL uniforms)
+        compare_images(img.permute(1, 2, 0).cpu().numpy(), _oracle(g, uniforms_for(cam)), tol=TOL_TMIN + 2e-5)
+    # one scene repack for all frames and cameras (renderer_cuda.py:147-150 happens once)
+    assert scene_cache.creates - creates0 == 1
+    # update_gaussian_data with new tensors -> a new scene
+    gc2 = _gaus_cuda(g)
+    _draw(rs, gc2)
+    assert scene_cache.creates - creates0 == 2
+    # in-place edit of a tensor (version bump) -> a new scene, and the image follows it
+    gc2["opacity"].mul_(0.0)
+    img, _ = _draw(rs, gc2)
+    assert scene_cache.creates - creates0 == 3
+    assert float(img.abs().max()) == 0.0
+    scene_cache.clear()
+
+
+def test_rasterizer_sh_degree_caps_like_render_mod(gpu):
+    g = random_scene(5000, sh_degree=3, seed=22)
+    W, H = 200, 150
+    gc = _gaus_cuda(g)
+    cam = Camera(H, W).yaw(15)
+    rs = _cuda_renderer_settings(cam, 16, W, H)
+    for deg in (0, 1, 2):
+        rs["sh_degree"] = deg
+        img, _ = _draw(rs, gc)
+        ref = _oracle(g, uniforms_for(cam, render_mod=deg))
+        compare_images(img.permute(1, 2, 0).cpu().numpy(), ref, tol=TOL_TMIN + 2e-5)
+
+
+def test_hip_renderer_setter_sequence(gpu):
+    """main.py:128-137 then appearance/box setters, each draw vs the oracle."""
+    from gsviewer_amd.renderer import HIPRenderer
+    from gsviewer_amd.rasterizer import RenderSettings
+    g = garden_standin(30_000, seed=4, sh_degree=3)
+    W, H = 256, 192
+    cam = Camera(H, W)
+    r = HIPRenderer(W, H, cam)
+    # update_activated_renderer_state (main.py:128-137), start-up values (main.py:66-75)
+    r.update_gaussian_data(g)
+    r.sort_and_update()
+    r.set_scale_modifier(1.0)
+    r.set_screen_scale_factor(1.0)
+    r.set_rot_modifier([0.0, 0.0, 0.0])
+    r.set_render_mod(9 - 3)
+    r.update_camera_pose()
+    r.update_camera_intrin()
+    r.set_render_reso(cam.w, cam.h)
+    st = RenderSettings()
+
+    def check():
+        img = r.draw()
+        torch.cuda.synchronize()
+        assert tuple(img.shape) == (H, W, 3)
+        ref = _oracle(g, uniforms_for(cam, st))
+        return compare_images(img.cpu().numpy(), ref, tol=TOL_TMIN + 2e-5)
+
+    check()
+    # reduce_updates: an unchanged state returns the same frame object
+    assert r.draw() is r.draw()
+    r.set_render_mod(1); st.render_mod = 1
+    check()
+    r.adjust_dc_features(0.7); st.dc_factor = 0.7
+    r.adjust_extra_features(1.6); st.extra_factor = 1.6
+    r.update_color_factor([1.0, 0.5, 0.8]); st.color_scale = [1.0, 0.5, 0.8]
+    r.set_render_mod(3); st.render_mod = 3
+    check()
+    r.set_scale_modifier(1.7); st.scale_modifier = 1.7
+    r.set_light_rotation([10.0, 40.0, 0.0]); st.light_rotation = [10.0, 40.0, 0.0]
+    r.set_rot_modifier([20.0, 0.0, 5.0]); st.set_rot_modifier_euler([20.0, 0.0, 5.0])
+    check()
+    pc = [float(v) for v in g.points_center]
+    r.set_points_center(pc); st.points_center = pc
+    r.set_enable_obb(1); st.enable_obb = 1
+    r.set_cube_rotation([30.0, 15.0, 0.0]); st.set_cube_rotation_euler([30.0, 15.0, 0.0])
+    r.set_point_cubeMin([-1.0, -1.0, -1.0]); st.cube_min = [-1.0, -1.0, -1.0]
+    r.set_point_cubeMax([1.0, 1.0, 1.0]); st.cube_max = [1.0, 1.0, 1.0]
+    check()
+    # camera move -> rerender
+    cam.yaw(30.0)
+    r.update_camera_pose()
+    check()
+    # the depth-order service matches the reference sort
+    order = r.depth_order().cpu().numpy().reshape(-1)
+    V = cam.get_view_matrix()
+    F = np.float32
+    vz = ((F(V[2, 0]) * g.xyz[:, 0] + F(V[2, 1]) * g.xyz[:, 1]) + F(V[2, 2]) * g.xyz[:, 2]) + F(V[2, 3])
+    np.testing.assert_array_equal(order, np.argsort(vz, kind="stable"))
+
+
+def test_scene_from_flat_matches_fields(gpu):
+    from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into
+    g = random_scene(8000, sh_degree=2, seed=23)
+    cam = Camera(144, 176).yaw(-20)
+    st = RenderSettings(t_min=0.0, out_layout=1)
+    outs = []
+    for scene in (HipScene.from_gaussian_data(g), HipScene.from_flat(torch.from_numpy(g.flat()).cuda(), g.sh_dim)):
+        ctx = HipContext()
+        out = torch.empty((cam.h, cam.w, 3), dtype=torch.float32, device="cuda")
+        render_into(ctx, scene, camera_from(cam), st, out)
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy())
+        ctx.close()
+        scene.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
+    compare_images(outs[1], _oracle(g, uniforms_for(cam, st)))
+
+
+@pytest.mark.parametrize("chunk", [None, "16"])
+def test_planar_layout_equals_interleaved(gpu, monkeypatch, chunk):
+    """out_layout 0 ([3,H,W], the rasterizer's) vs 1 ([H,W,3]): the single-chunk
+    write path and, with GSR_CHUNK=16, the multi-chunk merge path."""
+    from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into
+    if chunk:
+        monkeypatch.setenv("GSR_CHUNK", chunk)
+    g = garden_standin(40_000, seed=5, sh_degree=1)
+    cam = Camera(180, 320).yaw(10)
+    scene = HipScene.from_gaussian_data(g)
+    ctx = HipContext()
+    imgs = {}
+    for layout in (0, 1):
+        st = RenderSettings(t_min=1e-4, out_layout=layout)
+        shape = (3, cam.h, cam.w) if layout == 0 else (cam.h, cam.w, 3)
+        out = torch.full(shape, -1.0, dtype=torch.float32, device="cuda")
+        render_into(ctx, scene, camera_from(cam), st, out)
+        torch.cuda.synchronize()
+        imgs[layout] = out.cpu().numpy()
+    np.testing.assert_array_equal(imgs[0].transpose(1, 2, 0), imgs[1])
+    compare_images(imgs[1], _oracle(g, uniforms_for(cam)), tol=TOL_TMIN + 2e-5)
+    scene.close()
+    ctx.close()
+
+
+def test_bad_arguments_raise(gpu):
+    from gsviewer_amd import _lib
+    from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into
+    g = random_scene(100, sh_degree=0, seed=1)
+    scene = HipScene.from_gaussian_data(g)
+    ctx = HipContext()
+    cam = Camera(32, 32)
+    out = torch.empty((3, 32, 32), dtype=torch.float32, device="cuda")
+    with pytest.raises(RuntimeError, match="out_layout"):
+        render_into(ctx, scene, camera_from(cam), RenderSettings(out_layout=2), out)
+    lib = _lib.load()
+    st = RenderSettings().to_c()
+    st.out_layout = 7
+    rc = lib.gsr_render(ctx.handle, scene.handle, ctypes.byref(camera_from(cam)), ctypes.byref(st),
+                        ctypes.c_void_p(out.data_ptr()), None, None)
+    assert rc == _lib.GSR_ERR_INVALID and b"out_layout" in lib.gsr_last_error()
+    st = RenderSettings().to_c()
+    st.t_min = 1.5
+    rc = lib.gsr_render(ctx.handle, scene.handle, ctypes.byref(camera_from(cam)), ctypes.byref(st),
+                        ctypes.c_void_p(out.data_ptr()), None, None)
+    assert rc == _lib.GSR_ERR_INVALID
+    # the context still renders after rejected calls
+    render_into(ctx, scene, camera_from(cam), RenderSettings(out_layout=0), out)
+    torch.cuda.synchronize()
+    scene.close()
+    ctx.close()
+
+
+def test_context_regrowth_sequence(gpu):
+    """One context through empty -> small -> large -> small -> larger scenes and
+    frame sizes (buffers grow without freeing in-flight memory): every frame
+    equals a fresh context's frame."""
+    from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into
+    cases = [(0, 64, 48), (500, 64, 48), (200_000, 640, 360), (300, 32, 32), (400_000, 1280, 720)]
+    shared = HipContext()
+    for n, w, h in cases:
+        g = random_scene(max(n, 1), sh_degree=1, seed=n % 97)[:n] if n else random_scene(1, sh_degree=1)[:0]
+        scene = HipScene.from_gaussian_data(g)
+        cam = Camera(h, w).yaw(7.0)
+        st = RenderSettings(out_layout=1)
+        imgs = []
+        for ctx in (shared, HipContext()):
+            out = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
+            render_into(ctx, scene, camera_from(cam), st, out)
+            torch.cuda.synchronize()
+            imgs.append(out.cpu().numpy())
+            assert ctx.stats()["n_gaussians"] == n
+        np.testing.assert_array_equal(imgs[0], imgs[1])
+        if n == 0:
+            assert float(np.abs(imgs[0]).max()) == 0.0
+        scene.close()
+    shared.close()
+
+
+def test_wait_for_counts_has_a_deadline(gpu, monkeypatch):
+    """A stream that makes no progress fails gsr_render_finish with
+    GSR_ERR_HIP after GSR_WAIT_TIMEOUT_MS instead of hanging the host; the
+    context then refuses new frames."""
+    import time
+    from gsviewer_amd import _lib
+    from gsviewer_amd.rasterizer import (HipContext, HipScene, RenderSettings, _stream_handle, camera_from,
+                                         render_begin, render_finish, render_into)
+    monkeypatch.setenv("GSR_WAIT_TIMEOUT_MS", "300")
+    g = random_scene(1000, sh_degree=0, seed=3)
+    scene = HipScene.from_gaussian_data(g)
+    ctx = HipContext()
+    cam = Camera(48, 64)
+    out = torch.empty((3, 48, 64), dtype=torch.float32, device="cuda")
+    st = RenderSettings(out_layout=0)
+    s = torch.cuda.Stream()
+    lib = _lib.load()
+    _lib.check(lib.gsr_debug_stall(_stream_handle(s), 1_500_000), "debug_stall")  # 1.5 s of a busy stream
+    render_begin(ctx, scene, camera_from(cam), st, out, stream=s)
+    t0 = time.perf_counter()
+    with pytest.raises(RuntimeError, match="timed out"):
+        render_finish(ctx, s)
+    assert 0.25 < time.perf_counter() - t0 < 1.4
+    s.synchronize()
+    with pytest.raises(RuntimeError, match="failed earlier"):
+        render_begin(ctx, scene, camera_from(cam), st, out, stream=s)
+    ctx.close()
+    # a new context works
+    ctx2 = HipContext()
+    render_into(ctx2, scene, camera_from(cam), st, out)
+    torch.cuda.synchronize()
+    ctx2.close()
+    scene.close()
