@@ -213,7 +213,12 @@ struct ZeroLayout {
     }
 };
 
-int ensure_scene_buffers(gsr_context* c, size_t n) {
+// The completion counter is zeroed on the frame's own stream: a plain
+// hipMemset runs on the null stream, which does not order against the
+// non-blocking streams frames are issued on (torch's), so the first
+// preprocess could count on top of a memset still in flight and never
+// publish its (V, D, seq).
+int ensure_scene_buffers(gsr_context* c, size_t n, hipStream_t s) {
     const size_t nw = (n + 63) / 64 + 4;
     int rc;
     if ((rc = c->vis_mask.ensure(nw, "vis_mask"))) return rc;
@@ -234,7 +239,7 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
     if ((rc = c->radix_tmp.ensure(radix_tmp_elems(n), "radix_tmp"))) return rc;
     if (!c->done_ctr.p) {
         if ((rc = c->done_ctr.ensure(1, "done_ctr"))) return rc;
-        GSR_HIP_CHECK(hipMemset(c->done_ctr.p, 0, c->done_ctr.cap * sizeof(unsigned long long)));
+        GSR_HIP_CHECK(hipMemsetAsync(c->done_ctr.p, 0, c->done_ctr.cap * sizeof(unsigned long long), s));
     }
     if (!c->host_counters) {
         if (hipHostMalloc(&c->host_counters, 4 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
@@ -507,7 +512,7 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
     if (rc) return rc;
     const size_t n = (size_t)sc->d.n;
     const int num_tiles = u.tiles_x * u.tiles_y;
-    if ((rc = ensure_scene_buffers(c, n))) return rc;
+    if ((rc = ensure_scene_buffers(c, n, s))) return rc;
     const ZeroLayout zl(num_tiles);
     if ((rc = c->zero.ensure(zl.total, "zero block"))) return rc;
     uint32_t* counters = c->zero.p + zl.counters;
@@ -587,7 +592,7 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
         const auto h0 = std::chrono::steady_clock::now();
         if ((rc = build_uniforms(sc, &cams[v], st, u[v]))) return rc;
         const int num_tiles = u[v].tiles_x * u[v].tiles_y;
-        if ((rc = ensure_scene_buffers(c, n))) return rc;
+        if ((rc = ensure_scene_buffers(c, n, s))) return rc;
         const ZeroLayout zl(num_tiles);
         if ((rc = c->zero.ensure(zl.total, "zero block"))) return rc;
         uint32_t* counters = c->zero.p + zl.counters;
@@ -948,7 +953,7 @@ int gsr_debug_sort_pairs(gsr_context* c, const uint32_t* keys_dev, int64_t n, in
     hipStream_t s = (hipStream_t)stream;
     if (n == 0) return GSR_OK;
     const size_t un = (size_t)n;
-    int rc = ensure_scene_buffers(c, un);
+    int rc = ensure_scene_buffers(c, un, s);
     if (rc) return rc;
     if ((rc = c->zero.ensure(ZeroLayout(0).total, "zero block"))) return rc;
     GSR_HIP_CHECK(hipMemcpyAsync(c->keys_a.p, keys_dev, un * 4, hipMemcpyDeviceToDevice, s));
@@ -966,7 +971,7 @@ int gsr_sort_depth(gsr_context* c, const gsr_scene* sc, const float view[16], in
     hipStream_t s = (hipStream_t)stream;
     const size_t n = (size_t)sc->d.n;
     if (n == 0) return GSR_OK;
-    int rc = ensure_scene_buffers(c, n);
+    int rc = ensure_scene_buffers(c, n, s);
     if (rc) return rc;
     if ((rc = c->zero.ensure(ZeroLayout(0).total, "zero block"))) return rc;
     GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * ZeroLayout(0).total, s));
