@@ -45,6 +45,7 @@ template <typename T>
 struct DevBuf {
     T* p = nullptr;
     size_t cap = 0;  // elements
+    int64_t allocs = 0;  // allocations made (gsr_context_workspace)
     std::vector<void*> retired;
     int ensure(size_t n, const char* what) {
         if (n <= cap && p) return GSR_OK;
@@ -55,8 +56,10 @@ struct DevBuf {
         if (p) retired.push_back(p);
         p = q;
         cap = want;
+        ++allocs;
         return GSR_OK;
     }
+    size_t bytes() const { return cap * sizeof(T); }
     void release() {
         if (p) (void)hipFree(p);
         for (void* r : retired) (void)hipFree(r);
@@ -132,6 +135,20 @@ struct gsr_context {
     bool failed = false;           // a wait timed out or the stream faulted: no further frames
     int64_t wait_timeout_ms = 2000;
 };
+
+namespace gsr {
+namespace {
+// Every device buffer of a context (workspace accounting and release).
+template <typename F>
+void each_buf(gsr_context* c, F&& f) {
+    f(c->vis_mask); f(c->wave_counts); f(c->block_ranges); f(c->scan_tmp); f(c->recs);
+    f(c->keys_a); f(c->keys_b); f(c->vals_a); f(c->vals_b); f(c->trect); f(c->trect_sorted);
+    f(c->rect4_a); f(c->rect4_b); f(c->bin_tmp); f(c->tkeys_a); f(c->tkeys_b); f(c->tvals_a); f(c->tvals_b);
+    f(c->radix_tmp); f(c->zero); f(c->chunk_cnt); f(c->chunk_base); f(c->chunk_desc); f(c->chunk_order);
+    f(c->partial); f(c->tmax); f(c->done_ctr);
+}
+}  // namespace
+}  // namespace gsr
 
 namespace gsr {
 namespace {
@@ -476,15 +493,7 @@ int gsr_context_create(gsr_context** out) {
 int gsr_context_destroy(gsr_context* c) {
     if (!c) return GSR_OK;
     (void)hipDeviceSynchronize();
-    c->vis_mask.release(); c->wave_counts.release(); c->scan_tmp.release(); c->recs.release();
-    c->block_ranges.release();
-    c->keys_a.release(); c->keys_b.release(); c->vals_a.release(); c->vals_b.release();
-    c->trect.release(); c->trect_sorted.release(); c->rect4_a.release(); c->rect4_b.release(); c->bin_tmp.release(); c->tkeys_a.release(); c->tkeys_b.release(); c->tvals_a.release();
-    c->tvals_b.release(); c->radix_tmp.release(); c->zero.release();
-    c->chunk_cnt.release(); c->chunk_base.release();
-    c->chunk_desc.release(); c->chunk_order.release(); c->partial.release();
-    c->tmax.release();
-    c->done_ctr.release();
+    each_buf(c, [](auto& b) { b.release(); });
     if (c->host_counters) (void)hipHostFree(c->host_counters);
     for (auto& row : c->ev)
         for (auto& e : row)
@@ -497,6 +506,46 @@ int gsr_context_stats(const gsr_context* c, gsr_frame_stats* out) {
     if (!c || !out) return set_error(GSR_ERR_INVALID, "null argument");
     *out = c->stats;
     return GSR_OK;
+}
+
+int gsr_context_reserve(gsr_context* c, int64_t n, int32_t width, int32_t height, int64_t max_instances,
+                        void* stream) {
+    if (!c) return set_error(GSR_ERR_INVALID, "null argument");
+    if (n < 0 || width <= 0 || height <= 0 || width > 32768 || height > 32768)
+        return set_error(GSR_ERR_INVALID, "context_reserve: n >= 0 and 1..32768 pixels per side");
+    if (c->pend.active || c->pend.sort_ready)
+        return set_error(GSR_ERR_INVALID, "context_reserve: a frame is in flight on this context");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t un = (size_t)n;
+    const size_t d = max_instances > 0 ? (size_t)max_instances : 4 * un;
+    const int num_tiles = ((width + kTile - 1) / kTile) * ((height + kTile - 1) / kTile);
+    int rc;
+    if ((rc = ensure_scene_buffers(c, un, s))) return rc;
+    if ((rc = c->zero.ensure(ZeroLayout(num_tiles).total, "zero block"))) return rc;
+    if ((rc = c->tkeys_a.ensure(d, "tile_keys"))) return rc;
+    if ((rc = c->tkeys_b.ensure(d, "tile_keys"))) return rc;
+    if ((rc = c->tvals_a.ensure(d, "tile_vals"))) return rc;
+    if ((rc = c->tvals_b.ensure(d, "tile_vals"))) return rc;
+    if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(d), radix_tmp_elems(un)), "radix_tmp"))) return rc;
+    const size_t mc = (size_t)num_tiles + d / c->chunk + 1;
+    if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
+    if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
+    if ((rc = c->chunk_desc.ensure(mc, "chunk_desc"))) return rc;
+    if ((rc = c->chunk_order.ensure(mc, "chunk_order"))) return rc;
+    if ((rc = c->partial.ensure(mc * 256, "partial"))) return rc;
+    if ((rc = c->tmax.ensure(mc, "tmax"))) return rc;
+    return GSR_OK;
+}
+
+int64_t gsr_context_workspace(gsr_context* c, int64_t* n_allocations) {
+    if (!c) return set_error(GSR_ERR_INVALID, "null argument");
+    int64_t bytes = 0, allocs = 0;
+    each_buf(c, [&](auto& b) {
+        bytes += (int64_t)b.bytes();
+        allocs += b.allocs;
+    });
+    if (n_allocations) *n_allocations = allocs;
+    return bytes;
 }
 
 int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, float* out,

@@ -121,6 +121,21 @@ class HipContext:
     def handle(self):
         return self._h
 
+    def reserve(self, n: int, width: int, height: int, max_instances: int = 0, stream=None):
+        """gsr_context_reserve: size the workspace for scenes of <= n Gaussians
+        and frames of <= width x height (<= max_instances tile instances, 0 =
+        4 n), so that such frames never allocate."""
+        _lib.check(_lib.load().gsr_context_reserve(self._h, int(n), int(width), int(height), int(max_instances),
+                                                   _stream_handle(stream)), "gsr_context_reserve")
+
+    def workspace(self):
+        """(device bytes held, device allocations made so far)."""
+        allocs = ctypes.c_int64()
+        b = _lib.load().gsr_context_workspace(self._h, ctypes.byref(allocs))
+        if b < 0:
+            _lib.check(int(b), "gsr_context_workspace")
+        return int(b), int(allocs.value)
+
     def stats(self) -> dict:
         st = _lib.GsrFrameStats()
         _lib.check(_lib.load().gsr_context_stats(self._h, ctypes.byref(st)), "gsr_context_stats")

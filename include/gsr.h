@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 4
+#define GSR_ABI_VERSION 5
 
 typedef enum gsr_status {
     GSR_OK = 0,
@@ -119,9 +119,22 @@ int gsr_scene_destroy(gsr_scene* scene);
 int64_t gsr_scene_count(const gsr_scene* scene);
 int32_t gsr_scene_sh_dim(const gsr_scene* scene);
 
-/* Frame workspace. Device buffers grow on demand and are reused. */
+/* Frame workspace. Device buffers grow on demand and are reused; growth
+ * never frees (hipFree would synchronise the device): the old blocks are
+ * released with the context. */
 int gsr_context_create(gsr_context** out);
 int gsr_context_destroy(gsr_context* ctx);
+/* Size every workspace buffer up front for scenes of up to n Gaussians, frames
+ * of up to width x height and up to max_instances (splat, tile) instances per
+ * frame (<= 0: 4 n), so that frames within those bounds allocate nothing.
+ * The reference sizes its GL buffers once per scene in update_gaussian_data
+ * (renderer_ogl.py:235-242) and CUDARenderer keeps its tensors resident
+ * (renderer_cuda.py:147-150). */
+int gsr_context_reserve(gsr_context* ctx, int64_t n, int32_t width, int32_t height, int64_t max_instances,
+                        void* stream);
+/* Device bytes the context holds now (retired blocks excluded), or < 0 on
+ * error; *n_allocations (nullable) = device allocations made so far. */
+int64_t gsr_context_workspace(gsr_context* ctx, int64_t* n_allocations);
 
 /* Render one frame: cull + project + SH (preprocess), depth radix sort,
  * tile binning + stable tile sort, 16x16-tile front-to-back compositing.

@@ -38,7 +38,8 @@ def lib():
         _lib.oracle_render.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(_U),
                                        ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32]
         _lib.oracle_sort_depth.restype = ctypes.c_int64
-        _lib.oracle_sort_depth.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+        _lib.oracle_sort_depth.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int32]
     return _lib
 
 
@@ -79,9 +80,11 @@ def render(flat, sh_dim, U, mode="float", threads=0, return_order=False):
     return img
 
 
-def sort_depth(xyz, view):
+def sort_depth(xyz, view, threads=0):
+    """renderer_ogl.py:16-26 _sort_gaussian_cpu: ascending view z, ties by id."""
     xyz = np.ascontiguousarray(xyz, F)
     v = np.ascontiguousarray(view, F).reshape(16)
     out = np.empty(len(xyz), np.int32)
-    lib().oracle_sort_depth(xyz.ctypes.data, len(xyz), v.ctypes.data, out.ctypes.data)
+    if lib().oracle_sort_depth(xyz.ctypes.data, len(xyz), v.ctypes.data, out.ctypes.data, int(threads)) < 0:
+        raise MemoryError("oracle_sort_depth")
     return out

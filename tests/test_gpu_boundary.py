@@ -292,6 +292,51 @@ def test_context_regrowth_sequence(gpu):
     shared.close()
 
 
+def test_context_reserve_means_no_allocation_in_frames(gpu):
+    """gsr_context_reserve sizes the workspace up front: frames within the
+    reserved bounds (scene size, frame size, instances) make no device
+    allocation, across views in flight on other streams; a frame beyond them
+    still grows (and stays correct)."""
+    from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into
+    g = random_scene(50_000, sh_degree=1, seed=11)
+    scene = HipScene.from_gaussian_data(g)
+    ctx = HipContext()
+    ctx.reserve(50_000, 640, 480, max_instances=400_000)
+    b0, a0 = ctx.workspace()
+    assert b0 > 50_000 * 48 and a0 > 0
+    st = RenderSettings(out_layout=0)
+    ref_ctx = HipContext()
+    s = torch.cuda.Stream()
+    for yaw in (0.0, 40.0, 80.0):
+        for w, h in ((640, 480), (320, 200)):
+            cam = camera_from(Camera(h, w).yaw(yaw))
+            out = torch.empty((3, h, w), dtype=torch.float32, device="cuda")
+            ref = torch.empty_like(out)
+            render_into(ctx, scene, cam, st, out, stream=s)
+            render_into(ref_ctx, scene, cam, st, ref)
+            s.synchronize()
+            torch.cuda.synchronize()
+            assert ctx.stats()["n_instances"] <= 400_000
+            assert torch.equal(out, ref)
+    assert ctx.workspace() == (b0, a0)
+    # beyond the reservation: grows, still the same image
+    big = HipScene.from_gaussian_data(random_scene(120_000, sh_degree=1, seed=12))
+    cam = camera_from(Camera(720, 1280))
+    out = torch.empty((3, 720, 1280), dtype=torch.float32, device="cuda")
+    ref = torch.empty_like(out)
+    render_into(ctx, big, cam, st, out)
+    render_into(HipContext(), big, cam, st, ref)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert ctx.workspace()[1] > a0
+    with pytest.raises(RuntimeError, match="context_reserve"):
+        ctx.reserve(-1, 64, 64)
+    ctx.close()
+    ref_ctx.close()
+    scene.close()
+    big.close()
+
+
 def test_wait_for_counts_has_a_deadline(gpu, monkeypatch):
     """A stream that makes no progress fails gsr_render_finish with
     GSR_ERR_HIP after GSR_WAIT_TIMEOUT_MS instead of hanging the host; the

@@ -64,3 +64,21 @@ def test_naive_scene_known_answers():
     img = C.render(g.flat(), g.sh_dim, U)
     # centre pixel: Gaussian 3 (z=1, front) covers it at alpha 0.99 over Gaussian 0
     assert img[359:361, 639:641].max() > 0.9
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 1000, 300_000])
+@pytest.mark.parametrize("threads", [1, 4])
+def test_c_depth_sort_is_stable_argsort(n, threads):
+    """oracle_sort_depth (the parallel radix sort the CPU baseline times) gives
+    the reference's _sort_gaussian_cpu order: ascending view z, equal keys in
+    ascending id (renderer_ogl.py:16-26), -0.0 equal to +0.0."""
+    rng = np.random.default_rng(n + threads)
+    xyz = rng.normal(size=(n, 3)).astype(np.float32)
+    if n > 10:
+        xyz[::7] = xyz[3]                      # exact ties
+        xyz[5] = [0.0, 0.0, 0.0]               # z = +0.0 ...
+        xyz[9] = [-0.0, 0.0, 0.0]              # ... and -0.0 (equal keys)
+    V = np.eye(4, dtype=np.float32)
+    V[2, :3] = [0.3, -0.5, 0.8]
+    z = ((V[2, 0] * xyz[:, 0] + V[2, 1] * xyz[:, 1]) + V[2, 2] * xyz[:, 2]) + V[2, 3]
+    np.testing.assert_array_equal(C.sort_depth(xyz, V, threads=threads), np.argsort(z, kind="stable"))
