@@ -45,6 +45,7 @@ class GsrSettings(ctypes.Structure):
         ("bg", ctypes.c_float * 3),
         ("t_min", ctypes.c_float),
         ("out_layout", ctypes.c_int32),
+        ("blend", ctypes.c_int32),
     ]
 
 

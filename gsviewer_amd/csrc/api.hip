@@ -80,6 +80,7 @@ struct PendingFrame {
     float t_min = 0.f;
     float bg[3] = {0.f, 0.f, 0.f};
     int32_t out_layout = 0;
+    int32_t blend = GSR_BLEND_FLOAT;
     float* out = nullptr;
     hipStream_t stream = nullptr;
     size_t n = 0;
@@ -160,6 +161,8 @@ int build_uniforms(const gsr_scene* sc, const gsr_camera* cam, const gsr_setting
         return set_error(GSR_ERR_INVALID, "settings: out_layout must be 0 ([3,H,W]) or 1 ([H,W,3])");
     if (!(st->t_min >= 0.f && st->t_min < 1.f))
         return set_error(GSR_ERR_INVALID, "settings: t_min must be in [0, 1)");
+    if (st->blend != GSR_BLEND_FLOAT && st->blend != GSR_BLEND_UNORM8)
+        return set_error(GSR_ERR_INVALID, "settings: blend must be GSR_BLEND_FLOAT or GSR_BLEND_UNORM8");
     std::memcpy(u.V, cam->view, sizeof(u.V));
     std::memcpy(u.P, cam->proj, sizeof(u.P));
     std::memcpy(u.hfov, cam->hfovxy_focal, sizeof(u.hfov));
@@ -202,6 +205,7 @@ int build_uniforms(const gsr_scene* sc, const gsr_camera* cam, const gsr_setting
     u.height = cam->height;
     u.tiles_x = (cam->width + kTile - 1) / kTile;
     u.tiles_y = (cam->height + kTile - 1) / kTile;
+    u.plain_rec = st->blend == GSR_BLEND_UNORM8;
     return GSR_OK;
 }
 
@@ -609,6 +613,7 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
     f.t_min = st->t_min;
     std::memcpy(f.bg, st->bg, sizeof(f.bg));
     f.out_layout = st->out_layout;
+    f.blend = st->blend;
     f.out = out;
     f.stream = s;
     f.n = n;
@@ -663,6 +668,7 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
         f.t_min = st->t_min;
         std::memcpy(f.bg, st->bg, sizeof(f.bg));
         f.out_layout = st->out_layout;
+        f.blend = st->blend;
         f.out = outs[v];
         f.n = n;
         f.slot = (int)(c->frame_idx & 1);
@@ -790,26 +796,34 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     if ((rc = prof_record(c, slot, EV_TSORT, s))) return rc;
     if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, ranges, s))) return rc;
 
-    // compositing chunks: at most one per tile plus one per `chunk` instances
-    const size_t max_chunks = (size_t)num_tiles + n_dup / c->chunk + 1;
-    if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
-    if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
-    if ((rc = c->chunk_desc.ensure(max_chunks, "chunk_desc"))) return rc;
-    if ((rc = c->chunk_order.ensure(max_chunks, "chunk_order"))) return rc;
-    if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
-    if ((rc = c->tmax.ensure(max_chunks, "tmax"))) return rc;
-    if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
-                            c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s)))
-        return rc;
-    if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
-    if ((rc = launch_composite(c->chunk_desc.p, c->chunk_order.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
-                               sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.t_min, f.bg,
-                               f.out_layout, f.out, c->partial.p, c->tmax.p, s)))
-        return rc;
-    if ((rc = prof_record(c, slot, EV_COMPOSITE, s))) return rc;
-    if ((rc = launch_merge(c->chunk_cnt.p, c->chunk_base.p, c->partial.p, sat, u, f.t_min, f.bg, f.out_layout,
-                           f.out, s)))
-        return rc;
+    if (f.blend == GSR_BLEND_UNORM8) {  // the RGBA8 framebuffer: whole lists, back to front, no chunks
+        if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
+        if ((rc = launch_composite_unorm8(ranges, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.bg,
+                                          f.out_layout, f.out, s)))
+            return rc;
+        if ((rc = prof_record(c, slot, EV_COMPOSITE, s))) return rc;
+    } else {
+        // compositing chunks: at most one per tile plus one per `chunk` instances
+        const size_t max_chunks = (size_t)num_tiles + n_dup / c->chunk + 1;
+        if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
+        if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
+        if ((rc = c->chunk_desc.ensure(max_chunks, "chunk_desc"))) return rc;
+        if ((rc = c->chunk_order.ensure(max_chunks, "chunk_order"))) return rc;
+        if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
+        if ((rc = c->tmax.ensure(max_chunks, "tmax"))) return rc;
+        if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
+                                c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s)))
+            return rc;
+        if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
+        if ((rc = launch_composite(c->chunk_desc.p, c->chunk_order.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
+                                   sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.t_min, f.bg,
+                                   f.out_layout, f.out, c->partial.p, c->tmax.p, s)))
+            return rc;
+        if ((rc = prof_record(c, slot, EV_COMPOSITE, s))) return rc;
+        if ((rc = launch_merge(c->chunk_cnt.p, c->chunk_base.p, c->partial.p, sat, u, f.t_min, f.bg, f.out_layout,
+                               f.out, s)))
+            return rc;
+    }
     if ((rc = prof_record(c, slot, EV_COUNT, s))) return rc;
     if (c->prof_on) c->ev_pending[slot] = true;
     {
@@ -845,7 +859,7 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         for (int w = 0; w < v; ++w)
             if (ctxs[w] == c) return set_error(GSR_ERR_INVALID, "render_finish_views: contexts must differ");
         if (f.u.width != f0.u.width || f.u.height != f0.u.height || f.t_min != f0.t_min || f.bg[0] != f0.bg[0] ||
-            f.bg[1] != f0.bg[1] || f.bg[2] != f0.bg[2] || f.out_layout != f0.out_layout ||
+            f.bg[1] != f0.bg[1] || f.bg[2] != f0.bg[2] || f.out_layout != f0.out_layout || f.blend != f0.blend ||
             frag_class_of(f.u.render_mod) != frag_class_of(f0.u.render_mod) || c->chunk != c0->chunk)
             return set_error(GSR_ERR_INVALID, "render_finish_views: views differ in frame size or settings");
     }
@@ -916,12 +930,19 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         if (fv[v].n_dup > 0) ctxs[v]->last_tile_list = tva[v];
     }
     if ((rc = launch_tile_ranges_views(fv, k, s))) return rc;
-    if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk, s))) return rc;
     const PendingFrame& f0 = c0->pend;
-    if ((rc = launch_composite_views(fv, k, (uint32_t)max_chunks, u0, frag_class_of(u0.render_mod), f0.t_min, f0.bg,
-                                     f0.out_layout, s)))
-        return rc;
-    if ((rc = launch_merge_views(fv, k, u0, f0.t_min, f0.bg, f0.out_layout, s))) return rc;
+    if (f0.blend == GSR_BLEND_UNORM8) {  // the RGBA8 framebuffer: one launch per view, no chunks
+        for (int v = 0; v < k; ++v)
+            if ((rc = launch_composite_unorm8(fv[v].ranges, fv[v].tile_vals, fv[v].recs, u0,
+                                              frag_class_of(u0.render_mod), f0.bg, f0.out_layout, fv[v].out, s)))
+                return rc;
+    } else {
+        if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk, s))) return rc;
+        if ((rc = launch_composite_views(fv, k, (uint32_t)max_chunks, u0, frag_class_of(u0.render_mod), f0.t_min,
+                                         f0.bg, f0.out_layout, s)))
+            return rc;
+        if ((rc = launch_merge_views(fv, k, u0, f0.t_min, f0.bg, f0.out_layout, s))) return rc;
+    }
     const auto h3 = std::chrono::steady_clock::now();
     using ms = std::chrono::duration<double, std::milli>;
     for (int v = 0; v < k; ++v) {

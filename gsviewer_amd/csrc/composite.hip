@@ -959,6 +959,143 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_views(MergeViews vs, Co
     merge_tile(v.chunk_cnt, v.chunk_base, v.partial, v.sat, a, v.out, part);
 }
 
+// ---------------------------------------------------------------- unorm8 blend
+// GSR_BLEND_UNORM8: what the reference viewer's RGBA8 framebuffer holds.  GL
+// blends every fragment in draw order (back to front) with SRC_ALPHA /
+// ONE_MINUS_SRC_ALPHA and stores the result as unorm8 (renderer_ogl.py:178-180,
+// main.py:197-198), i.e. rounds after EVERY blend.  That is not associative, so
+// there are no chunks, no early termination and no merge: one wave per tile
+// walks the tile's list backwards (its lists are front to back), 4 pixels per
+// lane as in composite_chunk.  Records are in plain form (u.plain_rec: plain
+// opacity and colour, mid = 0).  The per-fragment arithmetic is the fragment
+// stage's (gau_frag.glsl:30-53) and the blend is evaluated unfused and
+// correctly rounded in the oracle's order (oracle/gl_oracle.c: n = c a + d (1 - a),
+// then q8(n) = floor(clamp(n) 255 + 0.5) / 255); the falloff is the record's
+// log2-scaled quadratic, so alpha can differ from the oracle's expf(power) by
+// an ulp, which moves a blend result across an 8-bit rounding boundary rarely.
+__device__ __forceinline__ float clamp01f(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
+
+__device__ __forceinline__ float q8(float v) {
+    return __fdiv_rn(floorf(__fadd_rn(__fmul_rn(clamp01f(v), 255.0f), 0.5f)), 255.0f);
+}
+
+__device__ __forceinline__ float blend8(float c, float a, float d) {
+    return q8(__fadd_rn(__fmul_rn(c, a), __fmul_rn(d, __fsub_rn(1.0f, a))));
+}
+
+template <int FRAG>
+__device__ __forceinline__ void composite_tile_unorm8(const int tile, const uint2 range, float4* __restrict__ my,
+                                                      const uint32_t* __restrict__ list,
+                                                      const SplatRec* __restrict__ recs, const CompositeArgs& a,
+                                                      float* __restrict__ out) {
+    const int lane = __lane_id();
+    const int tx = tile % a.tiles_x, ty = tile / a.tiles_x;
+    const int lcol = lane & 15, lrow = lane >> 4;
+    const int col_base = tx * kTile, row_base = ty * kTile;
+    const int x = col_base + lcol;
+    const float px = (float)x + 0.5f;
+    float pyw[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pyw[k] = (float)(a.height - 1 - (row_base + 4 * k + lrow)) + 0.5f;
+    float pr[4], pg[4], pb[4];  // the framebuffer (values k / 255), cleared to the background
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        pr[k] = q8(a.bg[0]);
+        pg[k] = q8(a.bg[1]);
+        pb[k] = q8(a.bg[2]);
+    }
+    // batches of up to 64 records, last (backmost) first
+    for (uint32_t top = range.y; top > range.x; top -= min((uint32_t)kBatch, top - range.x)) {
+        const uint32_t nb = min((uint32_t)kBatch, top - range.x);
+        __builtin_amdgcn_wave_barrier();
+        uint64_t sb[4];
+        {
+            float4 f0 = make_float4(0.f, 0.f, 0.f, 0.f), f1 = f0, f2 = f0;
+            uint32_t covx = 0, covy = 0;
+            if ((uint32_t)lane < nb) {  // batch record `lane` = list position top - 1 - lane (draw order)
+                const float4* r = reinterpret_cast<const float4*>(recs + list[top - 1 - lane]);
+                f0 = r[0]; f1 = r[1]; f2 = r[2];
+                const uint32_t xs = __float_as_uint(f0.w), ys = __float_as_uint(f1.w);
+                covx = span_bits16((int)(xs & 0xffffu) - col_base, (int)(xs >> 16) - col_base);
+                covy = span_bits16((int)(ys & 0xffffu) - row_base, (int)(ys >> 16) - row_base);
+            }
+            my[lane * 3 + 0] = make_float4(f0.x, f0.y, f0.z, __uint_as_float(covx | (covy << 16)));
+            my[lane * 3 + 1] = make_float4(f1.x, f1.y, f1.z, 0.f);
+            my[lane * 3 + 2] = make_float4(f2.x, f2.y, f2.z, 0.f);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sb[k] = (uint64_t)__ballot(((covy >> (4 * k)) & 0xfu) != 0u && covx != 0u);
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+        for (int j = 0; j < (int)nb; ++j) {
+            const float4 q0 = my[j * 3 + 0];  // cx cy opacity coverage
+            const float4 q1 = my[j * 3 + 1];  // qa qb qc -
+            const float4 q2 = my[j * 3 + 2];  // r g b -
+            const uint32_t cov = __float_as_uint(q0.w);
+            const bool colin = (cov >> lcol) & 1u;
+            const float dx = px - q0.x;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (!((sb[k] >> j) & 1ull)) continue;
+                const bool covered = colin && ((cov >> (16 + 4 * k + lrow)) & 1u);
+                float al = 1.0f, cr = q2.x, cg = q2.y, cbl = q2.z;
+                bool keep = covered;
+                if (FRAG != kFragBillboard) {
+                    const float dy = pyw[k] - q0.y;
+                    const float pw = (q1.z * dy + q1.y * dx) * dy + q1.x * dx * dx;  // power * log2(e)
+                    const float e = __builtin_amdgcn_exp2f(pw);
+                    al = fminf(0.99f, q0.z * e);
+                    keep = keep && !(pw > 0.0f) && !(al < 1.0f / 255.0f);
+                    if (FRAG == kFragFlatBall || FRAG == kFragGaussBall) al = al > 0.22f ? 1.0f : 0.0f;
+                    if (FRAG == kFragGaussBall) {
+                        cr = q2.x * e;
+                        cg = q2.y * e;
+                        cbl = q2.z * e;
+                    }
+                }
+                cr = clamp01f(cr);
+                cg = clamp01f(cg);
+                cbl = clamp01f(cbl);
+                al = clamp01f(al);
+                if (keep) {
+                    pr[k] = blend8(cr, al, pr[k]);
+                    pg[k] = blend8(cg, al, pg[k]);
+                    pb[k] = blend8(cbl, al, pb[k]);
+                }
+            }
+        }
+    }
+    if (x >= a.width) return;
+    const size_t plane = (size_t)a.width * a.height;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int row = row_base + 4 * k + lrow;
+        if (row >= a.height) continue;
+        const size_t pidx = (size_t)row * a.width + x;
+        if (a.out_layout == 0) {
+            out[pidx] = pr[k];
+            out[plane + pidx] = pg[k];
+            out[2 * plane + pidx] = pb[k];
+        } else {
+            out[3 * pidx] = pr[k];
+            out[3 * pidx + 1] = pg[k];
+            out[3 * pidx + 2] = pb[k];
+        }
+    }
+}
+
+template <int FRAG>
+__global__ __launch_bounds__(256) void k_composite_unorm8(const uint2* __restrict__ ranges,
+                                                          const uint32_t* __restrict__ list,
+                                                          const SplatRec* __restrict__ recs, CompositeArgs a,
+                                                          float* __restrict__ out) {
+    __shared__ float4 lds[4][kBatch * 3];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tile = blockIdx.x * 4 + wave;
+    if (tile >= a.num_tiles) return;
+    composite_tile_unorm8<FRAG>(tile, ranges[tile], lds[wave], list, recs, a, out);
+}
+
 }  // namespace
 
 #ifdef GSR_COMP_STATS
@@ -1070,6 +1207,25 @@ int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n
             break;
     }
     GSR_LAUNCH_CHECK("composite");
+    return GSR_OK;
+}
+
+int launch_composite_unorm8(const uint2* ranges, const uint32_t* tile_list, const SplatRec* recs,
+                            const FrameUniforms& u, int frag_class, const float* bg, int out_layout, float* out,
+                            hipStream_t s) {
+    const CompositeArgs a = make_args(u, 0.f, bg, out_layout);
+    const unsigned grid = (unsigned)((a.num_tiles + 3) / 4);
+    switch (frag_class) {
+        case kFragGauss: k_composite_unorm8<kFragGauss><<<grid, 256, 0, s>>>(ranges, tile_list, recs, a, out); break;
+        case kFragBillboard:
+            k_composite_unorm8<kFragBillboard><<<grid, 256, 0, s>>>(ranges, tile_list, recs, a, out);
+            break;
+        case kFragFlatBall:
+            k_composite_unorm8<kFragFlatBall><<<grid, 256, 0, s>>>(ranges, tile_list, recs, a, out);
+            break;
+        default: k_composite_unorm8<kFragGaussBall><<<grid, 256, 0, s>>>(ranges, tile_list, recs, a, out); break;
+    }
+    GSR_LAUNCH_CHECK("composite_unorm8");
     return GSR_OK;
 }
 

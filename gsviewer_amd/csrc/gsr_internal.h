@@ -73,6 +73,7 @@ struct FrameUniforms {
     int32_t sh_dim;         // floats of SH per Gaussian (3, 12, 27, 48)
     int32_t width, height;
     int32_t tiles_x, tiles_y;
+    int32_t plain_rec;      // records in plain form (GSR_BLEND_UNORM8), not interval form (SplatRec)
 };
 
 struct SceneData {
@@ -281,6 +282,10 @@ int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n
                      const uint32_t* tile_vals, const SplatRec* recs, const FrameUniforms& u,
                      int frag_class, float t_min, const float* bg, int out_layout, float* out,
                      float4* partial, float4* tmax, hipStream_t s);
+// GSR_BLEND_UNORM8: one wave per tile, back to front, 8-bit rounding after every blend
+int launch_composite_unorm8(const uint2* ranges, const uint32_t* tile_list, const SplatRec* recs,
+                            const FrameUniforms& u, int frag_class, const float* bg, int out_layout, float* out,
+                            hipStream_t s);
 // k_merge: folds the partials of multi-chunk tiles into `out` (after launch_composite)
 int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const float4* partial, const uint32_t* sat,
                  const FrameUniforms& u, float t_min, const float* bg, int out_layout, float* out, hipStream_t s);

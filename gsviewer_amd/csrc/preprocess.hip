@@ -519,8 +519,8 @@ __device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, 
     rec.r = col.x;
     rec.g = col.y;
     rec.b = col.z;
-    rec.mid = mid;
-    if (gauss) {  // interval form (gsr_internal.h, SplatRec)
+    rec.mid = u.plain_rec ? 0.f : mid;
+    if (gauss && !u.plain_rec) {  // interval form (gsr_internal.h, SplatRec)
         rec.opacity = sqrtf(po.w / 255.0f) / 0.99f;
         rec.r = 0.99f * col.x;
         rec.g = 0.99f * col.y;

@@ -175,6 +175,7 @@ class RenderSettings:
         self.bg = [0.0, 0.0, 0.0]
         self.t_min = 1e-4
         self.out_layout = 1
+        self.blend = 0          # 0: float; 1: the RGBA8 framebuffer (GSR_BLEND_UNORM8)
         for k, v in kw.items():
             if not hasattr(self, k):
                 raise KeyError(k)
@@ -207,6 +208,7 @@ class RenderSettings:
         if int(self.out_layout) not in (0, 1):
             raise RuntimeError(f"out_layout must be 0 ([3,H,W]) or 1 ([H,W,3]), got {self.out_layout}")
         s.out_layout = int(self.out_layout)
+        s.blend = int(self.blend)
         return s
 
 

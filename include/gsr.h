@@ -82,7 +82,15 @@ typedef struct gsr_settings {
     float t_min;                 /* stop a pixel once transmittance < t_min (0 = never)   */
     int32_t out_layout;          /* 0: planar [3,H,W] (rasterizer output, renderer_cuda.py:234)
                                     1: interleaved [H,W,3] (renderer_cuda.py:245)          */
+    int32_t blend;               /* GSR_BLEND_FLOAT: front-to-back in float (t_min applies);
+                                    GSR_BLEND_UNORM8: the viewer's RGBA8 framebuffer -- GL
+                                    SRC_ALPHA/ONE_MINUS_SRC_ALPHA blending in draw order,
+                                    every blend result rounded to 8 bits (renderer_ogl.py:178-180,
+                                    main.py:197-198); output values are k/255 (t_min unused) */
 } gsr_settings;
+
+#define GSR_BLEND_FLOAT 0
+#define GSR_BLEND_UNORM8 1
 
 /* Per-frame statistics of the last gsr_render on a context. */
 typedef struct gsr_frame_stats {
