@@ -45,6 +45,9 @@ CONFIGS = {
     "c2": (1_000_000, 3, 1920, 1080, "1M Gaussians, SH deg 3, 1920x1080 (garden stand-in)"),
     "c3": (6_000_000, 3, 1920, 1080, "6M Gaussians synthetic, SH deg 3, 1920x1080"),
     "c5": (1_000_000, 3, 3840, 2160, "1M Gaussians, SH deg 3, 3840x2160"),
+    # stress scene beside C2: heavy-tailed splat sizes
+    "c2h": (1_000_000, 3, 1920, 1080, "1M heavy-splat garden stand-in (scale exp(N(-3.5, 0.8))), SH deg 3, "
+                                      "1920x1080 (stress)"),
 }
 
 
@@ -57,6 +60,9 @@ def make_scene(cfg, n, deg):
     if cfg == "c1":
         return random_scene(n, sh_degree=deg, seed=0), "synthetic: random uniform (seed 0)"
     seed = 2 if cfg == "c3" else 1
+    if cfg == "c2h":
+        return (garden_standin(n, seed=seed, sh_degree=deg, log_scale=(-3.5, 0.8)),
+                f"synthetic: heavy-splat garden stand-in (seed {seed}, log-scale N(-3.5, 0.8)), no PLY offline")
     return garden_standin(n, seed=seed, sh_degree=deg), f"synthetic: garden stand-in (seed {seed}), no PLY offline"
 
 
@@ -403,6 +409,7 @@ def main():
     stats["tile_len_max"] = int(lens.max())
     stats["tile_len_p99"] = int(np.percentile(lens, 99))
     stats["tile_len_mean"] = float(lens.mean())
+    stats["instances_per_visible"] = stats["n_instances"] / max(stats["n_visible"], 1)
     stage = {}
     if not args.no_profile:
         ms = (ctypes.c_double * len(_lib.STAGES))()

@@ -117,11 +117,13 @@ def random_scene(n: int, sh_degree: int = 0, seed: int = 0, extent: float = 2.0,
     return GaussianData(xyz, rot, scale, opacity, sh)
 
 
-def garden_standin(n: int, seed: int = 1, sh_degree: int = 3) -> GaussianData:
+def garden_standin(n: int, seed: int = 1, sh_degree: int = 3, log_scale=(-4.6, 0.6)) -> GaussianData:
     """Seeded synthetic stand-in for the Mip-NeRF360 'garden' scene (SURVEY.md
     8d C2/C3): 70 % ground disc + 30 % blob, scale_data(5.0) applied as on PLY
     load (gs_elements_control.py:41-42), scale = exp(N(-4.6,0.6)) before the
-    rescale, opacity = sigmoid(N(0,2)), sh0 ~ N(0,0.6), rest ~ N(0,0.1)."""
+    rescale (`log_scale` = (mean, std); the heavy-splat stress scene of
+    bench.py --config c2h uses (-3.5, 0.8)), opacity = sigmoid(N(0,2)),
+    sh0 ~ N(0,0.6), rest ~ N(0,0.1)."""
     rng = np.random.default_rng(seed)
     k = (sh_degree + 1) ** 2
     n_disc = int(round(0.7 * n))
@@ -134,7 +136,7 @@ def garden_standin(n: int, seed: int = 1, sh_degree: int = 3) -> GaussianData:
     perm = rng.permutation(n)
     xyz = xyz[perm]
     rot = rng.normal(0, 1, (n, 4)).astype(np.float32)
-    scale = np.exp(rng.normal(-4.6, 0.6, (n, 3))).astype(np.float32)
+    scale = np.exp(rng.normal(log_scale[0], log_scale[1], (n, 3))).astype(np.float32)
     opacity = _sigmoid(rng.normal(0, 2, (n, 1))).astype(np.float32)
     sh = np.empty((n, 3 * k), np.float32)
     sh[:, :3] = rng.normal(0, 0.6, (n, 3))
