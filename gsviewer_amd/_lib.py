@@ -59,6 +59,17 @@ class GsrFrameStats(ctypes.Structure):
     ]
 
 
+class GsrPlySceneInfo(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int64),
+        ("sh_dim", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
+        ("points_center", ctypes.c_float * 3),
+        ("scale_factor", ctypes.c_float),
+        ("bbox_center", ctypes.c_float * 3),
+    ]
+
+
 class GsrPlyInfo(ctypes.Structure):
     _fields_ = [
         ("n", ctypes.c_int64),
@@ -120,6 +131,9 @@ SIGNATURES = {
     # gsr_io.h
     "gsr_ply_probe": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo)]),
     "gsr_ply_read": (ctypes.c_int, [ctypes.c_char_p, _P, _P, _P, _P, _P, ctypes.c_int32]),
+    "gsr_scene_load_ply": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_float, ctypes.c_int32, _P, ctypes.POINTER(_P),
+                                          ctypes.POINTER(GsrPlySceneInfo)]),
+    "gsr_scene_read_flat": (ctypes.c_int, [_P, _P, _P]),
     "gsr_ply_write_3dgs": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, _P, ctypes.c_int64, ctypes.c_int32]),
     "gsr_points_center": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.POINTER(ctypes.c_float * 3), _P]),
     "gsr_export_select": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.POINTER(ctypes.c_float * 3),

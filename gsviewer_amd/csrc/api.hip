@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "gsr_internal.h"
+#include "gsr_io.h"
 
 namespace gsr {
 
@@ -447,6 +448,71 @@ int gsr_scene_create(const float* xyz, const float* rot, const float* scale, con
     }
     *out = sc;
     return GSR_OK;
+}
+
+int gsr_scene_load_ply(const char* path, float scale_to_interval, int32_t n_threads, void* stream, gsr_scene** out,
+                       gsr_ply_scene_info* info) {
+    if (!path || !out) return set_error(GSR_ERR_INVALID, "scene_load_ply: null argument");
+    *out = nullptr;
+    hipStream_t s = (hipStream_t)stream;
+    float* flat = nullptr;
+    int64_t n = 0;
+    int32_t sh_dim = 0;
+    int rc = ply_stream_flat(path, n_threads, s, &flat, &n, &sh_dim);
+    if (rc) return rc;
+    // scratch: 6 min/max keys, (centre, factor), points_center, xyz [n,3]
+    void* tmp = nullptr;
+    const size_t tmp_bytes = 64 + (size_t)std::max<int64_t>(n, 1) * 3 * sizeof(float);
+    if (hipMalloc(&tmp, tmp_bytes) != hipSuccess) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(flat);
+        return set_error(GSR_ERR_NOMEM, "scene_load_ply: scratch allocation failed");
+    }
+    uint32_t* keys = static_cast<uint32_t*>(tmp);
+    float* cf = reinterpret_cast<float*>(keys + 8);  // centre xyz, factor
+    float* pc = cf + 4;                               // points_center
+    float* xyz = pc + 4;
+    float host[8] = {0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 0.f};
+    gsr_scene* sc = nullptr;
+    auto fail = [&](int code) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(flat);
+        (void)hipFree(tmp);
+        if (sc) {
+            if (sc->d.block) (void)hipFree(sc->d.block);
+            delete sc;
+        }
+        return code;
+    };
+    if ((rc = make_scene(n, sh_dim, out, &sc))) return fail(rc);
+    if ((rc = ply_activate_flat(flat, n, sh_dim, scale_to_interval, keys, cf, xyz, s))) return fail(rc);
+    if (n > 0 && (rc = launch_points_center(xyz, n, pc, s))) return fail(rc);
+    if ((rc = scene_repack_from_flat(sc->d, flat, s))) return fail(rc);
+    if (scale_to_interval > 0.f && n > 0 &&
+        hipMemcpyAsync(host, cf, 4 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess)
+        return fail(set_error(GSR_ERR_HIP, "scene_load_ply: copy back failed"));
+    if (n > 0 && hipMemcpyAsync(host + 4, pc, 3 * sizeof(float), hipMemcpyDeviceToHost, s) != hipSuccess)
+        return fail(set_error(GSR_ERR_HIP, "scene_load_ply: copy back failed"));
+    if (hipStreamSynchronize(s) != hipSuccess) return fail(set_error(GSR_ERR_HIP, "scene_load_ply: stream failed"));
+    (void)hipFree(flat);
+    (void)hipFree(tmp);
+    if (info) {
+        info->n = n;
+        info->sh_dim = sh_dim;
+        info->pad = 0;
+        for (int k = 0; k < 3; ++k) {
+            info->bbox_center[k] = host[k];
+            info->points_center[k] = host[4 + k];
+        }
+        info->scale_factor = host[3];
+    }
+    *out = sc;
+    return GSR_OK;
+}
+
+int gsr_scene_read_flat(const gsr_scene* sc, float* flat_dev, void* stream) {
+    if (!sc || (!flat_dev && sc->d.n > 0)) return set_error(GSR_ERR_INVALID, "scene_read_flat: null argument");
+    return scene_unpack_flat(sc->d, flat_dev, (hipStream_t)stream);
 }
 
 int gsr_scene_create_flat(const float* flat, int64_t n, int32_t sh_dim, void* stream, gsr_scene** out) {

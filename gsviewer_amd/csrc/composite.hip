@@ -976,11 +976,13 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_views(MergeViews vs, Co
 __device__ __forceinline__ float clamp01f(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
 
 __device__ __forceinline__ float q8(float v) {
-    return __fdiv_rn(floorf(__fadd_rn(__fmul_rn(clamp01f(v), 255.0f), 0.5f)), 255.0f);
+#pragma clang fp contract(off)  // plain operators: the __f*_rn intrinsics' bodies may still be fused
+    return floorf(clamp01f(v) * 255.0f + 0.5f) / 255.0f;
 }
 
 __device__ __forceinline__ float blend8(float c, float a, float d) {
-    return q8(__fadd_rn(__fmul_rn(c, a), __fmul_rn(d, __fsub_rn(1.0f, a))));
+#pragma clang fp contract(off)
+    return q8(c * a + d * (1.0f - a));
 }
 
 template <int FRAG>

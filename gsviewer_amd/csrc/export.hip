@@ -184,6 +184,14 @@ struct Tmp {
 };
 
 }  // namespace
+
+int launch_points_center(const float* xyz, int64_t n, float* out3, hipStream_t s) {
+    if (n <= 0) return set_error(GSR_ERR_INVALID, "points_center: empty point set");
+    k_center_seq<<<1, 64, 0, s>>>(xyz, n, out3);
+    GSR_LAUNCH_CHECK("center_seq");
+    return GSR_OK;
+}
+
 }  // namespace gsr
 
 using namespace gsr;

@@ -217,6 +217,20 @@ int scene_repack_from_fields(SceneData& sd, const float* xyz, const float* rot,
                              const float* scale, const float* opacity, const float* sh,
                              hipStream_t s);
 int scene_repack_from_flat(SceneData& sd, const float* flat, hipStream_t s);
+// the SoA planes back to a flat [n, 11 + sh_dim] device array
+int scene_unpack_flat(const SceneData& sd, float* flat, hipStream_t s);
+// PLY load (gsr_scene_load_ply): load_ply's activations on raw flat rows, then
+// (interval > 0) scale_data: keys = 6 uint32 scratch, out4 = (centre, factor)
+// device floats; xyz [n,3] receives the final positions (for points_center).
+int ply_activate_flat(float* flat, int64_t n, int sh_dim, float interval, uint32_t* keys, float* out4, float* xyz,
+                      hipStream_t s);
+// export.hip: points_center = np.mean(xyz, axis=0), bit-exact, into out3 (device)
+int launch_points_center(const float* xyz, int64_t n, float* out3, hipStream_t s);
+// ply.cpp: the raw (pre-activation) vertex rows of a PLY streamed into a new
+// device array flat [n, 11 + sh_dim] (hipMalloc'd; the caller frees it):
+// chunks parsed by host threads into pinned buffers, copied while the next
+// chunk is parsed.
+int ply_stream_flat(const char* path, int32_t n_threads, hipStream_t s, float** flat_dev, int64_t* n, int32_t* sh_dim);
 
 // preprocess.hip
 // k_cull also zeroes n_zero words at zero_words (the frame's zero block) and

@@ -319,6 +319,19 @@ std::vector<Column> columns(const Layout& L, float* xyz, float* rot, float* scal
     return c;
 }
 
+// The same columns into flat rows [xyz, rot, scale, opacity, sh] (util_gau.py:40-42).
+std::vector<Column> flat_columns(const Layout& L, float* flat) {
+    const int rec = 11 + L.sh_dim;
+    std::vector<Column> c;
+    for (int k = 0; k < 3; ++k) c.push_back({L.xyz[k], flat, rec, k});
+    for (int k = 0; k < 4; ++k) c.push_back({L.rot[k], flat, rec, 3 + k});
+    for (int k = 0; k < 3; ++k) c.push_back({L.scale[k], flat, rec, 7 + k});
+    c.push_back({L.op, flat, rec, 10});
+    for (int k = 0; k < 3; ++k) c.push_back({L.dc[k], flat, rec, 11 + k});
+    for (int r = 0; r < (int)L.rest.size(); ++r) c.push_back({L.rest[r], flat, rec, 11 + 3 + 3 * (r % 15) + r / 15});
+    return c;
+}
+
 int threads_for(int32_t n_threads, int64_t rows) {
     int t = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
     const int64_t min_rows = 16384;  // below this a thread costs more than it converts
@@ -415,6 +428,91 @@ extern "C" int gsr_ply_read(const char* path, float* xyz, float* rot, float* sca
     });
     return GSR_OK;
 }
+
+namespace gsr {
+
+// Raw vertex rows streamed to the device: chunks of kChunkRows rows are
+// converted by the thread pool into one of two pinned buffers and copied
+// asynchronously on `s` while the next chunk is converted (an event per
+// buffer guards its reuse).  ASCII bodies are parsed whole, then copied.
+int ply_stream_flat(const char* path, int32_t n_threads, hipStream_t s, float** flat_dev, int64_t* n_out,
+                    int32_t* sh_dim_out) {
+    *flat_dev = nullptr;
+    MappedFile f;
+    int rc = f.open_read(path);
+    if (rc) return rc;
+    Layout L;
+    if ((rc = make_layout(f, L))) return rc;
+    const Element& v = L.h.elements[L.vi];
+    const int64_t n = v.count;
+    const int rec = 11 + L.sh_dim;
+    *n_out = n;
+    *sh_dim_out = L.sh_dim;
+    float* dev = nullptr;
+    if (hipMalloc(&dev, (size_t)std::max<int64_t>(n, 1) * rec * sizeof(float)) != hipSuccess)
+        return set_error(GSR_ERR_NOMEM, "ply: hipMalloc of the row buffer failed");
+    constexpr int64_t kChunkRows = 1 << 17;
+    const int64_t chunk = L.h.format == GSR_PLY_ASCII ? std::max<int64_t>(n, 1) : std::min<int64_t>(kChunkRows, std::max<int64_t>(n, 1));
+    float* pin[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    auto cleanup = [&](int code) {
+        for (int b = 0; b < 2; ++b) {
+            if (done[b]) {
+                (void)hipEventSynchronize(done[b]);
+                (void)hipEventDestroy(done[b]);
+            }
+            if (pin[b]) (void)hipHostFree(pin[b]);
+        }
+        if (code != GSR_OK) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(dev);
+        } else {
+            *flat_dev = dev;
+        }
+        return code;
+    };
+    const int nbuf = L.h.format == GSR_PLY_ASCII ? 1 : 2;
+    for (int b = 0; b < nbuf; ++b) {
+        if (hipHostMalloc(&pin[b], (size_t)chunk * rec * sizeof(float), hipHostMallocDefault) != hipSuccess)
+            return cleanup(set_error(GSR_ERR_NOMEM, "ply: pinned staging allocation failed"));
+        if (hipEventCreateWithFlags(&done[b], hipEventDisableTiming) != hipSuccess)
+            return cleanup(set_error(GSR_ERR_HIP, "ply: event creation failed"));
+    }
+    if (n == 0) return cleanup(GSR_OK);
+    if (L.h.format == GSR_PLY_ASCII) {
+        if ((rc = read_ascii(f, L, flat_columns(L, pin[0])))) return cleanup(rc);
+        if (hipMemcpyAsync(dev, pin[0], (size_t)n * rec * sizeof(float), hipMemcpyHostToDevice, s) != hipSuccess)
+            return cleanup(set_error(GSR_ERR_HIP, "ply: host-to-device copy failed"));
+        return cleanup(GSR_OK);
+    }
+    const bool swap = L.h.format == GSR_PLY_BINARY_BE;
+    const int rb = v.row_bytes;
+    const int nt = threads_for(n_threads, chunk);
+    for (int64_t r0 = 0, k = 0; r0 < n; r0 += chunk, ++k) {
+        const int b = (int)(k & 1);
+        const int64_t m = std::min(chunk, n - r0);
+        if (k >= 2 && hipEventSynchronize(done[b]) != hipSuccess)  // its previous copy has left the buffer
+            return cleanup(set_error(GSR_ERR_HIP, "ply: staging copy failed"));
+        const std::vector<Column> cols = flat_columns(L, pin[b]);
+        std::vector<std::pair<int, PType>> src(cols.size());
+        for (size_t c = 0; c < cols.size(); ++c) src[c] = {v.props[cols[c].prop].offset, v.props[cols[c].prop].type};
+        const char* base = f.data + L.vertex_offset + (size_t)r0 * rb;
+        parallel_rows(m, std::min<int>(nt, std::max<int64_t>(1, m / 16384)), [&](int64_t a, int64_t e) {
+            for (int64_t r = a; r < e; ++r) {
+                const char* row = base + r * rb;
+                for (size_t c = 0; c < cols.size(); ++c)
+                    cols[c].dst[r * cols[c].stride + cols[c].col] = read_as_float(row + src[c].first, src[c].second, swap);
+            }
+        });
+        if (hipMemcpyAsync(dev + r0 * rec, pin[b], (size_t)m * rec * sizeof(float), hipMemcpyHostToDevice, s) !=
+                hipSuccess ||
+            hipEventRecord(done[b], s) != hipSuccess)
+            return cleanup(set_error(GSR_ERR_HIP, "ply: host-to-device copy failed"));
+    }
+    return cleanup(GSR_OK);
+}
+
+}  // namespace gsr
 
 extern "C" int gsr_ply_write_3dgs(const char* in_path, const char* out_path, const int64_t* rows, int64_t n_rows,
                                   int32_t n_threads) {

@@ -90,6 +90,35 @@ class HipScene:
         obj._keep = None
         return obj
 
+    @classmethod
+    def from_ply(cls, path: str, scale_to_interval: float = 5.0, n_threads: int = 0, stream=None):
+        """The viewer's "Open ply" (gs_elements_control.py:41-44: load_ply,
+        scale_data(5.0), points_center) straight into the device scene
+        (gsr_scene_load_ply).  Sets ``points_center``, ``scale_factor`` and
+        ``bbox_center`` from the load."""
+        import os
+        lib = _lib.load()
+        info = _lib.GsrPlySceneInfo()
+        h = ctypes.c_void_p()
+        _lib.check(lib.gsr_scene_load_ply(os.fsencode(path), float(scale_to_interval), int(n_threads),
+                                          _stream_handle(stream), ctypes.byref(h), ctypes.byref(info)),
+                   f"gsr_scene_load_ply({path})")
+        obj = cls.__new__(cls)
+        obj._h, obj._keep = h, None
+        obj.n, obj.sh_dim = int(info.n), int(info.sh_dim)
+        obj.points_center = np.array(list(info.points_center), np.float32)
+        obj.scale_factor = float(info.scale_factor)
+        obj.bbox_center = np.array(list(info.bbox_center), np.float32)
+        return obj
+
+    def read_flat(self, stream=None) -> torch.Tensor:
+        """The scene as flat rows [N, 11 + sh_dim] (util_gau.py:40-42), on the GPU."""
+        out = torch.empty((max(self.n, 1), 11 + self.sh_dim), dtype=torch.float32, device="cuda")
+        _lib.check(_lib.load().gsr_scene_read_flat(self._h, ctypes.c_void_p(out.data_ptr()), _stream_handle(stream)),
+                   "gsr_scene_read_flat")
+        _sync_stream(stream)
+        return out[: self.n]
+
     @property
     def handle(self):
         return self._h

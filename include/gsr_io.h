@@ -51,6 +51,30 @@ int gsr_ply_probe(const char* path, gsr_ply_info* info);
 int gsr_ply_read(const char* path, float* xyz, float* rot, float* scale, float* opacity, float* sh,
                  int32_t n_threads);
 
+/* The viewer's "Open ply" step straight into a device scene: util_gau.load_ply
+ * (util_gau.py:236-305), then GaussianData.scale_data(scale_to_interval)
+ * (util_gau.py:44-53; the viewer uses 5.0, gs_elements_control.py:41-42; <= 0
+ * skips it) and points_center (np.mean(xyz, axis=0), :44), then the SoA
+ * repack of update_gaussian_data.  The vertex rows are parsed by host threads
+ * in chunks into pinned buffers and copied while the next chunk is parsed;
+ * the activations, the rescale and the mean run on the GPU in the
+ * reference's float32 order (xyz, rot, sh bit-identical to load_ply +
+ * scale_data; scale and opacity within a few ulps: NumPy's float32 exp is its
+ * own SIMD polynomial).  Synchronous on `stream`. */
+typedef struct gsr_ply_scene_info {
+    int64_t n;
+    int32_t sh_dim;
+    int32_t pad;
+    float points_center[3];  /* after the rescale: set_points_center's value */
+    float scale_factor;      /* scale_data's factor (1 when skipped) */
+    float bbox_center[3];    /* scale_data's centre (0 when skipped) */
+} gsr_ply_scene_info;
+int gsr_scene_load_ply(const char* path, float scale_to_interval, int32_t n_threads, void* stream, gsr_scene** out,
+                       gsr_ply_scene_info* info);
+
+/* A scene back as flat rows [n, 11 + sh_dim] (util_gau.py:40-42) in device memory. */
+int gsr_scene_read_flat(const gsr_scene* scene, float* flat_dev, void* stream);
+
 /* Write rows of `in_path` to `out_path` in gsconverter's 3dgs layout:
  * binary_little_endian; float properties x y z nx ny nz f_dc_0..2
  * f_rest_0..44 opacity scale_0..2 rot_0..3.  Values are copied by name and a
