@@ -117,7 +117,13 @@ __device__ __forceinline__ void pixel_span(float lo, float hi, int limit, int& p
 // rounding of pw and of the box), so no kept fragment is ever dropped: the
 // result only narrows the tiles and 16x4 slices a splat is composited over.
 // opacity < 1/255 (thr > 0, or NaN): nothing is ever drawn, the rectangle is
-// emptied.  Degenerate or nearly degenerate forms keep the quad unchanged.
+// emptied.  Forms with disc = 4 qa qc - qb^2 <= 1e-2 * 4 qa qc (correlation
+// |rho| > 0.995: needles) keep the quad unchanged.  Error budget (DESIGN.md,
+// "alpha-box margin"): with disc / (4 qa qc) >= 1e-2 the cancellation in
+// qa - qb^2 / (4 qc) amplifies the few-ulp rounding of the terms by at most
+// 2 / 1e-2 = 200, i.e. <= ~1e-4 relative on hx^2, and the compositor's pw at a
+// pixel carries a relative error of the same order; the margin is 2e-3
+// relative + 0.01 px, an order of magnitude above both.
 // Evaluated without contraction in this fixed order: tests/helpers.py
 // (alpha_box_rects) mirrors it bit for bit.
 __device__ __forceinline__ void alpha_box(float qa, float qb, float qc, float thr, float cx, float cy, int height,
@@ -129,7 +135,7 @@ __device__ __forceinline__ void alpha_box(float qa, float qb, float qc, float th
     }
     const float d4 = (4.0f * qa) * qc;
     const float disc = d4 - qb * qb;
-    if (!(qa < 0.0f && qc < 0.0f && disc > 1e-4f * d4)) return;
+    if (!(qa < 0.0f && qc < 0.0f && disc > 1e-2f * d4)) return;
     const float hx = sqrtf(thr / (qa - (qb * qb) / (4.0f * qc))) * 1.002f + 0.01f;
     const float hy = sqrtf(thr / (qc - (qb * qb) / (4.0f * qa))) * 1.002f + 0.01f;
     if (!(hx < 65536.0f && hy < 65536.0f)) return;  // (cx, cy are within 1.3x of the viewport)

@@ -195,7 +195,7 @@ def alpha_box_rects(rec, rects, height):
         empty = ~(thr <= F(0.0))
         d4 = (F(4.0) * qa) * qc
         disc = d4 - qb * qb
-        ok = ~empty & (qa < F(0.0)) & (qc < F(0.0)) & (disc > F(1e-4) * d4)
+        ok = ~empty & (qa < F(0.0)) & (qc < F(0.0)) & (disc > F(1e-2) * d4)
         hx = np.sqrt(thr / (qa - (qb * qb) / (F(4.0) * qc))) * F(1.002) + F(0.01)
         hy = np.sqrt(thr / (qc - (qb * qb) / (F(4.0) * qa))) * F(1.002) + F(0.01)
         ok &= (hx < F(65536.0)) & (hy < F(65536.0))

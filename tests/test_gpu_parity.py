@@ -152,6 +152,37 @@ def test_alpha_box_keeps_every_fragment(gpu):
     compare_images(res["image"], O.composite(vs, U))
 
 
+def test_alpha_box_4k_large_anisotropic(gpu):
+    """The same at 3840x2160 with large, strongly anisotropic splats (needles
+    and flat discs at every orientation, hundreds of pixels long) and the
+    whole opacity range: the margin of the alpha box (x 1.002 + 0.01 px) and
+    its degeneracy cut (|rho| > 0.995 keeps the quad) hold every kept
+    fragment inside the narrowed rectangle."""
+    rng = np.random.default_rng(21)
+    g = random_scene(1200, sh_degree=0, seed=21, scale_range=(0.02, 0.35))
+    squash = rng.uniform(0.02, 1.0, g.scale.shape).astype(np.float32)
+    squash[np.arange(len(g)), rng.integers(0, 3, len(g))] = 1.0  # one long axis each
+    g.scale[:] = (g.scale * squash).astype(np.float32)
+    g.opacity[:] = rng.uniform(1.0 / 255, 1.0, g.opacity.shape).astype(np.float32)
+    cam = Camera(2160, 3840).yaw(10)
+    res = gpu_frame(g, cam, _settings(t_min=0.0), with_debug=True)
+    U = uniforms_for(cam)
+    vs = O.vertex_stage(g.flat(), 3, U)
+    x0, x1, r0, r1 = narrowed_rects(res, vs, U)
+    qx0, qx1, qr0, qr1 = O.splat_rects(vs, U)
+    ids = np.nonzero(vs["visible"] & (qx0 <= qx1) & (qr0 <= qr1))[0]
+    narrowed, big = 0, 0
+    for gid in ids:
+        xs = np.arange(qx0[gid], qx1[gid] + 1)
+        rows = np.arange(qr0[gid], qr1[gid] + 1)
+        keep = kept_fragments(vs, U, gid, xs, rows)
+        inside = ((xs >= x0[gid]) & (xs <= x1[gid]))[None, :] & ((rows >= r0[gid]) & (rows <= r1[gid]))[:, None]
+        assert not (keep & ~inside).any(), f"Gaussian {gid}"
+        narrowed += int(not inside.all())
+        big += int(max(len(xs), len(rows)) > 200)
+    assert narrowed > len(ids) // 10 and big > 20, (narrowed, big, len(ids))
+
+
 def test_radii(gpu):
     g = random_scene(2000, sh_degree=0, seed=8)
     cam = Camera(120, 160)
