@@ -258,14 +258,17 @@ def main():
     ap.add_argument("--t-min", type=float, default=1e-4)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=16,
+    ap.add_argument("--inflight", type=int, default=20,
                     help="independent views in flight per GPU (own context each, pipelined with "
-                         "gsr_render_begin[_views]/finish); 1 = one at a time")
+                         "gsr_render_begin[_views]/finish); 1 = one at a time.  Default 20: 4 groups of 5 "
+                         "(tools/short_region_sweep2.sh: 0.204 ms/frame over 100 frames and 0.215 over the "
+                         "driver's 20, against 0.209 / 0.230 for 16 as 4 x 4), and 20 frames are then exactly "
+                         "one begin + finish of every group")
     ap.add_argument("--share", type=int, default=None,
                     help="views per shared scene pass (gsr_render_begin_views): the views in flight form "
                          "inflight/share groups, one stream each, whose cull + preprocess read the scene once "
-                         "per group; 1 = off (one stream per view).  Default: 4 when --inflight is a multiple of 4 "
-                         "and >= 8, else 1")
+                         "per group; 1 = off (one stream per view).  Default: --inflight / 4 (four group streams) "
+                         "when --inflight is a multiple of 4 in [8, 32], else 1")
     ap.add_argument("--no-batched-sorts", action="store_true",
                     help="with --share > 1: one depth sort per view instead of one batched sort per group")
     ap.add_argument("--no-batched-finish", action="store_true",
@@ -290,7 +293,8 @@ def main():
     # One hardware queue per in-flight view stream (+ torch's own): HIP maps
     # streams round-robin onto GPU_MAX_HW_QUEUES queues (4 by default), and two
     # view streams sharing a queue serialise.  Must be set before HIP starts.
-    share = args.share if args.share is not None else (4 if args.inflight % 4 == 0 and args.inflight >= 8 else 1)
+    share = args.share if args.share is not None else (
+        args.inflight // 4 if args.inflight % 4 == 0 and 8 <= args.inflight <= 32 else 1)
     share = max(1, share)
     if args.inflight % share:
         ap.error("--inflight must be a multiple of --share")
