@@ -82,14 +82,19 @@ __global__ __launch_bounds__(kThreads) void k_bin_reduce(const uint32_t* __restr
 }
 
 // Exclusive offsets of the block's splats (block prefix + in-block scan), then
-// one (tile key, record slot) instance per covered tile, row-major.
+// one (tile key, record slot) instance per covered tile, row-major.  The
+// block prefix is the sum of the earlier blocks' totals (bin_reduce), read
+// here (a few thousand words at most, L2-resident) instead of scanned by a
+// launch of its own.
 template <bool kPacked>
 __device__ __forceinline__ void bin_write(const uint32_t* __restrict__ sorted_ids,
                                           const uint2* __restrict__ trect_sorted,
                                           const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
-                                          const uint32_t* __restrict__ block_off, int tiles_x,
+                                          const uint32_t* __restrict__ block_sums, int tiles_x,
                                           uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ tile_vals,
                                           uint32_t blk, uint32_t* lds) {
+    uint32_t pre = 0;  // this thread's share of the earlier blocks' totals
+    for (uint32_t b = threadIdx.x; b < blk; b += kThreads) pre += block_sums[b];
     const uint32_t base = blk * kBinBlock + threadIdx.x * kBinItems;  // 4 consecutive per thread
     uint32_t id[kBinItems];
     uint2 tr[kBinItems];
@@ -109,11 +114,13 @@ __device__ __forceinline__ void bin_write(const uint32_t* __restrict__ sorted_id
     }
     const int w = threadIdx.x >> 6;
     const uint32_t inc = wave_inclusive_scan(s);
+    pre = wave_reduce_sum(pre);
     if (__lane_id() == 63) lds[w] = inc;
+    if (__lane_id() == 0) lds[kThreads / 64 + w] = pre;
     __syncthreads();
-    uint32_t o = block_off[blk] + inc - s;
+    uint32_t o = inc - s;
 #pragma unroll
-    for (int k = 0; k < kThreads / 64; ++k) o += (k < w) ? lds[k] : 0u;
+    for (int k = 0; k < kThreads / 64; ++k) o += ((k < w) ? lds[k] : 0u) + lds[kThreads / 64 + k];
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
         const uint32_t tx0 = tr[k].x & 0xffffu, tx1 = tr[k].x >> 16, ty0 = tr[k].y & 0xffffu, ty1 = tr[k].y >> 16;
@@ -131,11 +138,11 @@ template <bool kPacked>
 __global__ __launch_bounds__(kThreads) void k_bin_write(const uint32_t* __restrict__ sorted_ids,
                                                         const uint2* __restrict__ trect_sorted,
                                                         const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
-                                                        const uint32_t* __restrict__ block_off, int tiles_x,
+                                                        const uint32_t* __restrict__ block_sums, int tiles_x,
                                                         uint32_t* __restrict__ tile_keys,
                                                         uint32_t* __restrict__ tile_vals) {
-    __shared__ uint32_t lds[kThreads / 64];
-    bin_write<kPacked>(sorted_ids, trect_sorted, rect4_sorted, n_vis, block_off, tiles_x, tile_keys, tile_vals,
+    __shared__ uint32_t lds[2 * kThreads / 64];
+    bin_write<kPacked>(sorted_ids, trect_sorted, rect4_sorted, n_vis, block_sums, tiles_x, tile_keys, tile_vals,
                        blockIdx.x, lds);
 }
 
@@ -165,7 +172,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_reduce_views(BinViews vs) {
 
 template <bool kPacked>
 __global__ __launch_bounds__(kThreads) void k_bin_write_views(BinViews vs, int tiles_x) {
-    __shared__ uint32_t lds[kThreads / 64];
+    __shared__ uint32_t lds[2 * kThreads / 64];
     const BinView& v = vs.v[blockIdx.y];
     if (blockIdx.x * kBinBlock >= v.n_vis) return;
     bin_write<kPacked>(v.sorted_ids, v.trect_sorted, v.rect4_sorted, v.n_vis, v.block_sums, tiles_x, v.tile_keys,
@@ -1131,8 +1138,6 @@ int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_
     else
         k_bin_reduce<false><<<nb, kThreads, 0, s>>>(sorted_ids, trect, rect4_sorted, n_vis, tmp, trect_sorted);
     GSR_LAUNCH_CHECK("bin_reduce");
-    int rc = scan_exclusive(tmp, tmp, nb, nullptr, nullptr, s);
-    if (rc) return rc;
     if (rect4_sorted)
         k_bin_write<true><<<nb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tmp, tiles_x,
                                                   tile_keys, tile_vals);
@@ -1242,7 +1247,6 @@ int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const fl
 // ------------------------------------------------------------ groups of views
 int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s) {
     BinViews bv{};
-    uint32_t* arrays[kMaxViews];
     uint32_t nb[kMaxViews];
     uint32_t nb_max = 0;
     for (int i = 0; i < k; ++i) {
@@ -1251,7 +1255,6 @@ int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s) {
                           f.n_vis};
         if ((f.rect4_sorted != nullptr) != (views[0].rect4_sorted != nullptr))
             return set_error(GSR_ERR_INVALID, "binning: packed rectangles on some views only");
-        arrays[i] = f.bin_tmp;
         nb[i] = (f.n_vis + kBinBlock - 1) / kBinBlock;
         nb_max = std::max(nb_max, nb[i]);
     }
@@ -1262,8 +1265,6 @@ int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s) {
     else
         k_bin_reduce_views<false><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv);
     GSR_LAUNCH_CHECK("bin_reduce_views");
-    int rc = scan_single_views(arrays, nb, k, s);
-    if (rc) return rc;
     if (packed)
         k_bin_write_views<true><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x);
     else

@@ -331,7 +331,7 @@ struct FinishView {
     float* out;
     float4* partial;
 };
-// binning: scan_tmp of each view is its bin_tmp (block sums scanned in place)
+// binning: bin_tmp of each view holds its per-block instance counts
 int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s);
 int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s);
 int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, hipStream_t s);
@@ -339,8 +339,6 @@ int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, const 
                            float t_min, const float* bg, int out_layout, hipStream_t s);
 int launch_merge_views(FinishView* views, int k, const FrameUniforms& u, float t_min, const float* bg,
                        int out_layout, hipStream_t s);
-// scan.hip: in-place exclusive scans of k small arrays (each n <= 131072), one launch
-int scan_single_views(uint32_t* const* arrays, const uint32_t* n, int k, hipStream_t s);
 
 }  // namespace gsr
 

@@ -13,12 +13,12 @@ constexpr int kItems = 16;
 constexpr int kTileItems = kThreads * kItems;  // 4096
 constexpr int kPartialThreads = 1024;
 constexpr size_t kSingleMax = 131072;  // single-workgroup scan up to this many elements
-// Short single-workgroup scans (the binning's block sums, ~1000 entries) run as
-// 4-wave blocks: a 16-wave block waits for a whole CU's worth of free slots
-// while other views' compositors hold the chip (in flight,
-// k_scan_single_views averaged 68 us against 4.5 us alone).  Longer ones (the
-// visibility words, ~16k at 1M) keep 16 waves: with 4 the cull stage took
-// 8 us longer alone.
+// Short single-workgroup scans (<= 1024 entries) run as 4-wave blocks: a
+// 16-wave block waits for a whole CU's worth of free slots while other views'
+// compositors hold the chip (in flight a 1024-thread scan of the binning's
+// block sums averaged 68 us against 4.5 us alone; the binning now sums those
+// itself, bin_write).  Longer ones (the visibility words, ~16k at 1M) keep 16
+// waves: with 4 the cull stage took 8 us longer alone.
 constexpr int kSingleThreads = 256;
 constexpr size_t kSmallScan = 4 * kSingleThreads;  // one chunk of the 256-thread scan
 
@@ -195,18 +195,6 @@ __global__ __launch_bounds__(NT) void k_scan_single(const uint32_t* __restrict__
     scan_single<NT>(in, out, n, total_dev, lds);
 }
 
-// In-place scans of up to kMaxViews small arrays, one workgroup each (blockIdx.y).
-struct ScanViews {
-    uint32_t* a[kMaxViews];
-    uint32_t n[kMaxViews];
-};
-
-__global__ __launch_bounds__(kSingleThreads) void k_scan_single_views(ScanViews v) {
-    __shared__ uint32_t lds[2][kSingleThreads / 64];
-    const int i = blockIdx.y;
-    scan_single<kSingleThreads>(v.a[i], v.a[i], v.n[i], nullptr, lds);
-}
-
 }  // namespace
 
 size_t scan_tmp_elems(size_t n) {
@@ -237,19 +225,6 @@ int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
     GSR_LAUNCH_CHECK("scan_partials");
     k_scan_final<<<dim3((unsigned)nb), dim3(kThreads), 0, s>>>(in, out, n, tmp);
     GSR_LAUNCH_CHECK("scan_final");
-    return GSR_OK;
-}
-
-int scan_single_views(uint32_t* const* arrays, const uint32_t* n, int k, hipStream_t s) {
-    if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "scan: view count out of range");
-    ScanViews v{};
-    for (int i = 0; i < k; ++i) {
-        if (n[i] > kSingleMax) return set_error(GSR_ERR_INVALID, "scan: array too long for a single-workgroup scan");
-        v.a[i] = arrays[i];
-        v.n[i] = n[i];
-    }
-    k_scan_single_views<<<dim3(1, (unsigned)k), kSingleThreads, 0, s>>>(v);
-    GSR_LAUNCH_CHECK("scan_single_views");
     return GSR_OK;
 }
 
