@@ -250,3 +250,31 @@ def test_rect_payload_matches_gathered_rects(gpu, monkeypatch):
     for c in ctxs:
         c.close()
     scene.close()
+
+
+@pytest.mark.parametrize("wh", [(16, 16), (13, 9)])
+def test_single_tile_frames(gpu, wh):
+    """A frame of one 16x16 tile has no tile sort; its range [0, D) is set
+    directly (single_tile_range).  Alone and batched, against the oracle."""
+    import sys
+
+    from gsviewer_amd.camera import view_for_rank
+    from gsviewer_amd.gaussian_data import random_scene
+    from gsviewer_amd.rasterizer import HipScene, RenderSettings
+    from helpers import TOL_MAX, batched_frames, compare_images, gpu_frame, uniforms_for
+    sys.path.insert(0, __file__.rsplit("/tests/", 1)[0])
+    from oracle import gl_oracle as O
+    w, h = wh
+    g = random_scene(800, sh_degree=1, seed=11, scale_range=(0.02, 0.08))
+    cams = [view_for_rank(h, w, k) for k in range(4)]
+    st = RenderSettings(t_min=0.0)
+    scene = HipScene.from_gaussian_data(g)
+    res = batched_frames(scene, cams, st, group=4)
+    for cam, r in zip(cams, res):
+        U = uniforms_for(cam, st)
+        ref = O.composite(O.vertex_stage(g.flat().astype(np.float32), g.sh_dim, U), U)
+        assert r["stats"]["n_instances"] > 0
+        compare_images(r["image"], ref, tol_max=TOL_MAX)
+        alone = gpu_frame(g, cam, RenderSettings(t_min=0.0))
+        compare_images(alone["image"], ref, tol_max=TOL_MAX)
+    scene.close()
