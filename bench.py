@@ -66,6 +66,18 @@ def make_scene(cfg, n, deg):
     return garden_standin(n, seed=seed, sh_degree=deg), f"synthetic: garden stand-in (seed {seed}), no PLY offline"
 
 
+def morton_order(xyz, bits=10):
+    """Permutation putting Gaussians in 3D Morton (Z-curve) order of their
+    positions (experiment: record gathers of spatially coherent scenes)."""
+    lo, hi = xyz.min(axis=0), xyz.max(axis=0)
+    q = ((xyz - lo) / np.maximum(hi - lo, 1e-12) * ((1 << bits) - 1)).astype(np.uint64)
+    code = np.zeros(len(xyz), np.uint64)
+    for b in range(bits):
+        for d in range(3):
+            code |= ((q[:, d] >> np.uint64(b)) & np.uint64(1)) << np.uint64(3 * b + d)
+    return np.argsort(code, kind="stable")
+
+
 def box_settings(g, kind):
     """SURVEY.md 8d C5 box cull settings (RenderSettings fields)."""
     if kind == "aabb":
@@ -280,6 +292,8 @@ def main():
     ap.add_argument("--box", default="none", choices=["none", "aabb", "obb"],
                     help="boundary-box cull (SURVEY.md 8d C5): aabb = compute_aabb min/max x 0.5 around "
                          "points_center; obb = euler(30, 15, 0) deg, +-1.5")
+    ap.add_argument("--scene-order", default="given", choices=["given", "morton"],
+                    help="experiment: render the scene with its Gaussians permuted into 3D Morton order")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank launch over gloo (no GPU, no rendering)")
     args = ap.parse_args()
@@ -331,6 +345,9 @@ def main():
     # ---- scene: generated on rank 0, broadcast once (RCCL over xGMI), untimed
     t_gen = time.perf_counter()
     g, data_desc = make_scene(args.config, n, deg) if rank == 0 else (None, None)
+    if g is not None and args.scene_order == "morton":  # experiment: spatially coherent Gaussian order
+        g = g[morton_order(g.xyz)]
+        data_desc += ", Gaussians in 3D Morton order"
     t_gen = time.perf_counter() - t_gen
     tensors, bcast = broadcast_scene(g, n, k_coef, dev)  # one RCCL broadcast at load (world > 1)
     scene = HipScene(*tensors)
