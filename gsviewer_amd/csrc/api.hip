@@ -743,13 +743,30 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
     if (n > 0) {
         if ((rc = launch_cull_views(sc->d, cull, k, s))) return rc;
         const size_t nw = (n + 63) / 64;
-        for (int v = 0; v < k; ++v) {
-            gsr_context* c = ctxs[v];
-            const ZeroLayout zl(u[v].tiles_x * u[v].tiles_y);
-            // visible-compaction offsets + V, and the frame's depth-key range
-            if ((rc = scan_exclusive(c->wave_counts.p, c->wave_counts.p, nw, c->scan_tmp.p, c->zero.p + zl.counters, s,
-                                     c->block_ranges.p, (n + kCullBlock - 1) / kCullBlock, c->zero.p + zl.key_range)))
-                return rc;
+        const size_t n_kr = (n + kCullBlock - 1) / kCullBlock;
+        // visible-compaction offsets + V, and the frame's depth-key range:
+        // one launch for the group when the arrays fit the one-pass scan
+        if (scan_views_fits(nw)) {
+            const uint32_t* in[GSR_MAX_VIEWS];
+            uint32_t *out[GSR_MAX_VIEWS], *tot[GSR_MAX_VIEWS], *kro[GSR_MAX_VIEWS];
+            const uint2* kri[GSR_MAX_VIEWS];
+            for (int v = 0; v < k; ++v) {
+                gsr_context* c = ctxs[v];
+                const ZeroLayout zl(u[v].tiles_x * u[v].tiles_y);
+                in[v] = out[v] = c->wave_counts.p;
+                tot[v] = c->zero.p + zl.counters;
+                kri[v] = c->block_ranges.p;
+                kro[v] = c->zero.p + zl.key_range;
+            }
+            if ((rc = scan_exclusive_views(in, out, nw, tot, kri, n_kr, kro, k, s))) return rc;
+        } else {
+            for (int v = 0; v < k; ++v) {
+                gsr_context* c = ctxs[v];
+                const ZeroLayout zl(u[v].tiles_x * u[v].tiles_y);
+                if ((rc = scan_exclusive(c->wave_counts.p, c->wave_counts.p, nw, c->scan_tmp.p, c->zero.p + zl.counters,
+                                         s, c->block_ranges.p, n_kr, c->zero.p + zl.key_range)))
+                    return rc;
+            }
         }
         if ((rc = launch_preprocess_views(sc->d, pre, k, s))) return rc;
     }

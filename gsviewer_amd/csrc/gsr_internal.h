@@ -172,6 +172,11 @@ size_t scan_tmp_elems(size_t n);
 int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
                    uint32_t* total_dev, hipStream_t s, const uint2* kr_in = nullptr,
                    size_t n_kr = 0, uint32_t* kr_out = nullptr);
+// The same for k views' arrays of n elements each in one launch (n <= 16384:
+// scan_views_fits), key ranges reduced alongside (kr_in/kr_out per view).
+bool scan_views_fits(size_t n);
+int scan_exclusive_views(const uint32_t* const* in, uint32_t* const* out, size_t n, uint32_t* const* total_dev,
+                         const uint2* const* kr_in, size_t n_kr, uint32_t* const* kr_out, int k, hipStream_t s);
 
 // radix_sort.hip: stable LSD sort of (key, val), `passes` passes of
 // w = ceil(B / passes) <= 11 bits, where B = `bits` (keys < 2^bits) or, when

@@ -183,6 +183,84 @@ __device__ __forceinline__ void scan_single(const uint32_t* __restrict__ in, uin
     if (threadIdx.x == 0 && total_dev) *total_dev = carry;
 }
 
+// One pass for arrays of at most NT * 16 elements (the visibility words of up
+// to ~1M Gaussians): each thread loads 16 contiguous elements (four dwordx4,
+// issued with the key-range loads), one block scan, 16 stores.  The chunked
+// loop above walks 4 chunks of 4096 with a block scan each (10 us for 15.6K
+// words; this: one round of loads and two barriers).
+constexpr int kOnePassItems = 16;
+
+template <int NT>
+__device__ __forceinline__ void scan_one_pass(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, size_t n,
+                                              uint32_t* __restrict__ total_dev, const uint2* __restrict__ kr_in,
+                                              size_t n_kr, uint32_t* __restrict__ kr_out, uint32_t* lds,
+                                              uint2* lds_kr) {
+    constexpr int IT = kOnePassItems;
+    const size_t base = (size_t)threadIdx.x * IT;
+    uint32_t v[IT];
+    const bool aligned = (reinterpret_cast<uintptr_t>(in) % 16 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0);
+    if (aligned && base + IT <= n) {
+        const uint4* p = reinterpret_cast<const uint4*>(in + base);
+#pragma unroll
+        for (int q = 0; q < IT / 4; ++q) {
+            const uint4 t = p[q];
+            v[4 * q + 0] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < IT; ++k) v[k] = (base + k < n) ? in[base + k] : 0u;
+    }
+    if (kr_in) reduce_ranges<NT>(kr_in, n_kr, kr_out, lds_kr);
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < IT; ++k) sum += v[k];
+    uint32_t total;
+    uint32_t run = block_exclusive<NT>(sum, lds, total);
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const uint32_t t = v[k];
+        v[k] = run;
+        run += t;
+    }
+    if (aligned && base + IT <= n) {
+        uint4* p = reinterpret_cast<uint4*>(out + base);
+#pragma unroll
+        for (int q = 0; q < IT / 4; ++q) p[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < IT; ++k)
+            if (base + k < n) out[base + k] = v[k];
+    }
+    if (threadIdx.x == 0 && total_dev) *total_dev = total;
+}
+
+__global__ __launch_bounds__(kPartialThreads) void k_scan_one_pass(const uint32_t* __restrict__ in,
+                                                                   uint32_t* __restrict__ out, size_t n,
+                                                                   uint32_t* __restrict__ total_dev,
+                                                                   const uint2* __restrict__ kr_in, size_t n_kr,
+                                                                   uint32_t* __restrict__ kr_out) {
+    __shared__ uint32_t lds[kPartialThreads / 64];
+    __shared__ uint2 lds_kr[kPartialThreads / 64];
+    scan_one_pass<kPartialThreads>(in, out, n, total_dev, kr_in, n_kr, kr_out, lds, lds_kr);
+}
+
+// The visibility scans of a group of views (gsr_render_begin_views) in one
+// launch, one workgroup per view (blockIdx.y).
+struct ScanViews {
+    const uint32_t* in[kMaxViews];
+    uint32_t* out[kMaxViews];
+    uint32_t* total[kMaxViews];
+    const uint2* kr_in[kMaxViews];
+    uint32_t* kr_out[kMaxViews];
+};
+
+__global__ __launch_bounds__(kPartialThreads) void k_scan_one_pass_views(ScanViews sv, size_t n, size_t n_kr) {
+    __shared__ uint32_t lds[kPartialThreads / 64];
+    __shared__ uint2 lds_kr[kPartialThreads / 64];
+    const int v = blockIdx.y;
+    scan_one_pass<kPartialThreads>(sv.in[v], sv.out[v], n, sv.total[v], sv.kr_in[v], n_kr, sv.kr_out[v], lds, lds_kr);
+}
+
 template <int NT>
 __global__ __launch_bounds__(NT) void k_scan_single(const uint32_t* __restrict__ in,
                                                                  uint32_t* __restrict__ out, size_t n,
@@ -212,6 +290,8 @@ int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
     if (n <= kSingleMax) {
         if (n <= kSmallScan)
             k_scan_single<kSingleThreads><<<1, kSingleThreads, 0, s>>>(in, out, n, total_dev, kr_in, n_kr, kr_out);
+        else if (n <= (size_t)kPartialThreads * kOnePassItems)
+            k_scan_one_pass<<<1, kPartialThreads, 0, s>>>(in, out, n, total_dev, kr_in, n_kr, kr_out);
         else
             k_scan_single<kPartialThreads><<<1, kPartialThreads, 0, s>>>(in, out, n, total_dev, kr_in, n_kr, kr_out);
         GSR_LAUNCH_CHECK("scan_single");
@@ -225,6 +305,25 @@ int scan_exclusive(const uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp,
     GSR_LAUNCH_CHECK("scan_partials");
     k_scan_final<<<dim3((unsigned)nb), dim3(kThreads), 0, s>>>(in, out, n, tmp);
     GSR_LAUNCH_CHECK("scan_final");
+    return GSR_OK;
+}
+
+bool scan_views_fits(size_t n) { return n > 0 && n <= (size_t)kPartialThreads * kOnePassItems; }
+
+int scan_exclusive_views(const uint32_t* const* in, uint32_t* const* out, size_t n, uint32_t* const* total_dev,
+                         const uint2* const* kr_in, size_t n_kr, uint32_t* const* kr_out, int k, hipStream_t s) {
+    if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "scan: view count out of range");
+    if (!scan_views_fits(n)) return set_error(GSR_ERR_INVALID, "scan: array too long for the batched one-pass scan");
+    ScanViews sv{};
+    for (int v = 0; v < k; ++v) {
+        sv.in[v] = in[v];
+        sv.out[v] = out[v];
+        sv.total[v] = total_dev[v];
+        sv.kr_in[v] = kr_in[v];
+        sv.kr_out[v] = kr_out[v];
+    }
+    k_scan_one_pass_views<<<dim3(1, (unsigned)k), kPartialThreads, 0, s>>>(sv, n, n_kr);
+    GSR_LAUNCH_CHECK("scan_one_pass_views");
     return GSR_OK;
 }
 
