@@ -360,44 +360,13 @@ __device__ __forceinline__ void load_gaussian(GaussLoad<DEG>& g, const float4* _
     }
 }
 
-template <int DEG>
-__device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, const FrameUniforms& u, uint64_t m,
-                                                       int64_t i, uint32_t slot_base, SplatRec* __restrict__ recs,
-                                                       uint32_t* __restrict__ depth_keys, uint2* __restrict__ trect,
-                                                       int32_t* __restrict__ radii);
+// The world-space covariance of a Gaussian: view-independent, so the views of
+// a group (k_preprocess_views) compute it once per Gaussian.
+struct Cov3 {
+    float S[3][3];
+};
 
-// Per-Gaussian body of k_preprocess for a visible lane; returns the number of
-// 16x16 tiles its covered pixel rectangle touches.
-template <int DEG>
-__device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ pos_op, const float4* __restrict__ rot,
-                                                  const float4* __restrict__ scale, const float4* __restrict__ sh,
-                                                  int64_t n, const FrameUniforms& u, uint64_t m, int64_t i,
-                                                  const uint32_t* __restrict__ wave_off,
-                                                  const uint32_t* __restrict__ n_vis_dev, SplatRec* __restrict__ recs,
-                                                  uint32_t* __restrict__ depth_keys, uint2* __restrict__ trect,
-                                                  int32_t* __restrict__ radii) {
-    GaussLoad<DEG> g;
-    load_gaussian<DEG>(g, pos_op, rot, scale, sh, n, i);
-    const uint32_t slot_base = n_vis_dev[0] - 1u - wave_off[i >> 6];
-    // keep the compiler from sinking the loads below the arithmetic (it would
-    // otherwise wait for pos/rot/scale before issuing the SH planes: two
-    // dependent memory round trips per wave instead of one)
-    __builtin_amdgcn_sched_barrier(0);
-    return preprocess_compute<DEG>(g, u, m, i, slot_base, recs, depth_keys, trect, radii);
-}
-
-// Everything after the loads: the vertex stage of one view for a visible lane.
-template <int DEG>
-__device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, const FrameUniforms& u, uint64_t m,
-                                                       int64_t i, uint32_t slot_base, SplatRec* __restrict__ recs,
-                                                       uint32_t* __restrict__ depth_keys, uint2* __restrict__ trect,
-                                                       int32_t* __restrict__ radii) {
-    const float4 po = g.po;
-    const float4 q1 = g.q1;
-    const float4 sc4 = g.sc4;
-    const float x = po.x, y = po.y, z = po.z;
-    const Projected pr = project(x, y, z, u);
-
+__device__ __forceinline__ Cov3 cov3d(const float4 q1, const float4 sc4, const FrameUniforms& u) {
     // quatMultiply(g_rot, rot_modifier) (gau_vert.glsl:134-141, :224)
     const float q1x = q1.x, q1y = q1.y, q1z = q1.z, q1w = q1.w;
     const float q2x = u.rotmod[0], q2y = u.rotmod[1], q2z = u.rotmod[2], q2w = u.rotmod[3];
@@ -426,6 +395,53 @@ __device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, 
             S[a][b] = (M[0][a] * M[0][b] + M[1][a] * M[1][b]) + M[2][a] * M[2][b];
             S[b][a] = S[a][b];
         }
+
+    Cov3 c;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) c.S[a][b] = S[a][b];
+    return c;
+}
+
+template <int DEG>
+__device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, const Cov3& S3, const FrameUniforms& u,
+                                                       uint64_t m, int64_t i, uint32_t slot_base,
+                                                       SplatRec* __restrict__ recs, uint32_t* __restrict__ depth_keys,
+                                                       uint2* __restrict__ trect, int32_t* __restrict__ radii);
+
+// Per-Gaussian body of k_preprocess for a visible lane; returns the number of
+// 16x16 tiles its covered pixel rectangle touches.
+template <int DEG>
+__device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ pos_op, const float4* __restrict__ rot,
+                                                  const float4* __restrict__ scale, const float4* __restrict__ sh,
+                                                  int64_t n, const FrameUniforms& u, uint64_t m, int64_t i,
+                                                  const uint32_t* __restrict__ wave_off,
+                                                  const uint32_t* __restrict__ n_vis_dev, SplatRec* __restrict__ recs,
+                                                  uint32_t* __restrict__ depth_keys, uint2* __restrict__ trect,
+                                                  int32_t* __restrict__ radii) {
+    GaussLoad<DEG> g;
+    load_gaussian<DEG>(g, pos_op, rot, scale, sh, n, i);
+    const uint32_t slot_base = n_vis_dev[0] - 1u - wave_off[i >> 6];
+    // keep the compiler from sinking the loads below the arithmetic (it would
+    // otherwise wait for pos/rot/scale before issuing the SH planes: two
+    // dependent memory round trips per wave instead of one)
+    __builtin_amdgcn_sched_barrier(0);
+    return preprocess_compute<DEG>(g, cov3d(g.q1, g.sc4, u), u, m, i, slot_base, recs, depth_keys, trect, radii);
+}
+
+// Everything after the loads: the vertex stage of one view for a visible lane
+// (S3: the Gaussian's covariance, cov3d).
+template <int DEG>
+__device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, const Cov3& S3, const FrameUniforms& u,
+                                                       uint64_t m, int64_t i, uint32_t slot_base,
+                                                       SplatRec* __restrict__ recs, uint32_t* __restrict__ depth_keys,
+                                                       uint2* __restrict__ trect, int32_t* __restrict__ radii) {
+    const float4 po = g.po;
+    const float x = po.x, y = po.y, z = po.z;
+    const Projected pr = project(x, y, z, u);
+
+    const float(&S)[3][3] = S3.S;
 
     // computeCov2D (gau_vert.glsl:97-122)
     const float fx = u.hfov[2], fy = u.hfov[2];
@@ -652,7 +668,11 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_views(const
         bool any = false;
         for (int v = 0; v < vs.k; ++v) any |= i < n && ((vs.v[v].vis_mask[i >> 6] >> lane) & 1ull);
         GaussLoad<DEG> g;
-        if (any) load_gaussian<DEG>(g, pos_op, rot, scale, sh, n, i);
+        Cov3 S3;
+        if (any) {
+            load_gaussian<DEG>(g, pos_op, rot, scale, sh, n, i);
+            S3 = cov3d(g.q1, g.sc4, vs.v[0].u);  // (the group shares rot_modifier and the scale factor)
+        }
 #pragma unroll 1
         for (int v = 0; v < vs.k; ++v) {
             const ViewPre& V = vs.v[v];
@@ -660,7 +680,7 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_views(const
             uint32_t tiles = 0;
             if ((m >> lane) & 1ull) {
                 const uint32_t slot_base = V.n_vis_dev[0] - 1u - V.wave_off[i >> 6];
-                tiles = preprocess_compute<DEG>(g, V.u, m, i, slot_base, V.recs, V.depth_keys, V.trect, V.radii);
+                tiles = preprocess_compute<DEG>(g, S3, V.u, m, i, slot_base, V.recs, V.depth_keys, V.trect, V.radii);
             } else if (i < n && V.radii) {
                 V.radii[i] = 0;
             }
