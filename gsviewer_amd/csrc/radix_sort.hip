@@ -37,7 +37,14 @@ constexpr int kRMin = 8;
 constexpr int kMinTileItems = kThreads * kRMin;  // sizes the digit matrix for any R
 constexpr int kMaxBits = 11;
 constexpr int kMaxRadix = 1 << kMaxBits;         // 2048
-constexpr int kDigitsPerThread = kMaxRadix / kThreads;  // 8
+// LDS of a pass is sized for its largest radix: the host picks R = 16 only for
+// digits of <= 8 bits (radix_sort_pairs), so those kernels size for 256
+// digits (about 20 KB less LDS per block: more blocks per CU beside the
+// compositor when views are in flight)
+template <int kR>
+constexpr int radix_cap() { return kR == 16 ? 256 : kMaxRadix; }
+template <int kR>
+constexpr int digits_per_thread() { return radix_cap<kR>() / kThreads; }
 
 struct PassArgs {
     const uint32_t* key_range;  // device {~kmin, kmax} or null (then kmin = 0 and B = bits)
@@ -88,7 +95,8 @@ __device__ __forceinline__ void rs_upsweep(const uint32_t* __restrict__ keys, co
                                            uint32_t n_host, const PassArgs& pa, uint32_t* __restrict__ hist,
                                            uint32_t ntiles, uint32_t tile) {
     constexpr int kTileItems = kThreads * kR;
-    __shared__ uint16_t h[kWaves][kMaxRadix];  // per-wave counts (<= 64*kR each)
+    constexpr int kCap = radix_cap<kR>();
+    __shared__ uint16_t h[kWaves][kCap];  // per-wave counts (<= 64*kR each)
     const Digit dg = digit_params(pa);
     const uint32_t radix = dg.mask + 1u;
     const uint32_t n = count_of(n_dev, n_host);
@@ -179,9 +187,17 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
     __shared__ uint32_t s_keys[kTileItems];
     __shared__ uint32_t s_vals[kTileItems];
     __shared__ uint32_t s_pay[kPay ? kTileItems : 1];
-    __shared__ uint16_t wcnt[kWaves][kMaxRadix];  // per-wave digit counts, then per-wave prefixes
-    __shared__ uint32_t dbase[kMaxRadix];         // tile-local exclusive digit offsets
-    __shared__ uint32_t gbase[kMaxRadix];         // global position of LDS index 0 of digit d's run
+    // per-wave digit counts, then per-wave prefixes; after the LDS staging the
+    // same bytes hold gbase[d], the global position of LDS index 0 of digit d's
+    // run (kept in registers until then): 8 KB less LDS per block, so 3
+    // blocks fit a CU instead of 2 for 2048-item tiles
+    constexpr int kCap = radix_cap<kR>();
+    constexpr int kDigitsPerThread = digits_per_thread<kR>();
+    __shared__ uint32_t wcnt_gbase[kWaves * kCap / 2];
+    static_assert(kWaves * kCap / 2 >= kCap, "gbase overlay");
+    uint16_t(&wcnt)[kWaves][kCap] = *reinterpret_cast<uint16_t(*)[kWaves][kCap]>(wcnt_gbase);
+    uint32_t* gbase = wcnt_gbase;
+    __shared__ uint32_t dbase[kCap];              // tile-local exclusive digit offsets
     __shared__ uint32_t wsum[2][kWaves];
 
     const uint32_t n = count_of(n_dev, n_host);
@@ -261,7 +277,7 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
             const uint32_t d = d0 + j;
             if (j < (int)q && d < radix) {
                 dbase[d] = e_loc;
-                gbase[d] = e_glob + ho[j] - e_loc;
+                ho[j] = e_glob + ho[j] - e_loc;  // gbase[d], stored after the staging
             }
             e_loc += tot[j];
             e_glob += gt[j];
@@ -278,6 +294,12 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
             s_vals[p] = v_reg[r];
             if constexpr (kPay) s_pay[p] = p_reg[r];
         }
+    }
+    __syncthreads();  // (every wcnt read is done: its bytes now take gbase)
+#pragma unroll
+    for (int j = 0; j < kDigitsPerThread; ++j) {
+        const uint32_t d = d0 + j;
+        if (j < (int)q && d < radix) gbase[d] = ho[j];
     }
     __syncthreads();
 
