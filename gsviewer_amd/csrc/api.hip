@@ -210,7 +210,15 @@ int build_uniforms(const gsr_scene* sc, const gsr_camera* cam, const gsr_setting
     return GSR_OK;
 }
 
-constexpr int kDepthPasses = 3;  // 32-bit depth keys: 3 passes of <= 11 bits (width chosen on the device)
+// 32-bit depth keys: 4 passes of <= 8 bits (width chosen on the device: a
+// camera's keys span ~24 bits, i.e. 6-bit digits).  3 passes of <= 11 bits
+// are 4 us faster alone, but their kernels need LDS for 2048 digits; with
+// views in flight the 8-bit kernels (28 KB per block, 5 blocks per CU beside
+// the compositor) win: 0.194 -> 0.187 ms per frame (profiles/r2_s24).
+#ifndef GSR_DEPTH_PASSES
+#define GSR_DEPTH_PASSES 4
+#endif
+constexpr int kDepthPasses = GSR_DEPTH_PASSES;
 
 int bits_for(uint32_t v) {  // bits needed to represent values < v
     int b = 0;

@@ -33,18 +33,34 @@ constexpr int kWaves = kThreads / 64;
 // tile holds 256*R items.  Bigger tiles mean longer digit runs in the
 // scatter's writes and a smaller digit matrix; the host picks R = 8 for wide
 // digits (depth keys, up to 11 bits) and R = 16 for narrow ones (tile ids).
-constexpr int kRMin = 8;
+// items per thread for wide digits (> 8 bits: the depth sort); build knob for A/B
+#ifndef GSR_WIDE_R
+#define GSR_WIDE_R 8
+#endif
+constexpr int kRWide = GSR_WIDE_R;
+// items per thread for device-chosen <= 8-bit digits (the depth sort); build knob for A/B
+#ifndef GSR_DEPTH_R
+#define GSR_DEPTH_R 8
+#endif
+constexpr int kRDepth = GSR_DEPTH_R;
+// items per thread for host-known <= 8-bit digits (the tile sort); build knob for A/B
+#ifndef GSR_TILE_R
+#define GSR_TILE_R 16
+#endif
+constexpr int kRTile = GSR_TILE_R;
+constexpr int kRMin = kRWide < kRDepth ? (kRWide < kRTile ? kRWide : kRTile) : (kRDepth < kRTile ? kRDepth : kRTile);
 constexpr int kMinTileItems = kThreads * kRMin;  // sizes the digit matrix for any R
+
 constexpr int kMaxBits = 11;
 constexpr int kMaxRadix = 1 << kMaxBits;         // 2048
-// LDS of a pass is sized for its largest radix: the host picks R = 16 only for
-// digits of <= 8 bits (radix_sort_pairs), so those kernels size for 256
-// digits (about 20 KB less LDS per block: more blocks per CU beside the
-// compositor when views are in flight)
-template <int kR>
-constexpr int radix_cap() { return kR == 16 ? 256 : kMaxRadix; }
-template <int kR>
-constexpr int digits_per_thread() { return radix_cap<kR>() / kThreads; }
+// LDS of a pass is sized for its largest radix (kCB: cap bits): the host
+// knows the widest digit a sort can have (ceil(bits / passes)), and sorts of
+// <= 8-bit digits use kernels sized for 256 digits (about 20 KB less LDS per
+// block: more blocks per CU beside the compositor when views are in flight)
+template <int kCB>
+constexpr int radix_cap() { return 1 << kCB; }
+template <int kCB>
+constexpr int digits_per_thread() { return radix_cap<kCB>() / kThreads; }
 
 struct PassArgs {
     const uint32_t* key_range;  // device {~kmin, kmax} or null (then kmin = 0 and B = bits)
@@ -90,12 +106,12 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t digit, uint32_t w, bool
     return peers;
 }
 
-template <int kR>
+template <int kR, int kCB>
 __device__ __forceinline__ void rs_upsweep(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ n_dev,
                                            uint32_t n_host, const PassArgs& pa, uint32_t* __restrict__ hist,
                                            uint32_t ntiles, uint32_t tile) {
     constexpr int kTileItems = kThreads * kR;
-    constexpr int kCap = radix_cap<kR>();
+    constexpr int kCap = radix_cap<kCB>();
     __shared__ uint16_t h[kWaves][kCap];  // per-wave counts (<= 64*kR each)
     const Digit dg = digit_params(pa);
     const uint32_t radix = dg.mask + 1u;
@@ -129,11 +145,11 @@ __device__ __forceinline__ void rs_upsweep(const uint32_t* __restrict__ keys, co
     }
 }
 
-template <int kR>
+template <int kR, int kCB>
 __global__ __launch_bounds__(kThreads) void k_rs_upsweep(const uint32_t* __restrict__ keys,
                                                          const uint32_t* __restrict__ n_dev, uint32_t n_host,
                                                          PassArgs pa, uint32_t* __restrict__ hist, uint32_t ntiles) {
-    rs_upsweep<kR>(keys, n_dev, n_host, pa, hist, ntiles, blockIdx.x);
+    rs_upsweep<kR, kCB>(keys, n_dev, n_host, pa, hist, ntiles, blockIdx.x);
 }
 
 // One wave per digit d: exclusive scan of row d (ntiles counts) in place; row total out.
@@ -173,7 +189,7 @@ __device__ __forceinline__ uint32_t pack_rect(uint2 tr) {
 // the depth sort, so the binning reads it in sorted order instead of
 // gathering it by id).  Its first pass reads the rectangles (rect_in, in
 // input order) and packs them; later passes read pay_in.
-template <int kR, bool kPay>
+template <int kR, bool kPay, int kCB>
 __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
                                            bool identity_vals, uint32_t* __restrict__ keys_out,
                                            uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ n_dev,
@@ -191,8 +207,8 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
     // same bytes hold gbase[d], the global position of LDS index 0 of digit d's
     // run (kept in registers until then): 8 KB less LDS per block, so 3
     // blocks fit a CU instead of 2 for 2048-item tiles
-    constexpr int kCap = radix_cap<kR>();
-    constexpr int kDigitsPerThread = digits_per_thread<kR>();
+    constexpr int kCap = radix_cap<kCB>();
+    constexpr int kDigitsPerThread = digits_per_thread<kCB>();
     __shared__ uint32_t wcnt_gbase[kWaves * kCap / 2];
     static_assert(kWaves * kCap / 2 >= kCap, "gbase overlay");
     uint16_t(&wcnt)[kWaves][kCap] = *reinterpret_cast<uint16_t(*)[kWaves][kCap]>(wcnt_gbase);
@@ -313,14 +329,14 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
     }
 }
 
-template <int kR, bool kPay>
+template <int kR, bool kPay, int kCB>
 __global__ __launch_bounds__(kThreads) void k_rs_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, bool identity_vals,
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* __restrict__ n_dev,
     uint32_t n_host, PassArgs pa, const uint32_t* __restrict__ hist_off, const uint32_t* __restrict__ totals,
     uint32_t ntiles, const uint2* __restrict__ rect_in, const uint32_t* __restrict__ pay_in,
     uint32_t* __restrict__ pay_out) {
-    rs_scatter<kR, kPay>(keys_in, vals_in, identity_vals, keys_out, vals_out, n_dev, n_host, pa, hist_off, totals,
+    rs_scatter<kR, kPay, kCB>(keys_in, vals_in, identity_vals, keys_out, vals_out, n_dev, n_host, pa, hist_off, totals,
                          ntiles, blockIdx.x, rect_in, pay_in, pay_out);
 }
 
@@ -343,10 +359,10 @@ struct SortViews {
     SortView v[kMaxViews];
 };
 
-template <int kR>
+template <int kR, int kCB>
 __global__ __launch_bounds__(kThreads) void k_rs_upsweep_views(SortViews sv, uint32_t n_host, uint32_t ntiles) {
     const SortView& v = sv.v[blockIdx.y];
-    rs_upsweep<kR>(v.keys_in, v.n_dev, n_host, v.pa, v.hist, ntiles, blockIdx.x);
+    rs_upsweep<kR, kCB>(v.keys_in, v.n_dev, n_host, v.pa, v.hist, ntiles, blockIdx.x);
 }
 
 __global__ __launch_bounds__(64) void k_rs_offsets_views(SortViews sv, uint32_t ntiles) {
@@ -354,11 +370,11 @@ __global__ __launch_bounds__(64) void k_rs_offsets_views(SortViews sv, uint32_t 
     rs_offsets(v.hist, ntiles, v.pa, v.totals, blockIdx.x);
 }
 
-template <int kR, bool kPay>
+template <int kR, bool kPay, int kCB>
 __global__ __launch_bounds__(kThreads) void k_rs_scatter_views(SortViews sv, bool identity_vals, uint32_t n_host,
                                                                uint32_t ntiles) {
     const SortView& v = sv.v[blockIdx.y];
-    rs_scatter<kR, kPay>(v.keys_in, v.vals_in, identity_vals, v.keys_out, v.vals_out, v.n_dev, n_host, v.pa, v.hist,
+    rs_scatter<kR, kPay, kCB>(v.keys_in, v.vals_in, identity_vals, v.keys_out, v.vals_out, v.n_dev, n_host, v.pa, v.hist,
                          v.totals, ntiles, blockIdx.x, v.rect_in, v.pay_in, v.pay_out);
 }
 
@@ -373,7 +389,7 @@ size_t radix_totals_elems() { return (size_t)kMaxRadix; }  // digit totals scrat
 
 int radix_passes_for(int bits) { return bits <= 0 ? 0 : (bits + kMaxBits - 1) / kMaxBits; }
 
-template <int kR>
+template <int kR, int kCB>
 static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
                        bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
                        const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s,
@@ -385,16 +401,16 @@ static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_a
     bool ident = identity_vals;
     for (int p = 0; p < passes; ++p) {
         const PassArgs pa{key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p};
-        k_rs_upsweep<kR><<<nt, kThreads, 0, s>>>(*keys_io, n_dev, (uint32_t)n, pa, tmp, nt);
+        k_rs_upsweep<kR, kCB><<<nt, kThreads, 0, s>>>(*keys_io, n_dev, (uint32_t)n, pa, tmp, nt);
         GSR_LAUNCH_CHECK("rs_upsweep");
         k_rs_offsets<<<radix_max, 64, 0, s>>>(tmp, nt, pa, totals);
         GSR_LAUNCH_CHECK("rs_offsets");
         if (rect_in) {
-            k_rs_scatter<kR, true><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev,
+            k_rs_scatter<kR, true, kCB><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev,
                                                            (uint32_t)n, pa, tmp, totals, nt, p == 0 ? rect_in : nullptr,
                                                            *pay_io, *pay_alt);
         } else {
-            k_rs_scatter<kR, false><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev,
+            k_rs_scatter<kR, false, kCB><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev,
                                                             (uint32_t)n, pa, tmp, totals, nt, nullptr, nullptr,
                                                             nullptr);
         }
@@ -409,7 +425,7 @@ static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_a
     return GSR_OK;
 }
 
-template <int kR>
+template <int kR, int kCB>
 static int sort_passes_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
                              hipStream_t s) {
     constexpr int kTileItems = kThreads * kR;
@@ -426,14 +442,14 @@ static int sort_passes_views(RadixViewArgs* views, int k, bool identity_vals, si
                                a.rect_in ? *a.pay_alt : nullptr};
         }
         const bool pay = views[0].rect_in != nullptr;  // all views or none (radix_sort_pairs_views)
-        k_rs_upsweep_views<kR><<<dim3(nt, k), kThreads, 0, s>>>(sv, (uint32_t)n, nt);
+        k_rs_upsweep_views<kR, kCB><<<dim3(nt, k), kThreads, 0, s>>>(sv, (uint32_t)n, nt);
         GSR_LAUNCH_CHECK("rs_upsweep_views");
         k_rs_offsets_views<<<dim3(radix_max, k), 64, 0, s>>>(sv, nt);
         GSR_LAUNCH_CHECK("rs_offsets_views");
         if (pay)
-            k_rs_scatter_views<kR, true><<<dim3(nt, k), kThreads, 0, s>>>(sv, ident, (uint32_t)n, nt);
+            k_rs_scatter_views<kR, true, kCB><<<dim3(nt, k), kThreads, 0, s>>>(sv, ident, (uint32_t)n, nt);
         else
-            k_rs_scatter_views<kR, false><<<dim3(nt, k), kThreads, 0, s>>>(sv, ident, (uint32_t)n, nt);
+            k_rs_scatter_views<kR, false, kCB><<<dim3(nt, k), kThreads, 0, s>>>(sv, ident, (uint32_t)n, nt);
         GSR_LAUNCH_CHECK("rs_scatter_views");
         ident = false;
         for (int v = 0; v < k; ++v) {
@@ -458,8 +474,10 @@ int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size
     for (int v = 1; v < k; ++v)
         if ((views[v].rect_in != nullptr) != (views[0].rect_in != nullptr))
             return set_error(GSR_ERR_INVALID, "radix sort: payload on some views only");
-    if ((bits + passes - 1) / passes <= 8) return sort_passes_views<16>(views, k, identity_vals, n, bits, passes, s);
-    return sort_passes_views<8>(views, k, identity_vals, n, bits, passes, s);
+    if ((bits + passes - 1) / passes <= 8)
+        return views[0].key_range ? sort_passes_views<kRDepth, 8>(views, k, identity_vals, n, bits, passes, s)
+                                  : sort_passes_views<kRTile, 8>(views, k, identity_vals, n, bits, passes, s);
+    return sort_passes_views<kRWide, kMaxBits>(views, k, identity_vals, n, bits, passes, s);
 }
 
 int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
@@ -470,12 +488,17 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
     if (n > 0xffffffffull - 4 * kMinTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
     if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
         return set_error(GSR_ERR_INVALID, "radix sort: digit width out of range");
-    // measured on MI355X: 2048-item tiles for wide digits, 4096 for <= 8-bit digits
-    if ((bits + passes - 1) / passes <= 8)
-        return sort_passes<16>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes, key_range,
-                               tmp, totals, s, rect_in, pay_io, pay_alt);
-    return sort_passes<8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes, key_range, tmp,
-                          totals, s, rect_in, pay_io, pay_alt);
+    // measured on MI355X: 2048-item tiles for wide digits and for device-chosen
+    // widths (the depth sort), 4096 for host-known <= 8-bit digits (the tile sort)
+    if ((bits + passes - 1) / passes <= 8) {
+        if (key_range)
+            return sort_passes<kRDepth, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
+                                     key_range, tmp, totals, s, rect_in, pay_io, pay_alt);
+        return sort_passes<kRTile, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
+                                  key_range, tmp, totals, s, rect_in, pay_io, pay_alt);
+    }
+    return sort_passes<kRWide, kMaxBits>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
+                                         key_range, tmp, totals, s, rect_in, pay_io, pay_alt);
 }
 
 }  // namespace gsr

@@ -1,5 +1,5 @@
 """Busy fraction and concurrency of the views-in-flight region of a rocprofv3
-kernel trace (tooling): python tools/timeline.py prof_kernel_trace.csv"""
+kernel trace (tooling): python tools/timeline.py prof_kernel_trace.csv [groups] [views_per_group]"""
 import csv
 import sys
 from collections import defaultdict
@@ -18,6 +18,7 @@ ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel
 views = [e for e in ev if "_views" in e[2]]
 # the timed region: the last `groups` groups of views (default 13 = 50 frames of 4-view groups)
 groups = int(sys.argv[2]) if len(sys.argv) > 2 else 13
+vpg = int(sys.argv[3]) if len(sys.argv) > 3 else 4
 culls = [e for e in views if e[2].startswith("k_cull_views")]
 merges = [e for e in views if e[2].startswith("k_merge_views")]
 t0, t1 = culls[-groups][0], merges[-1][1]
@@ -34,13 +35,13 @@ busy += ce - cs
 span = t1 - t0
 tot = sum(e - s for s, e, n in seg)
 nc = sum(1 for e in seg if e[2].startswith("k_composite_views"))
-print(f"span {span/1e3:.1f} us, busy {busy/span:.3f}, sum(kernel)/span {tot/span:.2f}, frames {4*nc}, "
-      f"us/frame {span/1e3/(4*nc):.1f}")
+print(f"span {span/1e3:.1f} us, busy {busy/span:.3f}, sum(kernel)/span {tot/span:.2f}, frames {vpg*nc}, "
+      f"us/frame {span/1e3/(vpg*nc):.1f}")
 d = defaultdict(int)
 for s, e, n in seg:
     d[n] += e - s
 for n, v in sorted(d.items(), key=lambda x: -x[1])[:16]:
-    print(f"  {n:28s} share {v/tot:.3f}  {v/1e3/(4*nc):7.1f} us/frame of kernel time")
+    print(f"  {n:28s} share {v/tot:.3f}  {v/1e3/(vpg*nc):7.1f} us/frame of kernel time")
 ts = np.linspace(t0, t1, 4000)
 st = np.array([s for s, e, n in seg])
 en = np.array([e for s, e, n in seg])
