@@ -179,12 +179,40 @@ __global__ __launch_bounds__(kThreads) void k_bin_write_views(BinViews vs, int t
                        v.tile_vals, blockIdx.x, lds);
 }
 
+// Tile ranges from the tile-sorted keys: kRangeItems consecutive instances per
+// thread (four dwordx4 loads plus the two neighbours), a write at each tile
+// boundary only.  (One instance per thread meant 7K blocks per view at 1080p,
+// each doing almost nothing: with views in flight they queued behind the
+// compositors for CU slots.)
+constexpr int kRangeItems = 16;
+
 __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, uint32_t n, uint2* __restrict__ ranges,
-                                            uint32_t i) {
-    if (i >= n) return;
-    const uint32_t k = keys[i];
-    if (i == 0 || keys[i - 1] != k) ranges[k].x = i;
-    if (i == n - 1 || keys[i + 1] != k) ranges[k].y = i + 1;
+                                            uint32_t t) {
+    const uint32_t base = t * kRangeItems;
+    if (base >= n) return;
+    uint32_t k[kRangeItems];
+    if (base + kRangeItems <= n) {
+        const uint4* p = reinterpret_cast<const uint4*>(keys + base);  // (base: a multiple of 16)
+#pragma unroll
+        for (int q = 0; q < kRangeItems / 4; ++q) {
+            const uint4 v = p[q];
+            k[4 * q] = v.x; k[4 * q + 1] = v.y; k[4 * q + 2] = v.z; k[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kRangeItems; ++j) k[j] = base + j < n ? keys[base + j] : 0xffffffffu;
+    }
+    const uint32_t prev = base > 0 ? keys[base - 1] : 0xffffffffu;
+    const uint32_t next = base + kRangeItems < n ? keys[base + kRangeItems] : 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < kRangeItems; ++j) {
+        const uint32_t i = base + j;
+        if (i >= n) break;
+        const uint32_t before = j == 0 ? prev : k[j - 1];
+        const uint32_t after = (j + 1 < kRangeItems) ? (i + 1 < n ? k[j + 1] : 0xffffffffu) : next;
+        if (i == 0 || before != k[j]) ranges[k[j]].x = i;
+        if (i == n - 1 || after != k[j]) ranges[k[j]].y = i + 1;
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void k_tile_ranges(const uint32_t* __restrict__ keys, uint32_t n,
@@ -1150,7 +1178,8 @@ int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_
 
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, hipStream_t s) {
     if (n_dup == 0) return GSR_OK;
-    k_tile_ranges<<<(n_dup + kThreads - 1) / kThreads, kThreads, 0, s>>>(tile_keys, n_dup, ranges);
+    const uint32_t per_block = kThreads * kRangeItems;
+    k_tile_ranges<<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges);
     GSR_LAUNCH_CHECK("tile_ranges");
     return GSR_OK;
 }
@@ -1283,7 +1312,8 @@ int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s) {
         n_max = std::max(n_max, views[i].n_dup);
     }
     if (n_max == 0) return GSR_OK;
-    k_tile_ranges_views<<<dim3((n_max + kThreads - 1) / kThreads, (unsigned)k), kThreads, 0, s>>>(rv);
+    const uint32_t per_block = kThreads * kRangeItems;
+    k_tile_ranges_views<<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
     GSR_LAUNCH_CHECK("tile_ranges_views");
     return GSR_OK;
 }

@@ -11,7 +11,7 @@
 // One pass = three launches over tiles of 256*R items:
 //   k_rs_upsweep   per-tile digit counts (wave ballot digit matching, no
 //                  atomics), stored digit-major: hist[d * ntiles + tile];
-//   k_rs_offsets   one wave per digit: exclusive scan of that digit's row
+//   k_rs_offsets   one wave per digit (4 per block): exclusive scan of that digit's row
 //                  (in place) and the row total;
 //   k_rs_scatter   digit bases (block scan of the row totals), stable in-tile
 //                  ranks (waves own consecutive 64*R-item ranges, R rounds of
@@ -173,9 +173,13 @@ __device__ __forceinline__ void rs_offsets(uint32_t* __restrict__ hist, uint32_t
     if (__lane_id() == 63) totals[d] = inc;
 }
 
-__global__ __launch_bounds__(64) void k_rs_offsets(uint32_t* __restrict__ hist, uint32_t ntiles, PassArgs pa,
-                                                   uint32_t* __restrict__ totals) {
-    rs_offsets(hist, ntiles, pa, totals, blockIdx.x);
+// 4 digits per 256-thread block (one wave each): a quarter of the workgroups
+// of one-wave blocks, which queued for CU slots behind other views' kernels
+constexpr int kOffWaves = 4;
+
+__global__ __launch_bounds__(64 * kOffWaves) void k_rs_offsets(uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                               PassArgs pa, uint32_t* __restrict__ totals) {
+    rs_offsets(hist, ntiles, pa, totals, blockIdx.x * kOffWaves + (threadIdx.x >> 6));
 }
 
 // Tile rectangle of a splat packed in 32 bits (tx0 | tx1 << 8 | ty0 << 16 |
@@ -365,9 +369,9 @@ __global__ __launch_bounds__(kThreads) void k_rs_upsweep_views(SortViews sv, uin
     rs_upsweep<kR, kCB>(v.keys_in, v.n_dev, n_host, v.pa, v.hist, ntiles, blockIdx.x);
 }
 
-__global__ __launch_bounds__(64) void k_rs_offsets_views(SortViews sv, uint32_t ntiles) {
+__global__ __launch_bounds__(64 * kOffWaves) void k_rs_offsets_views(SortViews sv, uint32_t ntiles) {
     const SortView& v = sv.v[blockIdx.y];
-    rs_offsets(v.hist, ntiles, v.pa, v.totals, blockIdx.x);
+    rs_offsets(v.hist, ntiles, v.pa, v.totals, blockIdx.x * kOffWaves + (threadIdx.x >> 6));
 }
 
 template <int kR, bool kPay, int kCB>
@@ -403,7 +407,7 @@ static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_a
         const PassArgs pa{key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p};
         k_rs_upsweep<kR, kCB><<<nt, kThreads, 0, s>>>(*keys_io, n_dev, (uint32_t)n, pa, tmp, nt);
         GSR_LAUNCH_CHECK("rs_upsweep");
-        k_rs_offsets<<<radix_max, 64, 0, s>>>(tmp, nt, pa, totals);
+        k_rs_offsets<<<(radix_max + kOffWaves - 1) / kOffWaves, 64 * kOffWaves, 0, s>>>(tmp, nt, pa, totals);
         GSR_LAUNCH_CHECK("rs_offsets");
         if (rect_in) {
             k_rs_scatter<kR, true, kCB><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev,
@@ -444,7 +448,7 @@ static int sort_passes_views(RadixViewArgs* views, int k, bool identity_vals, si
         const bool pay = views[0].rect_in != nullptr;  // all views or none (radix_sort_pairs_views)
         k_rs_upsweep_views<kR, kCB><<<dim3(nt, k), kThreads, 0, s>>>(sv, (uint32_t)n, nt);
         GSR_LAUNCH_CHECK("rs_upsweep_views");
-        k_rs_offsets_views<<<dim3(radix_max, k), 64, 0, s>>>(sv, nt);
+        k_rs_offsets_views<<<dim3((radix_max + kOffWaves - 1) / kOffWaves, k), 64 * kOffWaves, 0, s>>>(sv, nt);
         GSR_LAUNCH_CHECK("rs_offsets_views");
         if (pay)
             k_rs_scatter_views<kR, true, kCB><<<dim3(nt, k), kThreads, 0, s>>>(sv, ident, (uint32_t)n, nt);
