@@ -112,8 +112,12 @@ struct gsr_context {
     gsr::DevBuf<uint32_t> chunk_order;            // per chunk: dispatch position -> chunk slot
     gsr::DevBuf<float4> partial;                  // per chunk x 256 px (multi-chunk tiles)
     gsr::DevBuf<float4> tmax;                     // per chunk: published slice maxima of local T
-    uint32_t chunk = 192;                         // instances per compositing chunk (swept, 4 views in flight:
-                                                  // 192-256 best throughput (fewer partials), 128 best latency)
+    uint32_t chunk = 192;                         // instances per compositing chunk of a frame finished alone
+                                                  // (gsr_render / gsr_render_finish): latency (r2_s17 sweep)
+    uint32_t chunk_views = 3072;                  // ... of a group's frames (gsr_render_finish_views): with
+                                                  // views in flight the other views fill the chip while a
+                                                  // deep tile's long chunk runs, so few chunks (fewer partials,
+                                                  // merges, descriptors) win (r2_s28 sweep)
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
     uint32_t seq = 0;                       // frame sequence number the host waits for
     uint32_t* host_counters_dev = nullptr;  // its device address
@@ -561,6 +565,10 @@ int gsr_context_create(gsr_context** out) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 16 && v <= (1 << 20)) (*out)->chunk = (uint32_t)v;
     }
+    if (const char* e = std::getenv("GSR_CHUNK_VIEWS")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 16 && v <= (1 << 20)) (*out)->chunk_views = (uint32_t)v;
+    }
     if (const char* e = std::getenv("GSR_WAIT_TIMEOUT_MS")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1) (*out)->wait_timeout_ms = v;
@@ -605,7 +613,7 @@ int gsr_context_reserve(gsr_context* c, int64_t n, int32_t width, int32_t height
     if ((rc = c->tvals_a.ensure(d, "tile_vals"))) return rc;
     if ((rc = c->tvals_b.ensure(d, "tile_vals"))) return rc;
     if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(d), radix_tmp_elems(un)), "radix_tmp"))) return rc;
-    const size_t mc = (size_t)num_tiles + d / c->chunk + 1;
+    const size_t mc = (size_t)num_tiles + d / std::min(c->chunk, c->chunk_views) + 1;
     if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
     if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
     if ((rc = c->chunk_desc.ensure(mc, "chunk_desc"))) return rc;
@@ -951,7 +959,7 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
             if (ctxs[w] == c) return set_error(GSR_ERR_INVALID, "render_finish_views: contexts must differ");
         if (f.u.width != f0.u.width || f.u.height != f0.u.height || f.t_min != f0.t_min || f.bg[0] != f0.bg[0] ||
             f.bg[1] != f0.bg[1] || f.bg[2] != f0.bg[2] || f.out_layout != f0.out_layout || f.blend != f0.blend ||
-            frag_class_of(f.u.render_mod) != frag_class_of(f0.u.render_mod) || c->chunk != c0->chunk)
+            frag_class_of(f.u.render_mod) != frag_class_of(f0.u.render_mod) || c->chunk_views != c0->chunk_views)
             return set_error(GSR_ERR_INVALID, "render_finish_views: views differ in frame size or settings");
     }
     const FrameUniforms& u0 = c0->pend.u;
@@ -983,7 +991,7 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
             if ((rc = c->tvals_a.ensure(n_dup, "tile_vals"))) return rc;
             if ((rc = c->tvals_b.ensure(n_dup, "tile_vals"))) return rc;
         }
-        const size_t mc = (size_t)num_tiles + n_dup / c->chunk + 1;
+        const size_t mc = (size_t)num_tiles + n_dup / c->chunk_views + 1;
         max_chunks = std::max(max_chunks, mc);
         if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
         if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
@@ -1028,7 +1036,7 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
                                               frag_class_of(u0.render_mod), f0.bg, f0.out_layout, fv[v].out, s)))
                 return rc;
     } else {
-        if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk, s))) return rc;
+        if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk_views, s))) return rc;
         if ((rc = launch_composite_views(fv, k, (uint32_t)max_chunks, u0, frag_class_of(u0.render_mod), f0.t_min,
                                          f0.bg, f0.out_layout, s)))
             return rc;

@@ -191,7 +191,10 @@ int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream);
 /* gsr_render_finish for k begun frames pending on the same `stream` (e.g. the
  * views of one gsr_render_begin_sorts): binning, tile sort, compositing and
  * merge run as one launch per step for all k.  The views must share frame
- * size, t_min, background, output layout, fragment mode and chunk length.
+ * size, t_min, background, output layout, fragment mode and chunk length.  A group's frames are
+ * composited in chunks of GSR_CHUNK_VIEWS instances (default 3072: views in flight fill the chip
+ * while a deep tile's chunk runs), a frame finished alone in chunks of GSR_CHUNK (default 192:
+ * latency); both read when the context is created.
  * Results are identical to k gsr_render_finish calls. */
 int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream);
 

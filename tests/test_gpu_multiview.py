@@ -11,6 +11,17 @@ from gsviewer_amd.gaussian_data import garden_standin
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _same_chunk_length(monkeypatch):
+    """Frames finished alone use GSR_CHUNK (default 192) and a group's frames
+    GSR_CHUNK_VIEWS (default 3072); with t_min > 0 the chunking decides where
+    compositing stops (within t_min), so the bit-identity checks here give
+    both paths one length, short enough that busy tiles take the multi-chunk
+    merge in both."""
+    monkeypatch.setenv("GSR_CHUNK", "256")
+    monkeypatch.setenv("GSR_CHUNK_VIEWS", "256")
+
+
 def _setup(n_views, h=180, w=320, n=60_000):
     import torch
 
