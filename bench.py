@@ -310,9 +310,7 @@ def main():
     share = args.share if args.share is not None else (
         args.inflight // 4 if args.inflight % 4 == 0 and 8 <= args.inflight <= 32 else 1)
     share = max(1, share)
-    if args.inflight % share:
-        ap.error("--inflight must be a multiple of --share")
-    want_q = min(32, max(8, args.inflight // share + 2))  # one stream per view (share 1) or per group
+    want_q = min(32, max(8, -(-args.inflight // share) + 2))  # one stream per view (share 1) or per group
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < want_q:
         os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)
 
@@ -379,6 +377,7 @@ def main():
     if share == 1:
         pipe = ViewPipeline(ctxs, streams, scene, camcs, st, outs)
     else:
+        # groups of `share` views (the last one may be smaller), one stream each
         groups = [(ctxs[g:g + share], camcs[g:g + share], outs[g:g + share], streams[g])
                   for g in range(0, K, share)]
         pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=not args.no_batched_sorts,
@@ -387,7 +386,7 @@ def main():
     def serial_frame():
         render_into(ctx, scene, camc, st, outs[0])
 
-    for _ in range(max(args.warmup // share, 2 * K // share)):
+    for _ in range(max(args.warmup // share, 2 * ((K + share - 1) // share))):
         pipe.step()
     pipe.drain()
     torch.cuda.synchronize()
@@ -404,11 +403,18 @@ def main():
     if share == 1:
         elapsed = timed_region(lambda: pipelined(args.steps), 1, dev, own)
     else:
-        # a step renders a group of `share` frames: time whole steps covering
-        # args.steps frames, normalised to args.steps frames
-        calls = (args.steps + share - 1) // share
-        elapsed = timed_region(lambda: pipelined(calls), 1, dev, own) * args.steps / (calls * share)
-        own[0] *= args.steps / (calls * share)
+        # a step renders one group's frames (groups in round-robin order from
+        # group 0 after the drain): time the whole steps covering args.steps
+        # frames -- exactly args.steps when the group sizes add up to it (the
+        # defaults do for multiples of --inflight), else normalised to it
+        sizes = [len(gr[0]) for gr in groups]
+        calls, timed_frames = 0, 0
+        while timed_frames < args.steps:
+            timed_frames += sizes[calls % len(sizes)]
+            calls += 1
+        pipe.next = 0
+        elapsed = timed_region(lambda: pipelined(calls), 1, dev, own) * args.steps / timed_frames
+        own[0] *= args.steps / timed_frames
     # single-view latency: the same number of frames of view 0, one at a time
     latency = timed_region(serial_frame, args.steps, dev) if K > 1 else elapsed
 
@@ -517,7 +523,8 @@ def main():
                    "t_min": args.t_min,
                    "parallelism": f"replicated scene, {world * K} independent views ({K} per GPU in flight)"
                                   + (f", cull + preprocess shared by groups of {share} views (one scene pass "
-                                     f"per group)" if share > 1 else "")},
+                                     f"per group; the last group {K - share * ((K - 1) // share)})"
+                                     if share > 1 else "")},
         "frame_stats": stats,
         "stage_ms": stage,
         "roofline": roof,
