@@ -118,6 +118,9 @@ struct gsr_context {
                                                   // views in flight the other views fill the chip while a
                                                   // deep tile's long chunk runs, so few chunks (fewer partials,
                                                   // merges, descriptors) win (r2_s28 sweep)
+    uint32_t len_classes = 8;                     // compositing dispatch order: full chunks, then the partial
+                                                  // ones in len_classes - 1 length classes, longest first
+    bool views_interleave = true;                 // a group's compositing dispatch class-major over its views
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
     uint32_t seq = 0;                       // frame sequence number the host waits for
     uint32_t* host_counters_dev = nullptr;  // its device address
@@ -569,6 +572,11 @@ int gsr_context_create(gsr_context** out) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 16 && v <= (1 << 20)) (*out)->chunk_views = (uint32_t)v;
     }
+    if (const char* e = std::getenv("GSR_LEN_CLASSES")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 2 && v <= gsr::kMaxLenClasses) (*out)->len_classes = (uint32_t)v;
+    }
+    if (const char* e = std::getenv("GSR_VIEWS_INTERLEAVE")) (*out)->views_interleave = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_WAIT_TIMEOUT_MS")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1) (*out)->wait_timeout_ms = v;
@@ -910,7 +918,7 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         if ((rc = c->chunk_order.ensure(max_chunks, "chunk_order"))) return rc;
         if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
         if ((rc = c->tmax.ensure(max_chunks, "tmax"))) return rc;
-        if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
+        if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->len_classes, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
                                 c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s)))
             return rc;
         if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
@@ -959,7 +967,8 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
             if (ctxs[w] == c) return set_error(GSR_ERR_INVALID, "render_finish_views: contexts must differ");
         if (f.u.width != f0.u.width || f.u.height != f0.u.height || f.t_min != f0.t_min || f.bg[0] != f0.bg[0] ||
             f.bg[1] != f0.bg[1] || f.bg[2] != f0.bg[2] || f.out_layout != f0.out_layout || f.blend != f0.blend ||
-            frag_class_of(f.u.render_mod) != frag_class_of(f0.u.render_mod) || c->chunk_views != c0->chunk_views)
+            frag_class_of(f.u.render_mod) != frag_class_of(f0.u.render_mod) || c->chunk_views != c0->chunk_views ||
+            c->len_classes != c0->len_classes)
             return set_error(GSR_ERR_INVALID, "render_finish_views: views differ in frame size or settings");
     }
     const FrameUniforms& u0 = c0->pend.u;
@@ -1036,9 +1045,9 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
                                               frag_class_of(u0.render_mod), f0.bg, f0.out_layout, fv[v].out, s)))
                 return rc;
     } else {
-        if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk_views, s))) return rc;
-        if ((rc = launch_composite_views(fv, k, (uint32_t)max_chunks, u0, frag_class_of(u0.render_mod), f0.t_min,
-                                         f0.bg, f0.out_layout, s)))
+        if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk_views, c0->len_classes, s))) return rc;
+        if ((rc = launch_composite_views(fv, k, (uint32_t)max_chunks, c0->len_classes, c0->views_interleave, u0,
+                                         frag_class_of(u0.render_mod), f0.t_min, f0.bg, f0.out_layout, s)))
             return rc;
         if ((rc = launch_merge_views(fv, k, u0, f0.t_min, f0.bg, f0.out_layout, s))) return rc;
     }

@@ -274,11 +274,14 @@ constexpr uint32_t kTraceMax = 1u << 16;  // waves traced per launch
 // num_tiles + extra_off[t] + k - 1.
 //
 // Dispatch order (longest first): order[i] is the slot the i-th compositing
-// wave takes.  Every full chunk (`chunk` instances) is dispatched before every
-// partial one (a tile's last, shorter chunk, or its only one), so the waves
-// that start last are the short ones.  In slot order the full extra chunks of
-// the deep tiles started last and ran alone at the end of the launch (trace:
-// the last third of the launch at falling occupancy).
+// wave takes.  Chunks are dispatched by length class: every full chunk
+// (`chunk` instances) first, then the partial ones (a tile's last, shorter
+// chunk, or its only one) from the longest class to the shortest, in tile
+// order within a class, so the waves that start last are the short ones.  In
+// slot order the full extra chunks of the deep tiles started last and ran alone
+// at the end of the launch (trace: the last third of the launch at falling
+// occupancy).  A group's compositing launch interleaves its views by class
+// (k_composite_views), so no view's long chunks start at the end.
 __device__ __forceinline__ uint32_t chunks_of(uint2 r, uint32_t chunk) {
     const uint32_t len = r.y - r.x;
     return len == 0 ? 1u : (len + chunk - 1) / chunk;
@@ -287,82 +290,117 @@ __device__ __forceinline__ uint32_t chunks_of(uint2 r, uint32_t chunk) {
 // Chunks of a tile that hold exactly `chunk` instances (all but the last).
 __device__ __forceinline__ uint32_t full_chunks_of(uint2 r, uint32_t chunk) { return (r.y - r.x) / chunk; }
 
+// Length class of a tile's partial chunk, 1 (longest) .. classes - 1, or 0 if
+// the tile has none (its list is a positive multiple of `chunk`).
+__device__ __forceinline__ uint32_t partial_class_of(uint2 r, uint32_t chunk, uint32_t classes) {
+    const uint32_t len = r.y - r.x;
+    const uint32_t rem = len % chunk;
+    if (len != 0 && rem == 0) return 0u;
+    return (classes - 1u) - rem * (classes - 1u) / chunk;
+}
+
 // Chunk descriptors in two parallel launches (one thread per tile):
-// k_chunk_count writes each block's totals of extra chunks (beyond the first
-// per tile) and of full chunks; k_chunk_write takes its block's offsets as
-// sums of the earlier block totals (a few dozen at 1080p), scans its tiles'
-// counts, and writes the descriptors (tile, begin, end, count << 16 | index)
-// and each chunk's dispatch position.
+// k_chunk_count writes each block's totals (extra chunks beyond the first per
+// tile; full chunks; partial chunks of each length class) into `tot`, array j
+// at tot + j * gridDim.x; k_chunk_write takes its block's offsets as sums of
+// the earlier block totals (a few dozen at 1080p), ranks its tiles' chunks,
+// and writes the descriptors (tile, begin, end, count << 16 | index), each
+// chunk's dispatch position and (block 0) the frame's chunks per class, at
+// tot + (1 + classes) * gridDim.x.
 __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
-                                            uint32_t* __restrict__ block_extra, uint32_t* __restrict__ block_full,
+                                            uint32_t classes, uint32_t* __restrict__ tot,
                                             uint32_t (*lds)[kThreads / 64]) {
     const int t = blockIdx.x * kThreads + threadIdx.x;
-    const uint2 r = t < num_tiles ? ranges[t] : make_uint2(0u, 0u);
-    uint32_t e = t < num_tiles ? chunks_of(r, chunk) - 1u : 0u;
-    uint32_t f = full_chunks_of(r, chunk);
-    e = wave_reduce_sum(e);
-    f = wave_reduce_sum(f);
+    const bool valid = t < num_tiles;
+    const uint2 r = valid ? ranges[t] : make_uint2(0u, 0u);
+    const uint32_t e = wave_reduce_sum(valid ? chunks_of(r, chunk) - 1u : 0u);
+    const uint32_t f = wave_reduce_sum(full_chunks_of(r, chunk));
+    const uint32_t pc = valid ? partial_class_of(r, chunk, classes) : 0u;
+    const int w = threadIdx.x >> 6;
     if (__lane_id() == 0) {
-        lds[0][threadIdx.x >> 6] = e;
-        lds[1][threadIdx.x >> 6] = f;
+        lds[0][w] = e;
+        lds[1][w] = f;
+    }
+    for (uint32_t k = 1; k < classes; ++k) {
+        const uint32_t n = (uint32_t)__popcll(__ballot(pc == k));
+        if (__lane_id() == 0) lds[1 + k][w] = n;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        block_extra[blockIdx.x] = lds[0][0] + lds[0][1] + lds[0][2] + lds[0][3];
-        block_full[blockIdx.x] = lds[1][0] + lds[1][1] + lds[1][2] + lds[1][3];
-    }
+    if (threadIdx.x <= classes)
+        tot[threadIdx.x * gridDim.x + blockIdx.x] =
+            lds[threadIdx.x][0] + lds[threadIdx.x][1] + lds[threadIdx.x][2] + lds[threadIdx.x][3];
 }
 
 __global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restrict__ ranges, int num_tiles,
-                                                          uint32_t chunk, uint32_t* __restrict__ block_extra,
-                                                          uint32_t* __restrict__ block_full) {
-    __shared__ uint32_t lds[2][kThreads / 64];
-    chunk_count(ranges, num_tiles, chunk, block_extra, block_full, lds);
+                                                          uint32_t chunk, uint32_t classes,
+                                                          uint32_t* __restrict__ tot) {
+    __shared__ uint32_t lds[1 + kMaxLenClasses][kThreads / 64];
+    chunk_count(ranges, num_tiles, chunk, classes, tot, lds);
 }
 
+struct ChunkWriteLds {
+    uint32_t scan[2][kThreads / 64];
+    uint32_t cls[kMaxLenClasses][kThreads / 64];  // partials of class k per wave
+    uint32_t pre[1 + kMaxLenClasses];             // sums over the earlier blocks
+    uint32_t base[kMaxLenClasses];                // first dispatch position of each class
+};
+
 __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
-                                            const uint32_t* __restrict__ block_extra,
-                                            const uint32_t* __restrict__ block_full, uint32_t* __restrict__ chunk_cnt,
-                                            uint32_t* __restrict__ chunk_base, uint32_t* __restrict__ n_extra_dev,
-                                            uint4* __restrict__ desc, uint32_t* __restrict__ order,
-                                            float4* __restrict__ tmax, uint32_t (*lds)[kThreads / 64],
-                                            uint32_t* s_sh) {
-    uint32_t &s_prefix = s_sh[0], &s_full_prefix = s_sh[1], &s_full_total = s_sh[2];
+                                            uint32_t classes, const uint32_t* __restrict__ tot,
+                                            uint32_t* __restrict__ chunk_cnt, uint32_t* __restrict__ chunk_base,
+                                            uint32_t* __restrict__ n_extra_dev, uint4* __restrict__ desc,
+                                            uint32_t* __restrict__ order, float4* __restrict__ tmax,
+                                            ChunkWriteLds& sh) {
     const int t = blockIdx.x * kThreads + threadIdx.x;
-    if (threadIdx.x < 64) {  // wave 0: offsets of this block = sums of the earlier blocks' totals
-        uint32_t p = 0, pf = 0, tf = 0;
-        for (uint32_t b = __lane_id(); b < gridDim.x; b += 64) {
-            const uint32_t f = block_full[b];
-            if (b < blockIdx.x) {
-                p += block_extra[b];
-                pf += f;
+    const int w = threadIdx.x >> 6;
+    if (w == 0) {  // wave 0: offsets of this block = sums of the earlier blocks' totals
+        uint32_t* cls_tot = const_cast<uint32_t*>(tot) + (1 + classes) * gridDim.x;
+        uint32_t run = 0;  // class bases: full chunks, then the partial classes in order
+        for (uint32_t j = 0; j <= classes; ++j) {
+            uint32_t p = 0, a = 0;
+            for (uint32_t b = __lane_id(); b < gridDim.x; b += 64) {
+                const uint32_t v = tot[j * gridDim.x + b];
+                p += b < blockIdx.x ? v : 0u;
+                a += v;
             }
-            tf += f;
-        }
-        p = wave_reduce_sum(p);
-        pf = wave_reduce_sum(pf);
-        tf = wave_reduce_sum(tf);
-        if (__lane_id() == 0) {
-            s_prefix = p;
-            s_full_prefix = pf;
-            s_full_total = tf;
+            p = wave_reduce_sum(p);
+            a = wave_reduce_sum(a);
+            if (__lane_id() == 0) {
+                sh.pre[j] = p;
+                if (j >= 1) {
+                    sh.base[j - 1] = run;
+                    run += a;
+                    if (blockIdx.x == 0) cls_tot[j - 1] = a;
+                }
+            }
         }
     }
-    const uint2 r = t < num_tiles ? ranges[t] : make_uint2(0u, 0u);
+    const bool valid = t < num_tiles;
+    const uint2 r = valid ? ranges[t] : make_uint2(0u, 0u);
     const uint32_t cnt = chunks_of(r, chunk);
     const uint32_t full = full_chunks_of(r, chunk);
-    const uint32_t mine = t < num_tiles ? cnt - 1u : 0u;
+    const uint32_t pc = valid ? partial_class_of(r, chunk, classes) : 0u;
+    uint32_t rank = 0;  // among this wave's partials of class pc
+    for (uint32_t k = 1; k < classes; ++k) {
+        const uint64_t m = __ballot(pc == k);
+        if (pc == k) rank = (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
+        if (__lane_id() == 0) sh.cls[k][w] = (uint32_t)__popcll(m);
+    }
+    const uint32_t mine = valid ? cnt - 1u : 0u;
     uint32_t total, total_f;
-    const uint32_t excl = block_exclusive<kThreads>(mine, lds[0], total);  // (its barrier also publishes s_*)
-    const uint32_t excl_f = block_exclusive<kThreads>(full, lds[1], total_f);
-    const uint32_t extra = s_prefix + excl;
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_extra_dev = s_prefix + total;
-    const bool valid = t < num_tiles;
+    const uint32_t excl = block_exclusive<kThreads>(mine, sh.scan[0], total);  // (its barrier also publishes sh)
+    const uint32_t excl_f = block_exclusive<kThreads>(full, sh.scan[1], total_f);
+    const uint32_t extra = sh.pre[0] + excl;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_extra_dev = sh.pre[0] + total;
     const uint32_t base = (uint32_t)num_tiles + extra;
-    // dispatch positions: full chunks in tile order, then the partial ones
-    // (at most one per tile: chunks before this tile minus full ones before it)
-    const uint32_t full_before = s_full_prefix + excl_f;
-    const uint32_t part_pos = s_full_total + ((uint32_t)t + extra - full_before);
+    // dispatch positions: full chunks in tile order from 0, the partial one
+    // (at most one per tile) after the earlier partials of its class
+    const uint32_t full_before = sh.pre[1] + excl_f;
+    uint32_t part_pos = 0;
+    if (pc != 0) {
+        part_pos = sh.base[pc] + sh.pre[1 + pc] + rank;
+        for (int i = 0; i < w; ++i) part_pos += sh.cls[pc][i];
+    }
     // chunk j of this tile: descriptor, dispatch position, published maxima
     auto emit = [&](uint32_t tt, uint32_t rx, uint32_t ry, uint32_t c, uint32_t f, uint32_t bs, uint32_t fb,
                     uint32_t pp, uint32_t j) {
@@ -393,17 +431,15 @@ __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, in
 }
 
 __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restrict__ ranges, int num_tiles,
-                                                          uint32_t chunk, const uint32_t* __restrict__ block_extra,
-                                                          const uint32_t* __restrict__ block_full,
+                                                          uint32_t chunk, uint32_t classes,
+                                                          const uint32_t* __restrict__ tot,
                                                           uint32_t* __restrict__ chunk_cnt,
                                                           uint32_t* __restrict__ chunk_base,
                                                           uint32_t* __restrict__ n_extra_dev,
                                                           uint4* __restrict__ desc, uint32_t* __restrict__ order,
                                                           float4* __restrict__ tmax) {
-    __shared__ uint32_t lds[2][kThreads / 64];
-    __shared__ uint32_t s_sh[3];
-    chunk_write(ranges, num_tiles, chunk, block_extra, block_full, chunk_cnt, chunk_base, n_extra_dev, desc, order,
-                tmax, lds, s_sh);
+    __shared__ ChunkWriteLds sh;
+    chunk_write(ranges, num_tiles, chunk, classes, tot, chunk_cnt, chunk_base, n_extra_dev, desc, order, tmax, sh);
 }
 
 struct ChunkView {
@@ -419,20 +455,19 @@ struct ChunkViews {
     ChunkView v[kMaxViews];
 };
 
-__global__ __launch_bounds__(kThreads) void k_chunk_count_views(ChunkViews vs, int num_tiles, uint32_t chunk) {
-    __shared__ uint32_t lds[2][kThreads / 64];
+__global__ __launch_bounds__(kThreads) void k_chunk_count_views(ChunkViews vs, int num_tiles, uint32_t chunk,
+                                                                uint32_t classes) {
+    __shared__ uint32_t lds[1 + kMaxLenClasses][kThreads / 64];
     const ChunkView& v = vs.v[blockIdx.y];
-    uint32_t* block_extra = v.chunk_cnt + num_tiles;
-    chunk_count(v.ranges, num_tiles, chunk, block_extra, block_extra + gridDim.x, lds);
+    chunk_count(v.ranges, num_tiles, chunk, classes, v.chunk_cnt + num_tiles, lds);
 }
 
-__global__ __launch_bounds__(kThreads) void k_chunk_write_views(ChunkViews vs, int num_tiles, uint32_t chunk) {
-    __shared__ uint32_t lds[2][kThreads / 64];
-    __shared__ uint32_t s_sh[3];
+__global__ __launch_bounds__(kThreads) void k_chunk_write_views(ChunkViews vs, int num_tiles, uint32_t chunk,
+                                                                uint32_t classes) {
+    __shared__ ChunkWriteLds sh;
     const ChunkView& v = vs.v[blockIdx.y];
-    const uint32_t* block_extra = v.chunk_cnt + num_tiles;
-    chunk_write(v.ranges, num_tiles, chunk, block_extra, block_extra + gridDim.x, v.chunk_cnt, v.chunk_base,
-                v.n_extra_dev, v.desc, v.order, v.tmax, lds, s_sh);
+    chunk_write(v.ranges, num_tiles, chunk, classes, v.chunk_cnt + num_tiles, v.chunk_cnt, v.chunk_base,
+                v.n_extra_dev, v.desc, v.order, v.tmax, sh);
 }
 
 // Bits [lo, hi] of a 16-bit mask, clamped to [0, 15]; 0 if the range is empty.
@@ -854,12 +889,18 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
 #endif
 }
 
-// The composite of a group of views: blockIdx.y = view, each view's chunks in
-// its own dispatch order; a view's waves past its chunk count exit.
+// The composite of a group of views, one wave per chunk of any view.  By
+// default (interleaved) the group's dispatch runs class-major over the views:
+// every view's full chunks, then every view's longest partials, and so on
+// (each view's chunks of one class in its own dispatch order), so the last
+// waves of the launch are short chunks of all views.  View-major (interleave
+// off: all of view 0, then view 1, ...) left the last view's long chunks to
+// run alone at the end.  Waves past the group's chunk count exit.
 struct CompView {
     const uint4* desc;
     const uint32_t* order;
     const uint32_t* n_chunks_dev;
+    const uint32_t* cls_tot;  // the view's chunks per length class (chunk_class_totals)
     const uint32_t* list;
     const SplatRec* recs;
     float* out;
@@ -869,14 +910,51 @@ struct CompView {
 };
 struct CompViews {
     CompView v[kMaxViews];
+    uint32_t k, classes;      // views; length classes (k * classes <= 64 when interleaved)
+    uint32_t view_blocks;     // view-major: blocks per view
+    uint32_t interleave;
 };
+
+// Interleaved dispatch: the (view, position) of the group's p-th chunk, or
+// view -1 past the end.  Lane j = v * classes + c holds view v's count of
+// class c; lane q = c * k + v takes it in dispatch (class-major) order.
+__device__ __forceinline__ int interleaved_chunk(const CompViews& vs, uint32_t p, uint32_t& pos) {
+    const uint32_t lane = __lane_id();
+    const uint32_t kc = vs.k * vs.classes;
+    uint32_t n = 0;
+    for (uint32_t v = 0; v < vs.k; ++v)  // independent loads, one view's classes each
+        if (lane >= v * vs.classes && lane < (v + 1) * vs.classes) n = vs.v[v].cls_tot[lane - v * vs.classes];
+    const uint32_t vm_incl = wave_inclusive_scan(n);  // view-major
+    const uint32_t qc = lane / vs.k, qv = lane - qc * vs.k;
+    const uint32_t nq = __shfl(n, (int)(lane < kc ? qv * vs.classes + qc : 0u), 64);
+    const uint32_t q_incl = wave_inclusive_scan(lane < kc ? nq : 0u);  // class-major
+    const uint64_t hit = __ballot(lane < kc && p < q_incl);
+    if (hit == 0) return -1;
+    const int q = (int)__builtin_ctzll(hit);
+    const uint32_t c = (uint32_t)q / vs.k, v = (uint32_t)q - c * vs.k;
+    const uint32_t q_excl = __shfl(q_incl - nq, q, 64);
+    // the view's own dispatch position: its chunks of the earlier classes first
+    const uint32_t vm_excl = vm_incl - n;
+    const uint32_t cls_base = __shfl(vm_excl, (int)(v * vs.classes + c), 64) - __shfl(vm_excl, (int)(v * vs.classes), 64);
+    pos = cls_base + (p - q_excl);
+    return (int)v;
+}
 
 template <int FRAG>
 __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite_views(CompViews vs, CompositeArgs a) {
     __shared__ float4 lds[kCompWaves][kBatch * 3];
-    const CompView& v = vs.v[blockIdx.y];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t pos = blockIdx.x * kCompWaves + wave;
+    int view;
+    uint32_t pos;
+    if (vs.interleave) {
+        view = __builtin_amdgcn_readfirstlane(interleaved_chunk(vs, blockIdx.x * kCompWaves + wave, pos));
+        pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)pos);
+        if (view < 0) return;
+    } else {
+        view = (int)(blockIdx.x / vs.view_blocks);
+        pos = (blockIdx.x - (uint32_t)view * vs.view_blocks) * kCompWaves + wave;
+    }
+    const CompView& v = vs.v[view];
     if (pos >= (uint32_t)a.num_tiles + v.n_chunks_dev[0]) return;
     const uint32_t slot = v.order[pos];
     const uint4 d = v.desc[slot];
@@ -1198,21 +1276,29 @@ static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float*
     return a;
 }
 
-size_t chunk_cnt_elems(int num_tiles) { return (size_t)num_tiles + 2 * ((size_t)num_tiles / kThreads + 1); }
+size_t chunk_cnt_elems(int num_tiles) {
+    return (size_t)num_tiles + (1 + kMaxLenClasses) * ((size_t)num_tiles / kThreads + 1) + kMaxLenClasses;
+}
 
-int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t* chunk_cnt, uint32_t* chunk_base,
-                  uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax, hipStream_t s) {
+const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes) {
+    const size_t g = ((size_t)num_tiles + kThreads - 1) / kThreads;
+    return chunk_cnt + num_tiles + (1 + classes) * g;
+}
+
+int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
+                  uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
+                  hipStream_t s) {
 #ifndef GSR_COMP_BOUND
     tmax = nullptr;  // the published maxima are only read by the bound variant
 #endif
+    if (classes < 2 || classes > (uint32_t)kMaxLenClasses) return set_error(GSR_ERR_INVALID, "chunk length classes");
     const unsigned g = (unsigned)((num_tiles + kThreads - 1) / kThreads);
     // the per-block totals live in chunk_cnt past its num_tiles entries
-    uint32_t* block_extra = chunk_cnt + num_tiles;
-    uint32_t* block_full = block_extra + g;
-    k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, block_extra, block_full);
+    uint32_t* tot = chunk_cnt + num_tiles;
+    k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot);
     GSR_LAUNCH_CHECK("chunk_count");
-    k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, block_extra, block_full, chunk_cnt, chunk_base,
-                                         n_extra_dev, desc, order, tmax);
+    k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot, chunk_cnt, chunk_base, n_extra_dev,
+                                         desc, order, tmax);
     GSR_LAUNCH_CHECK("chunk_write");
     return GSR_OK;
 }
@@ -1318,7 +1404,8 @@ int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s) {
     return GSR_OK;
 }
 
-int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, hipStream_t s) {
+int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, uint32_t classes, hipStream_t s) {
+    if (classes < 2 || classes > (uint32_t)kMaxLenClasses) return set_error(GSR_ERR_INVALID, "chunk length classes");
     ChunkViews cv{};
     for (int i = 0; i < k; ++i) {
         const FinishView& f = views[i];
@@ -1330,22 +1417,28 @@ int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk,
         cv.v[i] = ChunkView{f.ranges, f.chunk_cnt, f.chunk_base, f.n_extra_dev, f.desc, f.order, tmax};
     }
     const dim3 grid((unsigned)((num_tiles + kThreads - 1) / kThreads), (unsigned)k);
-    k_chunk_count_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk);
+    k_chunk_count_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk, classes);
     GSR_LAUNCH_CHECK("chunk_count_views");
-    k_chunk_write_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk);
+    k_chunk_write_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk, classes);
     GSR_LAUNCH_CHECK("chunk_write_views");
     return GSR_OK;
 }
 
-int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, const FrameUniforms& u, int frag_class,
-                           float t_min, const float* bg, int out_layout, hipStream_t s) {
+int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32_t classes, bool interleave,
+                           const FrameUniforms& u, int frag_class, float t_min, const float* bg, int out_layout,
+                           hipStream_t s) {
     const CompositeArgs a = make_args(u, t_min, bg, out_layout);
     CompViews cv{};
     for (int i = 0; i < k; ++i) {
         const FinishView& f = views[i];
-        cv.v[i] = CompView{f.desc, f.order, f.n_extra_dev, f.tile_vals, f.recs, f.out, f.partial, f.sat, f.tmax};
+        cv.v[i] = CompView{f.desc, f.order, f.n_extra_dev, chunk_class_totals(f.chunk_cnt, a.num_tiles, classes),
+                           f.tile_vals, f.recs, f.out, f.partial, f.sat, f.tmax};
     }
-    const dim3 grid((unsigned)((max_chunks + kCompWaves - 1) / kCompWaves), (unsigned)k);
+    cv.k = (uint32_t)k;
+    cv.classes = classes;
+    cv.view_blocks = (max_chunks + kCompWaves - 1) / kCompWaves;
+    cv.interleave = interleave && (uint32_t)k * classes <= 64u;
+    const dim3 grid(cv.view_blocks * (unsigned)k);
     switch (frag_class) {
         case kFragGauss: k_composite_views<kFragGauss><<<grid, kCompThreads, 0, s>>>(cv, a); break;
         case kFragBillboard: k_composite_views<kFragBillboard><<<grid, kCompThreads, 0, s>>>(cv, a); break;

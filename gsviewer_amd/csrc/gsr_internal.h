@@ -13,6 +13,7 @@ namespace gsr {
 
 constexpr int kTile = 16;              // composite tile edge (pixels)
 constexpr int kMaxViews = GSR_MAX_VIEWS;  // views of one scene begun together (gsr_render_begin_views)
+constexpr int kMaxLenClasses = 16;        // compositing dispatch: full chunks + partial-length classes
 constexpr int kWave = 64;              // CDNA wavefront
 
 // One visible splat after preprocess: 48 bytes = exactly three float4, so the
@@ -293,9 +294,13 @@ int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
 // chunk_cnt must hold chunk_cnt_elems(num_tiles) entries (block totals after the tiles);
 // order: one entry per chunk (dispatch position -> chunk slot)
 size_t chunk_cnt_elems(int num_tiles);
-int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t* chunk_cnt,
+// classes (2 .. kMaxLenClasses): dispatch order = full chunks, then the partial
+// ones in classes - 1 length classes, longest first; the frame's chunk count
+// of each class lands at chunk_class_totals(chunk_cnt, num_tiles, classes)
+int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
                   hipStream_t s);
+const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes);
 int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n_chunks_dev, uint32_t max_chunks,
                      const uint32_t* chunk_cnt, const uint32_t* chunk_base, uint32_t* sat,
                      const uint32_t* tile_vals, const SplatRec* recs, const FrameUniforms& u,
@@ -339,9 +344,12 @@ struct FinishView {
 // binning: bin_tmp of each view holds its per-block instance counts
 int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s);
 int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s);
-int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, hipStream_t s);
-int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, const FrameUniforms& u, int frag_class,
-                           float t_min, const float* bg, int out_layout, hipStream_t s);
+int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, uint32_t classes,
+                        hipStream_t s);
+// interleave: dispatch class-major over the views (k * classes <= 64), else view after view
+int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32_t classes, bool interleave,
+                           const FrameUniforms& u, int frag_class, float t_min, const float* bg, int out_layout,
+                           hipStream_t s);
 int launch_merge_views(FinishView* views, int k, const FrameUniforms& u, float t_min, const float* bg,
                        int out_layout, hipStream_t s);
 
