@@ -142,6 +142,41 @@ def test_shared_scene_pass_matches_serial_renders(gpu, batched_sorts, batched_fi
     scene.close()
 
 
+@pytest.mark.parametrize("interleave,classes,k", [("0", "2", 3), ("1", "2", 3), ("1", "8", 5), ("1", "16", 3),
+                                                  ("1", "16", 5)])
+def test_compositing_dispatch_orders(gpu, monkeypatch, interleave, classes, k):
+    """The compositor's dispatch order (chunk length classes; a group's views
+    interleaved class-major, or view after view; k * classes > 64 falls back to
+    view after view) moves no pixel: a group's images equal each view rendered
+    alone.  Short chunks so that deep tiles have many and partials span the
+    classes."""
+    import torch
+
+    from gsviewer_amd.multiview import ViewBatchPipeline
+    from gsviewer_amd.rasterizer import HipContext, render_into
+    monkeypatch.setenv("GSR_CHUNK", "64")
+    monkeypatch.setenv("GSR_CHUNK_VIEWS", "64")
+    monkeypatch.setenv("GSR_LEN_CLASSES", classes)
+    monkeypatch.setenv("GSR_VIEWS_INTERLEAVE", interleave)
+    scene, st, cams, ctxs, streams, outs = _setup(k)
+    ref_ctx = HipContext()
+    want = []
+    for v in range(k):
+        o = torch.empty_like(outs[v])
+        render_into(ref_ctx, scene, cams[v], st, o)
+        want.append(o)
+    pipe = ViewBatchPipeline([(ctxs, cams, outs, streams[0])], scene, st)
+    for _ in range(2):
+        pipe.step()
+    pipe.drain()
+    torch.cuda.synchronize()
+    for v in range(k):
+        np.testing.assert_array_equal(outs[v].cpu().numpy(), want[v].cpu().numpy(), err_msg=f"view {v}")
+    for c in ctxs + [ref_ctx]:
+        c.close()
+    scene.close()
+
+
 def test_shared_scene_pass_radii_and_errors(gpu):
     import torch
 
