@@ -194,8 +194,10 @@ int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream);
  * size, t_min, background, output layout, fragment mode and chunk length.  A group's frames are
  * composited in chunks of GSR_CHUNK_VIEWS instances (default 3072: views in flight fill the chip
  * while a deep tile's chunk runs), a frame finished alone in chunks of GSR_CHUNK (default 192:
- * latency); both read when the context is created.
- * Results are identical to k gsr_render_finish calls. */
+ * latency); both read when the context is created.  Chunks are dispatched longest first (full
+ * chunks, then GSR_LEN_CLASSES - 1 length classes of the last chunks, default 8), a group's
+ * views interleaved class by class (GSR_VIEWS_INTERLEAVE=0: view after view).
+ * Results are identical to k gsr_render_finish calls (and independent of the dispatch order). */
 int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream);
 
 int gsr_context_stats(const gsr_context* ctx, gsr_frame_stats* out);
