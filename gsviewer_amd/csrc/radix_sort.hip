@@ -96,28 +96,40 @@ __device__ __forceinline__ uint32_t count_of(const uint32_t* n_dev, uint32_t n_h
 }
 
 // Lanes of the wave holding the same w-bit digit (only `valid` lanes).
+// Per digit bit: the ballot m, then each lane keeps the lanes that agree with
+// it: p &= ~(m ^ t), t = the lane's bit as 0 / all ones (a sign-extended bit
+// field; one 3-input bit op per 32-bit half: 4 VALU per bit, against 8 for
+// `p &= bit ? m : ~m` as the compiler emitted it).
 __device__ __forceinline__ uint64_t match_digit(uint32_t digit, uint32_t w, bool valid) {
-    uint64_t peers = __ballot(valid);
+    const uint64_t v = __ballot(valid);
+    uint32_t plo = (uint32_t)v, phi = (uint32_t)(v >> 32);
     for (uint32_t b = 0; b < w; ++b) {
-        const bool bit = (digit >> b) & 1u;
-        const uint64_t m = __ballot(bit);
-        peers &= bit ? m : ~m;
+        const uint32_t t = (uint32_t)__builtin_amdgcn_sbfe((int)digit, (int)b, 1);
+        const uint64_t m = __ballot(t != 0u);
+        plo &= ~((uint32_t)m ^ t);
+        phi &= ~((uint32_t)(m >> 32) ^ t);
     }
-    return peers;
+    return ((uint64_t)phi << 32) | plo;
 }
 
+// Per-tile digit counts: one LDS histogram per block, counted with LDS atomics
+// (counts need no order; the scatter's stable ranks use digit matching).  The
+// ballot-per-digit-bit matching the scatter needs cost ~8 VALU per digit bit
+// and item here, and with views in flight the chip is VALU-issue bound.
 template <int kR, int kCB>
 __device__ __forceinline__ void rs_upsweep(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ n_dev,
                                            uint32_t n_host, const PassArgs& pa, uint32_t* __restrict__ hist,
                                            uint32_t ntiles, uint32_t tile) {
     constexpr int kTileItems = kThreads * kR;
     constexpr int kCap = radix_cap<kCB>();
-    __shared__ uint16_t h[kWaves][kCap];  // per-wave counts (<= 64*kR each)
+    __shared__ uint32_t h[kCap];
     const Digit dg = digit_params(pa);
     const uint32_t radix = dg.mask + 1u;
     const uint32_t n = count_of(n_dev, n_host);
     const uint32_t tile0 = tile * kTileItems;
-    for (uint32_t i = threadIdx.x; i < kWaves * radix; i += kThreads) h[i / radix][i % radix] = 0u;
+#pragma unroll
+    for (int i = 0; i < (kCap + kThreads - 1) / kThreads; ++i)
+        if (i * kThreads + (int)threadIdx.x < kCap) h[i * kThreads + threadIdx.x] = 0u;
     const int w = threadIdx.x >> 6;
     const uint32_t base = tile0 + w * (kTileItems / kWaves) + __lane_id();
     uint32_t k[kR];
@@ -129,20 +141,11 @@ __device__ __forceinline__ void rs_upsweep(const uint32_t* __restrict__ keys, co
     __syncthreads();
     if (tile0 < n) {
 #pragma unroll
-        for (int r = 0; r < kR; ++r) {
-            const bool valid = base + r * 64 < n;
-            const uint32_t d = dg.of(k[r]);
-            const uint64_t peers = match_digit(d, dg.w, valid);
-            if (valid && (peers & lanemask_lt()) == 0) h[w][d] = (uint16_t)(h[w][d] + __popcll(peers));
-        }
+        for (int r = 0; r < kR; ++r)
+            if (base + r * 64 < n) atomicAdd(&h[dg.of(k[r])], 1u);
     }
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < radix; d += kThreads) {
-        uint32_t s = 0;
-#pragma unroll
-        for (int q = 0; q < kWaves; ++q) s += h[q][d];
-        hist[(size_t)d * ntiles + tile] = s;
-    }
+    for (uint32_t d = threadIdx.x; d < radix; d += kThreads) hist[(size_t)d * ntiles + tile] = h[d];
 }
 
 template <int kR, int kCB>
@@ -236,7 +239,12 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
         gt[j] = mine ? totals[d] : 0u;
         ho[j] = mine ? hist_off[(size_t)d * ntiles + tile] : 0u;
     }
-    for (uint32_t i = threadIdx.x; i < kWaves * radix; i += kThreads) wcnt[i / radix][i % radix] = 0u;
+    {  // clear the per-wave counts (as words: no division by the runtime radix)
+        uint32_t* wz = wcnt_gbase;
+#pragma unroll
+        for (int i = 0; i < (kWaves * kCap / 2 + kThreads - 1) / kThreads; ++i)
+            if (i * kThreads + (int)threadIdx.x < kWaves * kCap / 2) wz[i * kThreads + threadIdx.x] = 0u;
+    }
 
     const int w = threadIdx.x >> 6;
     const uint32_t base = tile0 + w * (kTileItems / kWaves) + __lane_id();
