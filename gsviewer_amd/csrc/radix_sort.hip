@@ -248,7 +248,6 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
 
     const int w = threadIdx.x >> 6;
     const uint32_t base = tile0 + w * (kTileItems / kWaves) + __lane_id();
-    const uint64_t lt = lanemask_lt();
 
     uint32_t k_reg[kR], v_reg[kR], rank[kR], p_reg[kPay ? kR : 1];
 #pragma unroll
@@ -268,8 +267,11 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
         uint32_t rk = 0xffffffffu;
         if (valid) {
             const uint32_t old = wcnt[w][d];
-            rk = old + (uint32_t)__popcll(peers & lt);
-            if ((peers & lt) == 0) wcnt[w][d] = (uint16_t)(old + __popcll(peers));
+            // peers in lower lanes: mbcnt (2 VALU; the lane mask itself was rebuilt per item)
+            const uint32_t below =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+            rk = old + below;
+            if (below == 0) wcnt[w][d] = (uint16_t)(old + __popcll(peers));
         }
         rank[r] = rk;
     }
