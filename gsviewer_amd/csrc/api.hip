@@ -93,6 +93,9 @@ struct PendingFrame {
 };
 }  // namespace gsr
 
+// depth sort passes of a frame rendered alone (gsr_render; see kDepthPasses)
+constexpr int kDepthPassesAlone = 3;
+
 struct gsr_context {
     gsr::DevBuf<uint64_t> vis_mask;
     gsr::DevBuf<uint32_t> wave_counts;
@@ -121,6 +124,8 @@ struct gsr_context {
     uint32_t len_classes = 8;                     // compositing dispatch order: full chunks, then the partial
                                                   // ones in len_classes - 1 length classes, longest first
     bool views_interleave = true;                 // a group's compositing dispatch class-major over its views
+    int depth_passes_alone = kDepthPassesAlone;   // depth sort passes of gsr_render's frames
+    int depth_passes_now = 0;                     // this frame's (0: kDepthPasses)
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
     uint32_t seq = 0;                       // frame sequence number the host waits for
     uint32_t* host_counters_dev = nullptr;  // its device address
@@ -226,6 +231,10 @@ int build_uniforms(const gsr_scene* sc, const gsr_camera* cam, const gsr_setting
 #define GSR_DEPTH_PASSES 4
 #endif
 constexpr int kDepthPasses = GSR_DEPTH_PASSES;
+// A frame rendered alone (gsr_render: begin + finish, nothing else in flight)
+// sorts in 3 passes of <= 11 bits: its kernels' LDS competes with no other
+// view's, and a pass costs more than the wider digits do (r2_s46: depth sort
+// 83.6 -> 78 us, latency 0.383 -> 0.376 ms).
 
 int bits_for(uint32_t v) {  // bits needed to represent values < v
     int b = 0;
@@ -348,7 +357,8 @@ int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const 
     f.pa = c->rect4_a.p, f.pb = c->rect4_b.p;
     f.packed = rects_packable(f.u);
     if (f.n == 0) return GSR_OK;
-    return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32, kDepthPasses, key_range,
+    return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32,
+                            c->depth_passes_now ? c->depth_passes_now : kDepthPasses, key_range,
                             c->radix_tmp.p, totals, s, f.packed ? c->trect.p : nullptr, &f.pa, &f.pb);
 }
 
@@ -575,6 +585,10 @@ int gsr_context_create(gsr_context** out) {
     if (const char* e = std::getenv("GSR_LEN_CLASSES")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 2 && v <= gsr::kMaxLenClasses) (*out)->len_classes = (uint32_t)v;
+    }
+    if (const char* e = std::getenv("GSR_DEPTH_PASSES_ALONE")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 3 && v <= 4) (*out)->depth_passes_alone = (int)v;
     }
     if (const char* e = std::getenv("GSR_VIEWS_INTERLEAVE")) (*out)->views_interleave = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_WAIT_TIMEOUT_MS")) {
@@ -1067,7 +1081,10 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
 
 int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, float* out,
                int32_t* radii, void* stream) {
+    if (!c) return set_error(GSR_ERR_INVALID, "null argument");
+    c->depth_passes_now = c->depth_passes_alone;  // nothing else in flight: the widest digits
     int rc = gsr_render_begin(c, sc, cam, st, out, radii, stream);
+    c->depth_passes_now = 0;
     if (rc) return rc;
     return gsr_render_finish(c, stream);
 }
