@@ -150,7 +150,10 @@ int64_t gsr_context_workspace(gsr_context* ctx, int64_t* n_allocations);
  * radii_dev: optional int32 [n]; 0 for culled Gaussians, else
  *            ceil(max(quad half-width, half-height)) in pixels.
  * Replaces CUDARenderer.draw's rasterizer call (renderer_cuda.py:230-243) and
- * OpenGLRenderer.draw + sort_and_update (renderer_ogl.py:263-268, 406-412). */
+ * OpenGLRenderer.draw + sort_and_update (renderer_ogl.py:263-268, 406-412).
+ * Its depth sort runs 3 radix passes (GSR_DEPTH_PASSES_ALONE, 3 or 4, read at
+ * context creation); frames begun with gsr_render_begin* run 4 narrower ones,
+ * whose kernels fit beside other views' compositing.  Same order either way. */
 int gsr_render(gsr_context* ctx, const gsr_scene* scene, const gsr_camera* cam,
                const gsr_settings* settings, float* out_image_dev, int32_t* radii_dev,
                void* stream);
