@@ -691,10 +691,14 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
             if (i2 < end) idx_next = list[i2];
         }
         const int nb = __builtin_amdgcn_readfirstlane((int)min((uint32_t)kBatch, end - b));
+        // records touching a live slice only (sb: live slices only): once a
+        // slice has stopped, records covering nothing else skip their setup
         // (not unrolled: unrolled by 2, the register allocator copies every
         // packed accumulator at each slice branch and needs 128 VGPRs)
+        uint64_t todo = (sb[0] | sb[1] | sb[2] | sb[3]) & (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull));
 #pragma unroll 1
-        for (int j = 0; j < nb; ++j) {
+        for (; todo; todo &= todo - 1ull) {
+            const int j = (int)__builtin_ctzll(todo);
             const float4 q0 = my[j * 3 + 0];  // cx cy opacity coverage
             const float4 q1 = my[j * 3 + 1];  // qa qb qc mid
             const float4 q2 = my[j * 3 + 2];  // r g b kT
