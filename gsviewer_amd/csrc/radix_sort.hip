@@ -4,13 +4,14 @@
 // most 3 passes.  For the depth sort the width is chosen ON THE DEVICE: the
 // preprocess records the key range [kmin, kmax] of the frame, keys are sorted
 // as key - kmin, and B = bits(kmax - kmin) is split over the host's fixed
-// number of passes (w = ceil(B / passes)).  A camera's visible depths span
-// ~26 of the 32 key bits, so 3 passes of 9 bits replace 4 passes of 8 and the
-// host never has to know B.
+// number of passes (w = ceil(B / passes)): a camera's visible depths span
+// ~24-27 of the 32 key bits, so 4 passes of <= 8 bits (frames in flight) or 3
+// of <= 11 (a frame rendered alone) cover any B and the host never has to
+// know it.
 //
 // One pass = three launches over tiles of 256*R items:
-//   k_rs_upsweep   per-tile digit counts (wave ballot digit matching, no
-//                  atomics), stored digit-major: hist[d * ntiles + tile];
+//   k_rs_upsweep   per-tile digit counts (LDS atomics: counts need no
+//                  order), stored digit-major: hist[d * ntiles + tile];
 //   k_rs_offsets   one wave per digit (4 per block): exclusive scan of that digit's row
 //                  (in place) and the row total;
 //   k_rs_scatter   digit bases (block scan of the row totals), stable in-tile
