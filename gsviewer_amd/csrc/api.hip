@@ -124,6 +124,7 @@ struct gsr_context {
     uint32_t len_classes = 8;                     // compositing dispatch order: full chunks, then the partial
                                                   // ones in len_classes - 1 length classes, longest first
     bool views_interleave = true;                 // a group's compositing dispatch class-major over its views
+    bool first_major = true;                      // ... every tile's first chunk before any later one
     int depth_passes_alone = kDepthPassesAlone;   // depth sort passes of gsr_render's frames
     int depth_passes_now = 0;                     // this frame's (0: kDepthPasses)
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
@@ -590,6 +591,7 @@ int gsr_context_create(gsr_context** out) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 3 && v <= 4) (*out)->depth_passes_alone = (int)v;
     }
+    if (const char* e = std::getenv("GSR_FIRST_MAJOR")) (*out)->first_major = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_VIEWS_INTERLEAVE")) (*out)->views_interleave = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_WAIT_TIMEOUT_MS")) {
         const long v = std::strtol(e, nullptr, 10);
@@ -982,7 +984,7 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         if (f.u.width != f0.u.width || f.u.height != f0.u.height || f.t_min != f0.t_min || f.bg[0] != f0.bg[0] ||
             f.bg[1] != f0.bg[1] || f.bg[2] != f0.bg[2] || f.out_layout != f0.out_layout || f.blend != f0.blend ||
             frag_class_of(f.u.render_mod) != frag_class_of(f0.u.render_mod) || c->chunk_views != c0->chunk_views ||
-            c->len_classes != c0->len_classes)
+            c->len_classes != c0->len_classes || c->first_major != c0->first_major)
             return set_error(GSR_ERR_INVALID, "render_finish_views: views differ in frame size or settings");
     }
     const FrameUniforms& u0 = c0->pend.u;
@@ -1059,8 +1061,8 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
                                               frag_class_of(u0.render_mod), f0.bg, f0.out_layout, fv[v].out, s)))
                 return rc;
     } else {
-        if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk_views, c0->len_classes, s))) return rc;
-        if ((rc = launch_composite_views(fv, k, (uint32_t)max_chunks, c0->len_classes, c0->views_interleave, u0,
+        if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk_views, c0->len_classes, c0->first_major, s))) return rc;
+        if ((rc = launch_composite_views(fv, k, (uint32_t)max_chunks, c0->len_classes, c0->first_major, c0->views_interleave, u0,
                                          frag_class_of(u0.render_mod), f0.t_min, f0.bg, f0.out_layout, s)))
             return rc;
         if ((rc = launch_merge_views(fv, k, u0, f0.t_min, f0.bg, f0.out_layout, s))) return rc;

@@ -307,15 +307,28 @@ __device__ __forceinline__ uint32_t partial_class_of(uint2 r, uint32_t chunk, ui
 // and writes the descriptors (tile, begin, end, count << 16 | index), each
 // chunk's dispatch position and (block 0) the frame's chunks per class, at
 // tot + (1 + classes) * gridDim.x.
+// First-major order (a group's frames, `first_major`): every tile's first
+// chunk (full ones, then by length class) before any later chunk (tile
+// order).  A deep tile's chunk 0 then usually runs, and often saturates,
+// before its later chunks start, so they find its saturation word and skip
+// (sequential early termination visits 33 % of the instances, 3072-instance
+// chunks started together 57 %: tools/comp_stats.py).
+__device__ __forceinline__ uint32_t first_full_of(uint2 r, uint32_t chunk, bool first_major) {
+    return first_major ? ((r.y - r.x) >= chunk ? 1u : 0u) : full_chunks_of(r, chunk);
+}
+__device__ __forceinline__ uint32_t first_class_of(uint2 r, uint32_t chunk, uint32_t classes, bool first_major) {
+    return first_major && (r.y - r.x) >= chunk ? 0u : partial_class_of(r, chunk, classes);
+}
+
 __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
-                                            uint32_t classes, uint32_t* __restrict__ tot,
+                                            uint32_t classes, bool first_major, uint32_t* __restrict__ tot,
                                             uint32_t (*lds)[kThreads / 64]) {
     const int t = blockIdx.x * kThreads + threadIdx.x;
     const bool valid = t < num_tiles;
     const uint2 r = valid ? ranges[t] : make_uint2(0u, 0u);
     const uint32_t e = wave_reduce_sum(valid ? chunks_of(r, chunk) - 1u : 0u);
-    const uint32_t f = wave_reduce_sum(full_chunks_of(r, chunk));
-    const uint32_t pc = valid ? partial_class_of(r, chunk, classes) : 0u;
+    const uint32_t f = wave_reduce_sum(first_full_of(r, chunk, first_major));
+    const uint32_t pc = valid ? first_class_of(r, chunk, classes, first_major) : 0u;
     const int w = threadIdx.x >> 6;
     if (__lane_id() == 0) {
         lds[0][w] = e;
@@ -335,7 +348,7 @@ __global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restric
                                                           uint32_t chunk, uint32_t classes,
                                                           uint32_t* __restrict__ tot) {
     __shared__ uint32_t lds[1 + kMaxLenClasses][kThreads / 64];
-    chunk_count(ranges, num_tiles, chunk, classes, tot, lds);
+    chunk_count(ranges, num_tiles, chunk, classes, false, tot, lds);
 }
 
 struct ChunkWriteLds {
@@ -346,7 +359,7 @@ struct ChunkWriteLds {
 };
 
 __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
-                                            uint32_t classes, const uint32_t* __restrict__ tot,
+                                            uint32_t classes, bool first_major, const uint32_t* __restrict__ tot,
                                             uint32_t* __restrict__ chunk_cnt, uint32_t* __restrict__ chunk_base,
                                             uint32_t* __restrict__ n_extra_dev, uint4* __restrict__ desc,
                                             uint32_t* __restrict__ order, float4* __restrict__ tmax,
@@ -367,6 +380,7 @@ __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, in
             a = wave_reduce_sum(a);
             if (__lane_id() == 0) {
                 sh.pre[j] = p;
+                if (j == 0 && blockIdx.x == 0) cls_tot[classes] = a;  // the later chunks (first-major order)
                 if (j >= 1) {
                     sh.base[j - 1] = run;
                     run += a;
@@ -378,8 +392,8 @@ __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, in
     const bool valid = t < num_tiles;
     const uint2 r = valid ? ranges[t] : make_uint2(0u, 0u);
     const uint32_t cnt = chunks_of(r, chunk);
-    const uint32_t full = full_chunks_of(r, chunk);
-    const uint32_t pc = valid ? partial_class_of(r, chunk, classes) : 0u;
+    const uint32_t full = first_full_of(r, chunk, first_major);
+    const uint32_t pc = valid ? first_class_of(r, chunk, classes, first_major) : 0u;
     uint32_t rank = 0;  // among this wave's partials of class pc
     for (uint32_t k = 1; k < classes; ++k) {
         const uint64_t m = __ballot(pc == k);
@@ -408,7 +422,8 @@ __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, in
         const uint32_t e = min(ry, b + chunk);
         const uint32_t slot = j == 0 ? tt : bs + j - 1;
         desc[slot] = make_uint4(tt, b, e, (c << 16) | j);
-        order[j < f ? fb + j : pp] = slot;
+        // first-major: chunk j >= 1 goes after every first chunk, in slot order
+        order[first_major && j > 0 ? slot : (j < f ? fb + j : pp)] = slot;
         if (tmax && c > 1) tmax[slot] = make_float4(1.f, 1.f, 1.f, 1.f);  // nothing composited yet
     };
     if (valid) {
@@ -439,7 +454,8 @@ __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restric
                                                           uint4* __restrict__ desc, uint32_t* __restrict__ order,
                                                           float4* __restrict__ tmax) {
     __shared__ ChunkWriteLds sh;
-    chunk_write(ranges, num_tiles, chunk, classes, tot, chunk_cnt, chunk_base, n_extra_dev, desc, order, tmax, sh);
+    chunk_write(ranges, num_tiles, chunk, classes, false, tot, chunk_cnt, chunk_base, n_extra_dev, desc, order, tmax,
+                sh);
 }
 
 struct ChunkView {
@@ -456,18 +472,18 @@ struct ChunkViews {
 };
 
 __global__ __launch_bounds__(kThreads) void k_chunk_count_views(ChunkViews vs, int num_tiles, uint32_t chunk,
-                                                                uint32_t classes) {
+                                                                uint32_t classes, uint32_t first_major) {
     __shared__ uint32_t lds[1 + kMaxLenClasses][kThreads / 64];
     const ChunkView& v = vs.v[blockIdx.y];
-    chunk_count(v.ranges, num_tiles, chunk, classes, v.chunk_cnt + num_tiles, lds);
+    chunk_count(v.ranges, num_tiles, chunk, classes, first_major != 0, v.chunk_cnt + num_tiles, lds);
 }
 
 __global__ __launch_bounds__(kThreads) void k_chunk_write_views(ChunkViews vs, int num_tiles, uint32_t chunk,
-                                                                uint32_t classes) {
+                                                                uint32_t classes, uint32_t first_major) {
     __shared__ ChunkWriteLds sh;
     const ChunkView& v = vs.v[blockIdx.y];
-    chunk_write(v.ranges, num_tiles, chunk, classes, v.chunk_cnt + num_tiles, v.chunk_cnt, v.chunk_base,
-                v.n_extra_dev, v.desc, v.order, v.tmax, sh);
+    chunk_write(v.ranges, num_tiles, chunk, classes, first_major != 0, v.chunk_cnt + num_tiles, v.chunk_cnt,
+                v.chunk_base, v.n_extra_dev, v.desc, v.order, v.tmax, sh);
 }
 
 // Bits [lo, hi] of a 16-bit mask, clamped to [0, 15]; 0 if the range is empty.
@@ -1281,7 +1297,7 @@ static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float*
 }
 
 size_t chunk_cnt_elems(int num_tiles) {
-    return (size_t)num_tiles + (1 + kMaxLenClasses) * ((size_t)num_tiles / kThreads + 1) + kMaxLenClasses;
+    return (size_t)num_tiles + (1 + kMaxLenClasses) * ((size_t)num_tiles / kThreads + 1) + kMaxLenClasses + 1;
 }
 
 const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes) {
@@ -1408,7 +1424,8 @@ int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s) {
     return GSR_OK;
 }
 
-int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, uint32_t classes, hipStream_t s) {
+int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, uint32_t classes, bool first_major,
+                        hipStream_t s) {
     if (classes < 2 || classes > (uint32_t)kMaxLenClasses) return set_error(GSR_ERR_INVALID, "chunk length classes");
     ChunkViews cv{};
     for (int i = 0; i < k; ++i) {
@@ -1421,16 +1438,16 @@ int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk,
         cv.v[i] = ChunkView{f.ranges, f.chunk_cnt, f.chunk_base, f.n_extra_dev, f.desc, f.order, tmax};
     }
     const dim3 grid((unsigned)((num_tiles + kThreads - 1) / kThreads), (unsigned)k);
-    k_chunk_count_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk, classes);
+    k_chunk_count_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk, classes, first_major ? 1u : 0u);
     GSR_LAUNCH_CHECK("chunk_count_views");
-    k_chunk_write_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk, classes);
+    k_chunk_write_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk, classes, first_major ? 1u : 0u);
     GSR_LAUNCH_CHECK("chunk_write_views");
     return GSR_OK;
 }
 
-int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32_t classes, bool interleave,
-                           const FrameUniforms& u, int frag_class, float t_min, const float* bg, int out_layout,
-                           hipStream_t s) {
+int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32_t classes, bool first_major,
+                           bool interleave, const FrameUniforms& u, int frag_class, float t_min, const float* bg,
+                           int out_layout, hipStream_t s) {
     const CompositeArgs a = make_args(u, t_min, bg, out_layout);
     CompViews cv{};
     for (int i = 0; i < k; ++i) {
@@ -1439,9 +1456,9 @@ int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32
                            f.tile_vals, f.recs, f.out, f.partial, f.sat, f.tmax};
     }
     cv.k = (uint32_t)k;
-    cv.classes = classes;
+    cv.classes = classes + (first_major ? 1u : 0u);  // first-major: the later chunks as one more class
     cv.view_blocks = (max_chunks + kCompWaves - 1) / kCompWaves;
-    cv.interleave = interleave && (uint32_t)k * classes <= 64u;
+    cv.interleave = interleave && (uint32_t)k * cv.classes <= 64u;
     const dim3 grid(cv.view_blocks * (unsigned)k);
     switch (frag_class) {
         case kFragGauss: k_composite_views<kFragGauss><<<grid, kCompThreads, 0, s>>>(cv, a); break;

@@ -344,12 +344,13 @@ struct FinishView {
 // binning: bin_tmp of each view holds its per-block instance counts
 int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s);
 int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s);
-int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, uint32_t classes,
+// first_major: every tile's first chunk dispatched before any later chunk
+int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, uint32_t classes, bool first_major,
                         hipStream_t s);
 // interleave: dispatch class-major over the views (k * classes <= 64), else view after view
-int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32_t classes, bool interleave,
-                           const FrameUniforms& u, int frag_class, float t_min, const float* bg, int out_layout,
-                           hipStream_t s);
+int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32_t classes, bool first_major,
+                           bool interleave, const FrameUniforms& u, int frag_class, float t_min, const float* bg,
+                           int out_layout, hipStream_t s);
 int launch_merge_views(FinishView* views, int k, const FrameUniforms& u, float t_min, const float* bg,
                        int out_layout, hipStream_t s);
 
