@@ -142,14 +142,15 @@ def test_shared_scene_pass_matches_serial_renders(gpu, batched_sorts, batched_fi
     scene.close()
 
 
-@pytest.mark.parametrize("interleave,classes,k", [("0", "2", 3), ("1", "2", 3), ("1", "8", 5), ("1", "16", 3),
-                                                  ("1", "16", 5)])
-def test_compositing_dispatch_orders(gpu, monkeypatch, interleave, classes, k):
+@pytest.mark.parametrize("interleave,classes,k,first", [("0", "2", 3, "1"), ("1", "2", 3, "1"), ("1", "8", 5, "1"),
+                                                        ("1", "16", 3, "1"), ("1", "16", 5, "1"), ("1", "8", 5, "0"),
+                                                        ("0", "8", 3, "0")])
+def test_compositing_dispatch_orders(gpu, monkeypatch, interleave, classes, k, first):
     """The compositor's dispatch order (chunk length classes; a group's views
     interleaved class-major, or view after view; k * classes > 64 falls back to
-    view after view) moves no pixel: a group's images equal each view rendered
-    alone.  Short chunks so that deep tiles have many and partials span the
-    classes."""
+    view after view; first chunks before later ones, or full chunks first)
+    moves no pixel: a group's images equal each view rendered alone.  Short
+    chunks so that deep tiles have many and partials span the classes."""
     import torch
 
     from gsviewer_amd.multiview import ViewBatchPipeline
@@ -158,6 +159,7 @@ def test_compositing_dispatch_orders(gpu, monkeypatch, interleave, classes, k):
     monkeypatch.setenv("GSR_CHUNK_VIEWS", "64")
     monkeypatch.setenv("GSR_LEN_CLASSES", classes)
     monkeypatch.setenv("GSR_VIEWS_INTERLEAVE", interleave)
+    monkeypatch.setenv("GSR_FIRST_MAJOR", first)
     scene, st, cams, ctxs, streams, outs = _setup(k)
     ref_ctx = HipContext()
     want = []
