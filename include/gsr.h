@@ -199,7 +199,9 @@ int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream);
  * while a deep tile's chunk runs), a frame finished alone in chunks of GSR_CHUNK (default 192:
  * latency); both read when the context is created.  Chunks are dispatched longest first (full
  * chunks, then GSR_LEN_CLASSES - 1 length classes of the last chunks, default 8), a group's
- * views interleaved class by class (GSR_VIEWS_INTERLEAVE=0: view after view).
+ * views interleaved class by class (GSR_VIEWS_INTERLEAVE=0: view after view); a group dispatches
+ * every tile's first chunk before any later chunk (GSR_FIRST_MAJOR=0: full chunks first), so a
+ * deep tile saturated by its first chunk skips the rest.
  * Results are identical to k gsr_render_finish calls (and independent of the dispatch order). */
 int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream);
 
