@@ -204,6 +204,41 @@ def valu_issue(kernel, args, ms_per_launch):
             "issue_ns_per_instr": {"valu": VALU_NS, "trans": TRANS_NS}, "source": src}
 
 
+def frame_valu_issue(args, share, ms_per_frame):
+    """VALU issue of the frame in flight over all its kernels (tools/frame_valu.py):
+    the view-batched kernels' SQ_INSTS_VALU (+ transcendentals) per view-frame
+    from the same committed PMC summary, priced like valu_issue, against the
+    measured frame time.  With views in flight the frame is VALU-issue bound
+    (DESIGN.md, "The frame in flight: VALU issue over all kernels")."""
+    if share <= 1 or args.config != "c2" or args.n or args.width or args.height or args.box != "none":
+        return None
+    import csv
+    try:
+        d = open(PMC_PROFILE).read().strip()
+        with open(os.path.join(ROOT, "profiles", d, "pmc_summary.csv")) as fh:
+            rows = list(csv.reader(fh))[1:]  # (kernel names hold commas: "k_rs_scatter_views<8, true, 8>")
+    except OSError:
+        return None
+    valu, trans, disp = {}, {}, {}
+    for r in rows:
+        k = r[0]
+        if "_views" not in k:
+            continue
+        if r[1] == "SQ_INSTS_VALU":
+            valu[k], disp[k] = float(r[4]), int(r[2])
+        elif r[1] == "SQ_INSTS_VALU_TRANS_F32":
+            trans[k] = float(r[4])
+    groups = disp.get("k_composite_views<0>")
+    if not groups:
+        return None
+    v = sum(valu[k] * disp[k] for k in valu) / groups / share
+    t = sum(trans.get(k, 0.0) * disp[k] for k in valu) / groups / share
+    issue_us = (VALU_NS * (v - t) + TRANS_NS * t) * 1e-3 / SIMDS
+    return {"valu_instr_per_view_frame": v, "trans_instr_per_view_frame": t, "issue_us": issue_us,
+            "frame_us": ms_per_frame * 1e3, "frac": issue_us / (ms_per_frame * 1e3),
+            "source": f"profiles/{d}/pmc_summary.csv (*_views kernels)"}
+
+
 def _free_port():
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -492,6 +527,7 @@ def main():
             roof["traffic"], roof["traffic_source"] = traffic
         if dom == "composite":
             roof["valu_issue"] = valu_issue(KERNEL_SYMBOL[dom], args, stage[dom])
+        roof["frame_valu_issue"] = frame_valu_issue(args, share, ms_per_step)
 
     cpu = None
     if not args.no_cpu_baseline and world == 1 and g is not None:
