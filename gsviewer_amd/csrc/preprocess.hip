@@ -136,8 +136,11 @@ __device__ __forceinline__ void alpha_box(float qa, float qb, float qc, float th
     const float d4 = (4.0f * qa) * qc;
     const float disc = d4 - qb * qb;
     if (!(qa < 0.0f && qc < 0.0f && disc > 1e-2f * d4)) return;
-    const float hx = sqrtf(thr / (qa - (qb * qb) / (4.0f * qc))) * 1.002f + 0.01f;
-    const float hy = sqrtf(thr / (qc - (qb * qb) / (4.0f * qa))) * 1.002f + 0.01f;
+    // half-extents of {q >= thr}: hx^2 = thr / (qa - qb^2 / 4qc) = qc * 4 thr / disc, and hy^2 likewise
+    // with qa (one correctly rounded division instead of four; the margin covers the rounding)
+    const float s4 = (4.0f * thr) / disc;
+    const float hx = sqrtf(qc * s4) * 1.002f + 0.01f;
+    const float hy = sqrtf(qa * s4) * 1.002f + 0.01f;
     if (!(hx < 65536.0f && hy < 65536.0f)) return;  // (cx, cy are within 1.3x of the viewport)
     // pixel p is a candidate if its centre p + 0.5 is within [c - h, c + h]
     const int bx0 = (int)ceilf((cx - hx) - 0.5f), bx1 = (int)floorf((cx + hx) - 0.5f);

@@ -196,8 +196,9 @@ def alpha_box_rects(rec, rects, height):
         d4 = (F(4.0) * qa) * qc
         disc = d4 - qb * qb
         ok = ~empty & (qa < F(0.0)) & (qc < F(0.0)) & (disc > F(1e-2) * d4)
-        hx = np.sqrt(thr / (qa - (qb * qb) / (F(4.0) * qc))) * F(1.002) + F(0.01)
-        hy = np.sqrt(thr / (qc - (qb * qb) / (F(4.0) * qa))) * F(1.002) + F(0.01)
+        s4 = (F(4.0) * thr) / disc
+        hx = np.sqrt(qc * s4) * F(1.002) + F(0.01)
+        hy = np.sqrt(qa * s4) * F(1.002) + F(0.01)
         ok &= (hx < F(65536.0)) & (hy < F(65536.0))
         bx0 = np.ceil((cx - hx) - F(0.5)); bx1 = np.floor((cx + hx) - F(0.5))
         bj0 = np.ceil((cy - hy) - F(0.5)); bj1 = np.floor((cy + hy) - F(0.5))
