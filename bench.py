@@ -357,9 +357,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    # Rehearsal of the multi-rank GPU path on a one-GPU box (GSR_BENCH_SHARED_GPU=1):
+    # every rank renders on device 0 and the process group is gloo (RCCL refuses
+    # two ranks on one GPU).  Launch, broadcast, per-rank views and the
+    # max-over-ranks timing are the driver's N-GPU run; the rate is not.
+    shared_gpu = world > 1 and os.environ.get("GSR_BENCH_SHARED_GPU", "0") == "1"
+    if shared_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if shared_gpu:
+        dist.init_process_group("gloo")
+    elif world > 1:
         dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI on ROCm
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
@@ -567,7 +576,8 @@ def main():
         "cpu_baseline": cpu,
         "broadcast": bcast,
         "process_group": {"backend": dist.get_backend() if world > 1 else None,
-                          "world_size": dist.get_world_size() if world > 1 else 1},
+                          "world_size": dist.get_world_size() if world > 1 else 1,
+                          "rehearsal_shared_gpu": shared_gpu},
         "per_rank": per_rank,
         "scene_gen_s": t_gen,
     }
