@@ -111,6 +111,9 @@ SIGNATURES = {
     "gsr_context_destroy": (ctypes.c_int, [_P]),
     "gsr_context_reserve": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, _P]),
     "gsr_context_workspace": (ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_int64)]),
+    "gsr_workspace_size": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64]),
+    "gsr_context_attach_workspace": (ctypes.c_int, [_P, _P, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int32,
+                                                    ctypes.c_int32, ctypes.c_int64, _P]),
     "gsr_render": (ctypes.c_int, [_P, _P, ctypes.POINTER(GsrCamera), ctypes.POINTER(GsrSettings), _P, _P, _P]),
     "gsr_render_begin": (ctypes.c_int, [_P, _P, ctypes.POINTER(GsrCamera), ctypes.POINTER(GsrSettings), _P, _P, _P]),
     "gsr_render_finish": (ctypes.c_int, [_P, _P]),
@@ -145,7 +148,7 @@ STAGES = ["cull", "preprocess", "depth_sort", "binning", "tile_sort", "tile_rang
 
 GSR_DEBUG_RECORDS, GSR_DEBUG_DEPTH_ORDER, GSR_DEBUG_TILE_RANGES, GSR_DEBUG_TILE_LIST = 0, 1, 2, 3
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_VIEWS = 8  # GSR_MAX_VIEWS (include/gsr.h)
 
 _lib = None

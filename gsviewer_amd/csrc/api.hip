@@ -35,6 +35,17 @@ int set_error(int code, const std::string& msg) {
     return code;
 }
 
+// A caller-provided workspace (gsr_context_attach_workspace), or with
+// `measure` set the sizing pass of gsr_workspace_size: a context's buffers are
+// carved off it in order, 256-B aligned, and nothing is returned to it.
+struct Arena {
+    char* base = nullptr;
+    size_t bytes = 0;
+    size_t used = 0;
+    bool measure = false;
+};
+constexpr size_t kArenaAlign = 256;
+
 namespace {
 
 // A context-owned device array that grows on demand.  Growth never frees the
@@ -42,19 +53,34 @@ namespace {
 // every other view in flight, and the context's previous frame may still read
 // the old block.  Retired blocks are freed with the context (release()).
 // gsr_context_reserve sizes everything up front, so a steady state never grows.
+// With an arena (caller workspace) the blocks come from it instead, and a
+// buffer that outgrows it fails the call with GSR_ERR_NOMEM.
 template <typename T>
 struct DevBuf {
     T* p = nullptr;
     size_t cap = 0;  // elements
     int64_t allocs = 0;  // allocations made (gsr_context_workspace)
     std::vector<void*> retired;
+    Arena* arena = nullptr;
     int ensure(size_t n, const char* what) {
         if (n <= cap && p) return GSR_OK;
         size_t want = n < 64 ? 64 : n + n / 8;  // 12.5% headroom against regrowth
         T* q = nullptr;
-        if (hipMalloc(&q, want * sizeof(T)) != hipSuccess)
+        if (arena) {
+            const size_t off = (arena->used + kArenaAlign - 1) & ~(kArenaAlign - 1);
+            const size_t end = off + want * sizeof(T);
+            if (!arena->measure && end > arena->bytes)
+                return set_error(GSR_ERR_NOMEM, std::string("context: the caller's workspace (") +
+                                                    std::to_string(arena->bytes) + " B) is too small for " + what +
+                                                    " (gsr_workspace_size gives the bytes a bound needs)");
+            arena->used = end;
+            // measuring: a stand-in address that is never dereferenced
+            q = arena->measure ? reinterpret_cast<T*>((uintptr_t)(kArenaAlign + off))
+                               : reinterpret_cast<T*>(arena->base + off);
+        } else if (hipMalloc(&q, want * sizeof(T)) != hipSuccess) {
             return set_error(GSR_ERR_NOMEM, std::string("context: hipMalloc failed for ") + what);
-        if (p) retired.push_back(p);
+        }
+        if (p && !arena) retired.push_back(p);
         p = q;
         cap = want;
         ++allocs;
@@ -62,6 +88,11 @@ struct DevBuf {
     }
     size_t bytes() const { return cap * sizeof(T); }
     void release() {
+        if (arena) {  // the caller owns the memory
+            p = nullptr;
+            cap = 0;
+            return;
+        }
         if (p) (void)hipFree(p);
         for (void* r : retired) (void)hipFree(r);
         retired.clear();
@@ -149,6 +180,8 @@ struct gsr_context {
     int64_t prof_frames = 0;
     bool failed = false;           // a wait timed out or the stream faulted: no further frames
     int64_t wait_timeout_ms = 2000;
+    gsr::Arena arena;              // caller workspace (gsr_context_attach_workspace) or sizing pass
+    bool has_arena = false;
 };
 
 namespace gsr {
@@ -284,6 +317,10 @@ int ensure_scene_buffers(gsr_context* c, size_t n, hipStream_t s) {
     if ((rc = c->rect4_b.ensure(n, "rect4"))) return rc;
     if ((rc = c->bin_tmp.ensure(bin_tmp_elems(n), "bin_tmp"))) return rc;
     if ((rc = c->radix_tmp.ensure(radix_tmp_elems(n), "radix_tmp"))) return rc;
+    if (c->has_arena && c->arena.measure) {  // gsr_workspace_size: sizes only, no HIP call
+        if (!c->done_ctr.p) return c->done_ctr.ensure(1, "done_ctr");
+        return GSR_OK;
+    }
     if (!c->done_ctr.p) {
         if ((rc = c->done_ctr.ensure(1, "done_ctr"))) return rc;
         GSR_HIP_CHECK(hipMemsetAsync(c->done_ctr.p, 0, c->done_ctr.cap * sizeof(unsigned long long), s));
@@ -630,6 +667,9 @@ int gsr_context_reserve(gsr_context* c, int64_t n, int32_t width, int32_t height
     const size_t d = max_instances > 0 ? (size_t)max_instances : 4 * un;
     const int num_tiles = ((width + kTile - 1) / kTile) * ((height + kTile - 1) / kTile);
     int rc;
+    // the shared radix scratch at its final size first: a smaller block sized by
+    // ensure_scene_buffers would be retired (and, in a caller's workspace, wasted)
+    if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(d), radix_tmp_elems(un)), "radix_tmp"))) return rc;
     if ((rc = ensure_scene_buffers(c, un, s))) return rc;
     if ((rc = c->zero.ensure(ZeroLayout(num_tiles).total, "zero block"))) return rc;
     if ((rc = c->tkeys_a.ensure(d, "tile_keys"))) return rc;
@@ -656,6 +696,38 @@ int64_t gsr_context_workspace(gsr_context* c, int64_t* n_allocations) {
     });
     if (n_allocations) *n_allocations = allocs;
     return bytes;
+}
+
+int64_t gsr_workspace_size(int64_t n, int32_t width, int32_t height, int64_t max_instances) {
+    gsr_context* c = nullptr;
+    int rc = gsr_context_create(&c);
+    if (rc) return rc;
+    c->has_arena = true;
+    c->arena.measure = true;
+    gsr::each_buf(c, [&](auto& b) { b.arena = &c->arena; });
+    rc = gsr_context_reserve(c, n, width, height, max_instances, nullptr);
+    const int64_t bytes = (int64_t)(c->arena.used + gsr::kArenaAlign);  // + slack for an unaligned base
+    delete c;  // nothing was allocated
+    return rc ? (int64_t)rc : bytes;
+}
+
+int gsr_context_attach_workspace(gsr_context* c, void* ws_dev, size_t ws_bytes, int64_t n, int32_t width,
+                                 int32_t height, int64_t max_instances, void* stream) {
+    if (!c || !ws_dev) return gsr::set_error(GSR_ERR_INVALID, "null argument");
+    bool fresh = !c->has_arena;
+    gsr::each_buf(c, [&](auto& b) { fresh = fresh && b.p == nullptr; });
+    if (!fresh)
+        return gsr::set_error(GSR_ERR_INVALID,
+                              "context_attach_workspace: the context already holds a workspace (use a new context)");
+    // carve from the first 256-B boundary of the caller's block
+    const uintptr_t a = ((uintptr_t)ws_dev + gsr::kArenaAlign - 1) & ~(uintptr_t)(gsr::kArenaAlign - 1);
+    const size_t skip = (size_t)(a - (uintptr_t)ws_dev);
+    c->has_arena = true;
+    c->arena = gsr::Arena{};
+    c->arena.base = reinterpret_cast<char*>(a);
+    c->arena.bytes = ws_bytes > skip ? ws_bytes - skip : 0;
+    gsr::each_buf(c, [&](auto& b) { b.arena = &c->arena; });
+    return gsr_context_reserve(c, n, width, height, max_instances, stream);
 }
 
 int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, float* out,

@@ -157,6 +157,18 @@ class HipContext:
         _lib.check(_lib.load().gsr_context_reserve(self._h, int(n), int(width), int(height), int(max_instances),
                                                    _stream_handle(stream)), "gsr_context_reserve")
 
+    def attach_workspace(self, ws, n: int, width: int, height: int, max_instances: int = 0, stream=None):
+        """gsr_context_attach_workspace: carve every buffer of this (new)
+        context out of ``ws``, a caller-owned device tensor of at least
+        ``workspace_size(n, width, height, max_instances)`` bytes, which this
+        context keeps alive.  Frames beyond the bounds then raise instead of
+        allocating."""
+        nbytes = ws.numel() * ws.element_size()
+        _lib.check(_lib.load().gsr_context_attach_workspace(
+            self._h, ctypes.c_void_p(ws.data_ptr()), nbytes, int(n), int(width), int(height), int(max_instances),
+            _stream_handle(stream)), "gsr_context_attach_workspace")
+        self._ws = ws
+
     def workspace(self):
         """(device bytes held, device allocations made so far)."""
         allocs = ctypes.c_int64()
@@ -172,14 +184,25 @@ class HipContext:
 
     def close(self):
         if getattr(self, "_h", None):
-            _lib.load().gsr_context_destroy(self._h)
+            _lib.load().gsr_context_destroy(self._h)  # synchronises: the workspace is free after it
             self._h = None
+        self._ws = None
 
     def __del__(self):
         try:
             self.close()
         except Exception:
             pass
+
+
+def workspace_size(n: int, width: int, height: int, max_instances: int = 0) -> int:
+    """gsr_workspace_size: device bytes one context needs for scenes of <= n
+    Gaussians and frames of <= width x height (<= max_instances tile
+    instances, 0 = 4 n).  Needs no GPU."""
+    b = _lib.load().gsr_workspace_size(int(n), int(width), int(height), int(max_instances))
+    if b < 0:
+        _lib.check(int(b), "gsr_workspace_size")
+    return int(b)
 
 
 class RenderSettings:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 5
+#define GSR_ABI_VERSION 6
 
 typedef enum gsr_status {
     GSR_OK = 0,
@@ -143,6 +143,23 @@ int gsr_context_reserve(gsr_context* ctx, int64_t n, int32_t width, int32_t heig
 /* Device bytes the context holds now (retired blocks excluded), or < 0 on
  * error; *n_allocations (nullable) = device allocations made so far. */
 int64_t gsr_context_workspace(gsr_context* ctx, int64_t* n_allocations);
+
+/* Caller-provided workspace ("writes into caller-provided output
+ * and workspace"; the reference's caller owns every buffer it hands the
+ * rasterizer, renderer_cuda.py:94-100, 230-243).
+ * gsr_workspace_size: device bytes one context needs for scenes of <= n
+ * Gaussians, frames of <= width x height and <= max_instances tile instances
+ * (<= 0: 4 n), or < 0 (a GSR_ERR_*) on bad arguments.  No HIP call: it runs
+ * without a GPU.
+ * gsr_context_attach_workspace: a new context takes ws_dev[0, ws_bytes) (device
+ * memory the caller owns and keeps alive until gsr_context_destroy) for all of
+ * its buffers instead of allocating, sized for the same bounds; GSR_ERR_NOMEM
+ * if ws_bytes < gsr_workspace_size(...).  Frames within the bounds then never
+ * allocate device memory; a frame beyond them fails with GSR_ERR_NOMEM instead
+ * of growing.  Only a context that holds no buffers yet can attach one. */
+int64_t gsr_workspace_size(int64_t n, int32_t width, int32_t height, int64_t max_instances);
+int gsr_context_attach_workspace(gsr_context* ctx, void* ws_dev, size_t ws_bytes, int64_t n, int32_t width,
+                                 int32_t height, int64_t max_instances, void* stream);
 
 /* Render one frame: cull + project + SH (preprocess), depth radix sort,
  * tile binning + stable tile sort, 16x16-tile front-to-back compositing.

@@ -81,3 +81,19 @@ int main(void){
             S.cube_rotation.offset, S.bg.offset,
             S.t_min.offset, S.out_layout.offset, C.hfovxy_focal.offset, C.height.offset]
     assert [int(x) for x in got] == want
+
+
+def test_workspace_size_needs_no_gpu():
+    """gsr_workspace_size sizes a caller-provided workspace on the host alone:
+    it grows with every bound and rejects bad arguments."""
+    from gsviewer_amd.rasterizer import workspace_size
+    base = workspace_size(100_000, 640, 480, 0)
+    assert base > 100_000 * 48
+    assert workspace_size(200_000, 640, 480, 0) > base
+    assert workspace_size(100_000, 1920, 1080, 0) > base
+    assert workspace_size(100_000, 640, 480, 1_000_000) > base
+    assert workspace_size(100_000, 640, 480, 0) == base
+    with pytest.raises(RuntimeError, match="context_reserve"):
+        workspace_size(-1, 640, 480, 0)
+    with pytest.raises(RuntimeError, match="context_reserve"):
+        workspace_size(10, 0, 480, 0)

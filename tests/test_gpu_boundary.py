@@ -337,6 +337,68 @@ def test_context_reserve_means_no_allocation_in_frames(gpu):
     big.close()
 
 
+def test_caller_provided_workspace(gpu):
+    """gsr_workspace_size + gsr_context_attach_workspace (the
+    rasterizer writes into caller-provided output and workspace): a context
+    carved out of a caller's device tensor (unaligned base) renders the same
+    images as a self-allocating one, makes no allocation of its own, and a
+    frame beyond its bounds or a too-small workspace fails loudly."""
+    from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into, workspace_size
+    n, w, h, d = 50_000, 640, 480, 400_000
+    need = workspace_size(n, w, h, d)
+    probe = HipContext()
+    probe.reserve(n, w, h, max_instances=d)
+    held, _ = probe.workspace()
+    probe.close()
+    assert held <= need <= held + 256 * 32
+    g = random_scene(n, sh_degree=1, seed=11)
+    scene = HipScene.from_gaussian_data(g)
+    base = torch.empty(need + 7, dtype=torch.uint8, device="cuda")
+    ws = base[7:]
+    ws.fill_(0xAB)  # the context must not rely on zeroed memory
+    torch.cuda.synchronize()
+    ctx = HipContext()
+    ctx.attach_workspace(ws, n, w, h, max_instances=d)
+    torch.cuda.synchronize()  # the attach zeroes the completion counter on the null stream
+    b0, a0 = ctx.workspace()
+    assert b0 == held
+    st = RenderSettings(out_layout=0)
+    ref_ctx = HipContext()
+    s = torch.cuda.Stream()
+    for yaw in (0.0, 40.0, 80.0):
+        for ww, hh in ((640, 480), (320, 200)):
+            cam = camera_from(Camera(hh, ww).yaw(yaw))
+            out = torch.empty((3, hh, ww), dtype=torch.float32, device="cuda")
+            ref = torch.empty_like(out)
+            render_into(ctx, scene, cam, st, out, stream=s)
+            render_into(ref_ctx, scene, cam, st, ref)
+            s.synchronize()
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref)
+    assert ctx.workspace() == (b0, a0)
+    # the frames wrote into the caller's tensor (it was filled with 0xAB before the attach)
+    assert int((ws != 0xAB).sum()) > 50_000
+    big = HipScene.from_gaussian_data(random_scene(120_000, sh_degree=1, seed=12))
+    out = torch.empty((3, h, w), dtype=torch.float32, device="cuda")
+    with pytest.raises(RuntimeError, match="too small"):
+        render_into(ctx, big, camera_from(Camera(h, w)), st, out)
+    torch.cuda.synchronize()
+    ctx.close()
+    small = HipContext()
+    with pytest.raises(RuntimeError, match="too small"):
+        small.attach_workspace(ws[: need // 2], n, w, h, max_instances=d)
+    small.close()
+    used = HipContext()
+    render_into(used, scene, camera_from(Camera(h, w)), st, out)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="already holds"):
+        used.attach_workspace(ws, n, w, h, max_instances=d)
+    used.close()
+    ref_ctx.close()
+    scene.close()
+    big.close()
+
+
 def test_wait_for_counts_has_a_deadline(gpu, monkeypatch):
     """A stream that makes no progress fails gsr_render_finish with
     GSR_ERR_HIP after GSR_WAIT_TIMEOUT_MS instead of hanging the host; the
