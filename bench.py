@@ -245,6 +245,27 @@ def _free_port():
         return sk.getsockname()[1]
 
 
+def measured_copy_gbps(dev, nbytes=1 << 31, reps=5):
+    """This box's device-to-device copy rate (read + write bytes / s) over a
+    2 GiB buffer, 8x the Infinity Cache, so it streams from HBM (SURVEY 8(d):
+    record the measured stream copy beside the 8 TB/s spec peak)."""
+    import torch
+    src = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    for _ in range(2):
+        dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    e1.synchronize()
+    gbps = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return gbps
+
+
 def launch_ranks(n, argv):
     """Start n ranks of this script under torch.distributed.run as a child
     process (one process per GPU, rendezvous on 127.0.0.1) and return its
@@ -461,6 +482,18 @@ def main():
         own[0] *= args.steps / timed_frames
     # single-view latency: the same number of frames of view 0, one at a time
     latency = timed_region(serial_frame, args.steps, dev) if K > 1 else elapsed
+    # SURVEY 8(d)'s GPU timing: the median of per-frame times, one frame at a
+    # time, each bracketed by device synchronizes (so it includes one host
+    # round trip per frame)
+    per_frame = []
+    for _ in range(max(args.steps, 20)):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        serial_frame()
+        torch.cuda.synchronize(dev)
+        per_frame.append(time.perf_counter() - t0)
+    latency_median_ms = 1e3 * float(np.median(per_frame))
+    copy_gbps = measured_copy_gbps(dev)
 
     # Per-stage times: a third region (view 0, one at a time) with libgsr's
     # HIP events recorded on the render stream between the stages.
@@ -529,7 +562,8 @@ def main():
         roof = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg,
                 "ms_per_launch": stage[dom], "traffic_source": None,
-                "frame": {"bytes": b_frame, "GBps": b_frame * fps / 1e9, "frac": b_frame * fps / 1e9 / HBM_PEAK_GBS}}
+                "frame": {"bytes": b_frame, "GBps": b_frame * fps / 1e9, "frac": b_frame * fps / 1e9 / HBM_PEAK_GBS},
+                "measured_copy_GBps": copy_gbps}
 
         traffic = pmc_traffic(KERNEL_SYMBOL.get(dom), args)
         if traffic:
@@ -553,6 +587,7 @@ def main():
         "ms_per_step": ms_per_step,
         "fps_per_gpu": fps,
         "latency_ms_per_frame": 1e3 * latency / args.steps,
+        "latency_ms_median": latency_median_ms,
         "views_in_flight": K,
         "splats_per_s_per_gpu": value / world,
         "higher_is_better": True,
