@@ -368,16 +368,28 @@ __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, in
     const int w = threadIdx.x >> 6;
     if (w == 0) {  // wave 0: offsets of this block = sums of the earlier blocks' totals
         uint32_t* cls_tot = const_cast<uint32_t*>(tot) + (1 + classes) * gridDim.x;
-        uint32_t run = 0;  // class bases: full chunks, then the partial classes in order
-        for (uint32_t j = 0; j <= classes; ++j) {
-            uint32_t p = 0, a = 0;
-            for (uint32_t b = __lane_id(); b < gridDim.x; b += 64) {
-                const uint32_t v = tot[j * gridDim.x + b];
-                p += b < blockIdx.x ? v : 0u;
-                a += v;
+        // every row's loads issued before any is summed: one memory round trip,
+        // not one per class (a row-by-row loop waited 1 + classes times)
+        uint32_t ps[1 + kMaxLenClasses], as[1 + kMaxLenClasses];
+#pragma unroll
+        for (int j = 0; j <= kMaxLenClasses; ++j) ps[j] = as[j] = 0u;
+        for (uint32_t b = __lane_id(); b < gridDim.x; b += 64) {
+            uint32_t v[1 + kMaxLenClasses];
+#pragma unroll
+            for (int j = 0; j <= kMaxLenClasses; ++j) v[j] = (uint32_t)j <= classes ? tot[j * gridDim.x + b] : 0u;
+#pragma unroll
+            for (int j = 0; j <= kMaxLenClasses; ++j) {
+                ps[j] += b < blockIdx.x ? v[j] : 0u;
+                as[j] += v[j];
             }
-            p = wave_reduce_sum(p);
-            a = wave_reduce_sum(a);
+        }
+        uint32_t run = 0;  // class bases: full chunks, then the partial classes in order
+#pragma unroll
+        for (int jj = 0; jj <= kMaxLenClasses; ++jj) {
+            const uint32_t j = (uint32_t)jj;
+            if (j > classes) continue;  // (uniform; `break` blocks the unrolling)
+            const uint32_t p = wave_reduce_sum(ps[jj]);
+            const uint32_t a = wave_reduce_sum(as[jj]);
             if (__lane_id() == 0) {
                 sh.pre[j] = p;
                 if (j == 0 && blockIdx.x == 0) cls_tot[classes] = a;  // the later chunks (first-major order)
@@ -438,9 +450,11 @@ __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, in
     while (multi) {
         const int src = (int)__builtin_ctzll(multi);
         multi &= multi - 1;
-        const uint32_t tt = __shfl((uint32_t)t, src, 64), rx = __shfl(r.x, src, 64), ry = __shfl(r.y, src, 64);
-        const uint32_t c = __shfl(cnt, src, 64), f = __shfl(full, src, 64), bs = __shfl(base, src, 64);
-        const uint32_t fb = __shfl(full_before, src, 64), pp = __shfl(part_pos, src, 64);
+        // src is wave-uniform: v_readlane into SGPRs, no LDS permute round trips
+        auto rl = [src](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, src); };
+        const uint32_t tt = rl((uint32_t)t), rx = rl(r.x), ry = rl(r.y);
+        const uint32_t c = rl(cnt), f = rl(full), bs = rl(base);
+        const uint32_t fb = rl(full_before), pp = rl(part_pos);
         for (uint32_t j = 1 + __lane_id(); j < c; j += 64) emit(tt, rx, ry, c, f, bs, fb, pp, j);
     }
 }
