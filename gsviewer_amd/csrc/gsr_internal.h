@@ -128,20 +128,29 @@ __device__ __forceinline__ uint64_t match_digit8(uint32_t digit, bool valid) {
     return peers;
 }
 
-// Inclusive wave scan (64 lanes).
+// Inclusive wave scan (64 lanes) with DPP lane moves, no LDS round trips (a
+// __shfl_up is a ds_bpermute: six dependent LDS trips per scan):
+// row_shr:1/2/4/8 scan each 16-lane row, then row_bcast:15 adds row 0's total
+// to row 1 and row 2's to row 3, and row_bcast:31 adds lane 31's (rows 0-1)
+// to rows 2-3.  Lanes a DPP move has no source for (or rows it masks off)
+// read `old` = 0.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_move0(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
 __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o, 64);
-        if (__lane_id() >= o) v += t;
-    }
+    v += dpp_move0<0x111>(v);        // row_shr:1
+    v += dpp_move0<0x112>(v);        // row_shr:2
+    v += dpp_move0<0x114>(v);        // row_shr:4
+    v += dpp_move0<0x118>(v);        // row_shr:8
+    v += dpp_move0<0x142, 0xa>(v);   // row_bcast:15 -> rows 1, 3
+    v += dpp_move0<0x143, 0xc>(v);   // row_bcast:31 -> rows 2, 3
     return v;
 }
 
+// Sum over the wave, in every lane (the scan's last lane, broadcast).
 __device__ __forceinline__ uint32_t wave_reduce_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_scan(v), 63);
 }
 
 // Exclusive scan of one value per thread across a block of NT threads.

@@ -157,6 +157,7 @@ __global__ __launch_bounds__(kThreads) void k_rs_upsweep(const uint32_t* __restr
 }
 
 // One wave per digit d: exclusive scan of row d (ntiles counts) in place; row total out.
+constexpr uint32_t kOffRegs = 16;  // counts per lane held in registers
 __device__ __forceinline__ void rs_offsets(uint32_t* __restrict__ hist, uint32_t ntiles, const PassArgs& pa,
                                            uint32_t* __restrict__ totals, uint32_t d) {
     const Digit dg = digit_params(pa);
@@ -165,6 +166,23 @@ __device__ __forceinline__ void rs_offsets(uint32_t* __restrict__ hist, uint32_t
     const uint32_t per = (ntiles + 63) / 64;
     const uint32_t b0 = __lane_id() * per;
     const uint32_t b1 = min(ntiles, b0 + per);
+    if (per <= kOffRegs) {  // rows of <= 64 * kOffRegs tiles (1M keys: 489): one load round trip, counts in registers
+        uint32_t c[kOffRegs];
+#pragma unroll
+        for (uint32_t k = 0; k < kOffRegs; ++k) c[k] = b0 + k < b1 ? row[b0 + k] : 0u;
+        uint32_t s = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kOffRegs; ++k) s += c[k];
+        const uint32_t inc = wave_inclusive_scan(s);
+        uint32_t run = inc - s;
+#pragma unroll
+        for (uint32_t k = 0; k < kOffRegs; ++k) {
+            if (b0 + k < b1) row[b0 + k] = run;
+            run += c[k];
+        }
+        if (__lane_id() == 63) totals[d] = inc;
+        return;
+    }
     uint32_t s = 0;
     for (uint32_t i = b0; i < b1; ++i) s += row[i];
     const uint32_t inc = wave_inclusive_scan(s);
