@@ -148,6 +148,18 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
     return v;
 }
 
+// Unsigned max over the wave, in every lane: the same DPP prefix pattern with
+// max (a lane with no DPP source reads 0, the identity of unsigned max).
+__device__ __forceinline__ uint32_t wave_reduce_max(uint32_t v) {
+    v = max(v, dpp_move0<0x111>(v));
+    v = max(v, dpp_move0<0x112>(v));
+    v = max(v, dpp_move0<0x114>(v));
+    v = max(v, dpp_move0<0x118>(v));
+    v = max(v, dpp_move0<0x142, 0xa>(v));
+    v = max(v, dpp_move0<0x143, 0xc>(v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // Sum over the wave, in every lane (the scan's last lane, broadcast).
 __device__ __forceinline__ uint32_t wave_reduce_sum(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_scan(v), 63);

@@ -175,12 +175,7 @@ __device__ __forceinline__ void cull_view(const float4 p, bool in_range, int64_t
         wave_counts[i >> 6] = (uint32_t)__popcll(m);
     }
     // depth-key range of the visible Gaussians ({~kmin, kmax}, componentwise max)
-    uint32_t a = vis ? ~key : 0u, b = vis ? key : 0u;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        a = max(a, (uint32_t)__shfl_xor((int)a, o, 64));
-        b = max(b, (uint32_t)__shfl_xor((int)b, o, 64));
-    }
+    const uint32_t a = wave_reduce_max(vis ? ~key : 0u), b = wave_reduce_max(vis ? key : 0u);
     if (__lane_id() == 0) s_kr[threadIdx.x >> 6] = make_uint2(a, b);
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -70,11 +70,8 @@ __device__ __forceinline__ void reduce_ranges(const uint2* __restrict__ kr_in, s
         m.x = max(m.x, v.x);
         m.y = max(m.y, v.y);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        m.x = max(m.x, (uint32_t)__shfl_xor((int)m.x, o, 64));
-        m.y = max(m.y, (uint32_t)__shfl_xor((int)m.y, o, 64));
-    }
+    m.x = wave_reduce_max(m.x);
+    m.y = wave_reduce_max(m.y);
     if (__lane_id() == 0) lds[threadIdx.x >> 6] = m;
     __syncthreads();
     if (threadIdx.x == 0) {
