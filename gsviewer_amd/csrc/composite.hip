@@ -966,10 +966,12 @@ __device__ __forceinline__ int interleaved_chunk(const CompViews& vs, uint32_t p
     if (hit == 0) return -1;
     const int q = (int)__builtin_ctzll(hit);
     const uint32_t c = (uint32_t)q / vs.k, v = (uint32_t)q - c * vs.k;
-    const uint32_t q_excl = __shfl(q_incl - nq, q, 64);
+    // (q, v, c are wave-uniform: readlane, not an LDS permute)
+    const uint32_t q_excl = (uint32_t)__builtin_amdgcn_readlane((int)(q_incl - nq), q);
     // the view's own dispatch position: its chunks of the earlier classes first
     const uint32_t vm_excl = vm_incl - n;
-    const uint32_t cls_base = __shfl(vm_excl, (int)(v * vs.classes + c), 64) - __shfl(vm_excl, (int)(v * vs.classes), 64);
+    const uint32_t cls_base = (uint32_t)__builtin_amdgcn_readlane((int)vm_excl, (int)(v * vs.classes + c)) -
+                              (uint32_t)__builtin_amdgcn_readlane((int)vm_excl, (int)(v * vs.classes));
     pos = cls_base + (p - q_excl);
     return (int)v;
 }
