@@ -105,7 +105,39 @@ def host_cpu():
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count()
-    return dict(cpu_model=model, nproc=os.cpu_count(), affinity_cpus=usable)
+    return dict(cpu_model=model, nproc=os.cpu_count(), affinity_cpus=usable, cgroup_quota_cpus=cgroup_cpus())
+
+
+def cgroup_cpus():
+    """CPUs this process's cgroup may use (cpu.max quota / period), or None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota != "max":
+                return max(1, int(int(quota) // int(period)))
+        except (OSError, ValueError):
+            pass
+    return None
+
+
+def baseline_threads():
+    """Threads for the CPU baseline: every host core this process may use
+    (OpenMP over all host cores), i.e. its CPU affinity capped by
+    its cgroup's CPU quota, unless OMP_NUM_THREADS says otherwise (the GPU
+    pool sets 16: its boxes grant one GPU's share of a 256-CPU host, and
+    threads beyond a quota only time-slice).  Returns (threads, reason)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    quota = cgroup_cpus()
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env > 0:
+        return env, (f"OMP_NUM_THREADS={env} (the environment's CPU share; affinity {usable} CPUs, "
+                     f"cgroup quota {quota if quota else 'none'})")
+    if quota and quota < usable:
+        return quota, f"all CPUs the cgroup quota grants ({quota}; affinity {usable})"
+    return usable, f"all CPUs in this process's affinity ({usable})"
 
 
 def cpu_baseline(g, cam, seconds):
@@ -117,7 +149,7 @@ def cpu_baseline(g, cam, seconds):
     of _sort_gaussian_cpu (renderer_ogl.py:16-26: view-z dot + argsort)."""
     from oracle import c_oracle as C
     from oracle import gl_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    threads, why = baseline_threads()
     U = O.default_uniforms(cam.get_view_matrix(), cam.get_project_matrix(),
                            np.asarray(cam.get_htanfovxy_focal(), np.float32), cam.position, cam.w, cam.h)
     flat = g.flat()
@@ -152,7 +184,8 @@ def cpu_baseline(g, cam, seconds):
                       f"through oracle/gl_oracle.c (OGL-path restatement: vertex stage, parallel radix depth "
                       f"sort, rect raster + fragment + blend), {threads} OpenMP threads, after one untimed frame",
                ms_per_frame=1e3 * t_total / frames,
-               sort_ms={"port_radix_all_threads": sort_mt, "port_radix_1thread": sort_1t,
+               threads_reason=why,
+               sort_ms={f"port_radix_{threads}threads": sort_mt, "port_radix_1thread": sort_1t,
                         "reference_numpy_argsort_1thread": sort_np})
     out.update(host_cpu())
     return out
@@ -302,13 +335,19 @@ def dry_run(args):
     views = [rank + world * j for j in range(max(1, args.inflight))]
     cam0 = view_of(views[0], H, W)
     elapsed = timed_region(lambda: None, args.steps, "cpu")
-    me = dict(rank=rank, world=dist.get_world_size() if world > 1 else 1, views=views,
+    c4_view = rank  # the C4 sub-record: view k on GPU k, one view per GPU
+    c4_elapsed = timed_region(lambda: None, args.steps, "cpu")
+    me = dict(rank=rank, world=dist.get_world_size() if world > 1 else 1, views=views, c4_view=c4_view,
               view0_row2=[float(x) for x in cam0.get_view_matrix()[2]],
+              c4_view_row2=[float(x) for x in view_of(c4_view, H, W).get_view_matrix()[2]],
               scene_sum=float(sum(float(t.double().sum()) for t in tensors)), elapsed=elapsed)
     ranks = gather_objects(me, world)
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "backend": "gloo" if world > 1 else None,
                           "workload": desc, "n_gaussians": n, "steps": args.steps, "broadcast": bcast,
+                          "views_batched": {"views_per_gpu": max(1, args.inflight), "elapsed_max_s": elapsed},
+                          "c4_one_view_per_gpu": None if world == 1 else
+                          {"views": [r["c4_view"] for r in ranks], "elapsed_max_s": c4_elapsed},
                           "ranks": ranks}), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -497,13 +536,36 @@ def main():
 
     # Per-stage times: a third region (view 0, one at a time) with libgsr's
     # HIP events recorded on the render stream between the stages.
+    import ctypes
     if not args.no_profile:
         _lib.check(lib.gsr_context_set_profiling(ctx.handle, 1), "set_profiling")
         prof_elapsed = timed_region(serial_frame, args.steps, dev)
 
+    # The compositing launch the timed region runs (k_composite_views, one per
+    # group): a fourth region, the same pipeline again with HIP events around
+    # every group's compositing launch on the group's stream.
+    group_comp = None
+    if not args.no_profile and share > 1:
+        leads = [gr[0][0] for gr in groups]
+        for c in leads:
+            _lib.check(lib.gsr_context_set_profiling(c.handle, 2), "set_profiling")
+        pipe.next = 0
+        gp_elapsed = timed_region(lambda: pipelined(calls), 1, dev)
+        tot_ms, tot_l, tot_v = 0.0, 0, 0
+        for c in leads:
+            cms, cl, cv = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+            _lib.check(lib.gsr_context_group_times(c.handle, ctypes.byref(cms), ctypes.byref(cl), ctypes.byref(cv)),
+                       "group_times")
+            tot_ms, tot_l, tot_v = tot_ms + cms.value, tot_l + cl.value, tot_v + cv.value
+            _lib.check(lib.gsr_context_set_profiling(c.handle, 0), "set_profiling")
+        vstats = [c.stats() for c in ctxs]
+        group_comp = dict(launches=tot_l, views=tot_v, ms_per_launch=tot_ms / max(tot_l, 1),
+                          views_per_launch=tot_v / max(tot_l, 1),
+                          mean_instances=float(np.mean([v["n_instances"] for v in vstats])),
+                          instrumented_ms_per_frame=1e3 * gp_elapsed / timed_frames)
+
     stats = ctx.stats()
     # tile-list length distribution of the last frame (load balance of the compositor)
-    import ctypes
     nt = stats["tiles_x"] * stats["tiles_y"]
     rb = torch.empty(2 * nt, dtype=torch.int32, device=dev)
     lib.gsr_debug_copy(ctx.handle, _lib.GSR_DEBUG_TILE_RANGES, ctypes.c_void_p(rb.data_ptr()), 8 * nt, None)
@@ -570,7 +632,30 @@ def main():
             roof["traffic"], roof["traffic_source"] = traffic
         if dom == "composite":
             roof["valu_issue"] = valu_issue(KERNEL_SYMBOL[dom], args, stage[dom])
-        roof["frame_valu_issue"] = frame_valu_issue(args, share, ms_per_step)
+        frame_valu = frame_valu_issue(args, share, ms_per_step)
+        if group_comp is not None and group_comp["launches"] > 0:
+            # the timed region's dominant kernel: k_composite_views<0>, one launch per
+            # group; its algorithmic bytes are the single-view formula per view
+            vpl = group_comp["views_per_launch"]
+            alg_view = group_comp["mean_instances"] * (48 + 4) + ntiles * 8 + W * H * 12
+            alg_launch = alg_view * vpl
+            ach = alg_launch / (group_comp["ms_per_launch"] * 1e-3) / 1e9
+            single = {k: roof.pop(k) for k in ("kernel", "achieved", "frac", "traffic", "alg_bytes_per_launch",
+                                               "ms_per_launch", "traffic_source", "valu_issue") if k in roof}
+            single["kernel"] = "k_composite<0> (one view at a time, gsr_render)"
+            gt = pmc_traffic("k_composite_views<0>", args)
+            roof.update({"kernel": "k_composite_views<0> (the timed region's compositing, one launch per group "
+                                   f"of {vpl:g} views)",
+                         "achieved": ach, "frac": ach / HBM_PEAK_GBS, "alg_bytes_per_launch": alg_launch,
+                         "ms_per_launch": group_comp["ms_per_launch"], "views_per_launch": vpl,
+                         "us_per_view": 1e3 * group_comp["ms_per_launch"] / vpl, "alg_bytes_per_view": alg_view,
+                         "traffic": gt[0] if gt else None, "traffic_per_view": gt[0] / vpl if gt else None,
+                         "traffic_source": gt[1] if gt else None,
+                         "timing": f"HIP events around every k_composite_views launch on its group's stream, "
+                                   f"{group_comp['launches']} launches over a repeat of the timed pipeline "
+                                   f"({group_comp['instrumented_ms_per_frame']:.4f} ms/frame instrumented)",
+                         "single_view": single})
+        roof["frame_valu_issue"] = frame_valu
 
     cpu = None
     if not args.no_cpu_baseline and world == 1 and g is not None:
@@ -609,6 +694,11 @@ def main():
         "stage_ms": stage,
         "roofline": roof,
         "cpu_baseline": cpu,
+        "c4_one_view_per_gpu": None if world == 1 else {
+            "definition": "SURVEY 8d C4: view k = default camera yawed k*45 deg on GPU k, one view per GPU, "
+                          "frames one at a time (gsr_render); barrier + synchronize around the region, max over ranks",
+            "value": n * args.steps * world / latency, "unit": "splats/s", "ms_per_frame": 1e3 * latency / args.steps,
+            "views": list(range(world))},
         "broadcast": bcast,
         "process_group": {"backend": dist.get_backend() if world > 1 else None,
                           "world_size": dist.get_world_size() if world > 1 else 1,

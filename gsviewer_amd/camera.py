@@ -185,3 +185,61 @@ def euler_to_quaternion(roll, pitch, yaw):
     qz = math.cos(r / 2) * math.cos(p / 2) * math.sin(y / 2) - math.sin(r / 2) * math.sin(p / 2) * math.cos(y / 2)
     qw = math.cos(r / 2) * math.cos(p / 2) * math.cos(y / 2) + math.sin(r / 2) * math.sin(p / 2) * math.sin(y / 2)
     return np.array([qx, qy, qz, qw], np.float32)
+
+
+def _quat_from_matrix(m):
+    """Unit quaternion (x, y, z, w) of a rotation matrix by the largest-pivot
+    method (Markley: the diagonal entry or the trace that is largest picks
+    the component computed from it), as scipy's Rotation.from_matrix does
+    (scipy 1.15, the reference's util.py:498 dependency)."""
+    m = np.asarray(m, np.float64)
+    dec = (m[0, 0], m[1, 1], m[2, 2], m[0, 0] + m[1, 1] + m[2, 2])
+    ch = int(np.argmax(dec))
+    q = [0.0, 0.0, 0.0, 0.0]
+    if ch != 3:
+        i = ch
+        j = (i + 1) % 3
+        k = (j + 1) % 3
+        q[i] = 1 - dec[3] + 2 * m[i, i]
+        q[j] = m[j, i] + m[i, j]
+        q[k] = m[k, i] + m[i, k]
+        q[3] = m[k, j] - m[j, k]
+    else:
+        q = [m[2, 1] - m[1, 2], m[0, 2] - m[2, 0], m[1, 0] - m[0, 1], 1 + dec[3]]
+    nrm = math.sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3])
+    return [c / nrm for c in q]
+
+
+def rotation_matrix_to_euler(R):
+    """util.convert_rotation_matrix_to_euler_angles (util.py:494-501): the
+    extrinsic 'xyz' Euler angles of R in degrees, the inverse of
+    euler_to_rotation_matrix (R = Rz Ry Rx).  scipy's as_euler algorithm
+    restated: the quaternion-based direct method of Bernardes & Viollet (2022)
+    (angles from two half-angle atan2s; the middle angle within 1e-7 of 0 or
+    pi is the gimbal-lock case, whose third angle is set to 0).  Bit-exact
+    against the reference-run fixtures (tests/golden)."""
+    q = _quat_from_matrix(R)
+    i, j, k = 0, 1, 2  # extrinsic x, y, z: Tait-Bryan, even permutation
+    sign = (i - j) * (j - k) * (k - i) // 2
+    a = q[3] - q[j]
+    b = q[i] + q[k] * sign
+    c = q[j] + q[3]
+    d = q[k] * sign - q[i]
+    ang = [0.0, 2 * math.atan2(math.hypot(c, d), math.hypot(a, b)), 0.0]
+    eps = 1e-7
+    case = 1 if abs(ang[1]) <= eps else (2 if abs(ang[1] - math.pi) <= eps else 0)
+    half_sum = math.atan2(b, a)
+    half_diff = math.atan2(d, c)
+    if case == 0:
+        ang[0] = half_sum - half_diff
+        ang[2] = half_sum + half_diff
+    else:  # gimbal lock: the third angle is not determined
+        ang[0] = 2 * half_sum if case == 1 else -2 * half_diff
+    ang[2] *= sign
+    ang[1] -= math.pi / 2
+    for t in range(3):
+        if ang[t] < -math.pi:
+            ang[t] += 2 * math.pi
+        elif ang[t] > math.pi:
+            ang[t] -= 2 * math.pi
+    return np.degrees(np.array(ang))

@@ -43,6 +43,7 @@ struct Arena {
     size_t bytes = 0;
     size_t used = 0;
     bool measure = false;
+    bool sealed = false;  // attached and sized: a buffer outgrowing its reservation fails instead of carving more
 };
 constexpr size_t kArenaAlign = 256;
 
@@ -66,6 +67,9 @@ struct DevBuf {
         if (n <= cap && p) return GSR_OK;
         size_t want = n < 64 ? 64 : n + n / 8;  // 12.5% headroom against regrowth
         T* q = nullptr;
+        if (arena && arena->sealed)
+            return set_error(GSR_ERR_NOMEM, std::string("context: ") + what +
+                                                " exceeds the bounds the caller's workspace was attached for");
         if (arena) {
             const size_t off = (arena->used + kArenaAlign - 1) & ~(kArenaAlign - 1);
             const size_t end = off + want * sizeof(T);
@@ -162,6 +166,7 @@ struct gsr_context {
     uint32_t seq = 0;                       // frame sequence number the host waits for
     uint32_t* host_counters_dev = nullptr;  // its device address
     gsr::DevBuf<unsigned long long> done_ctr;  // preprocess completion + instance count (self re-arming)
+    bool done_armed = false;                   // done_ctr zeroed on a frame's stream (arm_done_ctr)
     gsr_frame_stats stats{};
     // last frame's result arrays (for gsr_debug_copy)
     const uint32_t* last_depth_order = nullptr;
@@ -178,6 +183,16 @@ struct gsr_context {
     double host_ms[3] = {};  // host time in gsr_render: enqueue before the wait, the wait, enqueue after
     int64_t host_frames = 0;
     int64_t prof_frames = 0;
+    // group profiling (gsr_context_set_profiling(ctx, 2) on a group's first
+    // context): HIP events around each k_composite_views launch of the groups
+    // this context leads, two launches in flight
+    bool prof_group = false;
+    hipEvent_t evg[2][2] = {};
+    bool evg_pending[2] = {false, false};
+    int evg_views[2] = {0, 0};
+    int evg_slot = 0;
+    double group_comp_ms = 0.0;
+    int64_t group_launches = 0, group_views = 0;
     bool failed = false;           // a wait timed out or the stream faulted: no further frames
     int64_t wait_timeout_ms = 2000;
     gsr::Arena arena;              // caller workspace (gsr_context_attach_workspace) or sizing pass
@@ -293,12 +308,10 @@ struct ZeroLayout {
     }
 };
 
-// The completion counter is zeroed on the frame's own stream: a plain
-// hipMemset runs on the null stream, which does not order against the
-// non-blocking streams frames are issued on (torch's), so the first
-// preprocess could count on top of a memset still in flight and never
-// publish its (V, D, seq).
-int ensure_scene_buffers(gsr_context* c, size_t n, hipStream_t s) {
+// Sizes the per-Gaussian buffers.  Enqueues nothing: the load-time callers
+// (gsr_context_reserve, gsr_context_attach_workspace, the sort services) may
+// pass any stream, so no device work may come from here (see arm_done_ctr).
+int ensure_scene_buffers(gsr_context* c, size_t n) {
     const size_t nw = (n + 63) / 64 + 4;
     int rc;
     if ((rc = c->vis_mask.ensure(nw, "vis_mask"))) return rc;
@@ -317,14 +330,8 @@ int ensure_scene_buffers(gsr_context* c, size_t n, hipStream_t s) {
     if ((rc = c->rect4_b.ensure(n, "rect4"))) return rc;
     if ((rc = c->bin_tmp.ensure(bin_tmp_elems(n), "bin_tmp"))) return rc;
     if ((rc = c->radix_tmp.ensure(radix_tmp_elems(n), "radix_tmp"))) return rc;
-    if (c->has_arena && c->arena.measure) {  // gsr_workspace_size: sizes only, no HIP call
-        if (!c->done_ctr.p) return c->done_ctr.ensure(1, "done_ctr");
-        return GSR_OK;
-    }
-    if (!c->done_ctr.p) {
-        if ((rc = c->done_ctr.ensure(1, "done_ctr"))) return rc;
-        GSR_HIP_CHECK(hipMemsetAsync(c->done_ctr.p, 0, c->done_ctr.cap * sizeof(unsigned long long), s));
-    }
+    if ((rc = c->done_ctr.ensure(1, "done_ctr"))) return rc;
+    if (c->has_arena && c->arena.measure) return GSR_OK;  // gsr_workspace_size: sizes only, no HIP call
     if (!c->host_counters) {
         if (hipHostMalloc(&c->host_counters, 4 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess) {
@@ -334,6 +341,21 @@ int ensure_scene_buffers(gsr_context* c, size_t n, hipStream_t s) {
         std::memset(c->host_counters, 0, 4 * sizeof(uint32_t));
         GSR_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->host_counters_dev), c->host_counters, 0));
     }
+    return GSR_OK;
+}
+
+// The completion counter is zeroed once, on the stream of the context's first
+// frame, right before that frame's preprocess.  Zeroing it anywhere else (the
+// caller's stream of a reservation, the null stream of a plain hipMemset)
+// leaves the memset unordered against the non-blocking streams frames run on
+// (torch's), and a preprocess counting on top of a memset still in flight
+// never publishes its (V, D, seq).  Later frames need no zeroing: the last
+// preprocess block re-arms the counter, and the host waits for it before the
+// context's next frame begins.
+int arm_done_ctr(gsr_context* c, hipStream_t s) {
+    if (c->done_armed) return GSR_OK;
+    GSR_HIP_CHECK(hipMemsetAsync(c->done_ctr.p, 0, sizeof(unsigned long long), s));
+    c->done_armed = true;
     return GSR_OK;
 }
 
@@ -369,6 +391,17 @@ void prof_accumulate(gsr_context* c, int slot, bool wait) {
     c->acc_ms[GSR_STAGE_MERGE] += el(EV_COMPOSITE, EV_COUNT);
     c->prof_frames += 1;
     c->ev_pending[slot] = false;
+}
+
+void prof_group_accumulate(gsr_context* c, int slot) {
+    if (!c->evg_pending[slot]) return;
+    (void)hipEventSynchronize(c->evg[slot][1]);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, c->evg[slot][0], c->evg[slot][1]);
+    c->group_comp_ms += ms;
+    c->group_launches += 1;
+    c->group_views += c->evg_views[slot];
+    c->evg_pending[slot] = false;
 }
 
 // Stable sort of (key, val) pairs; totals = digit-total scratch.
@@ -645,6 +678,9 @@ int gsr_context_destroy(gsr_context* c) {
     for (auto& row : c->ev)
         for (auto& e : row)
             if (e) (void)hipEventDestroy(e);
+    for (auto& row : c->evg)
+        for (auto& e : row)
+            if (e) (void)hipEventDestroy(e);
     delete c;
     return GSR_OK;
 }
@@ -662,7 +698,7 @@ int gsr_context_reserve(gsr_context* c, int64_t n, int32_t width, int32_t height
         return set_error(GSR_ERR_INVALID, "context_reserve: n >= 0 and 1..32768 pixels per side");
     if (c->pend.active || c->pend.sort_ready)
         return set_error(GSR_ERR_INVALID, "context_reserve: a frame is in flight on this context");
-    hipStream_t s = (hipStream_t)stream;
+    (void)stream;  // sizing only: nothing is enqueued (the first frame zeroes its counter, arm_done_ctr)
     const size_t un = (size_t)n;
     const size_t d = max_instances > 0 ? (size_t)max_instances : 4 * un;
     const int num_tiles = ((width + kTile - 1) / kTile) * ((height + kTile - 1) / kTile);
@@ -670,7 +706,7 @@ int gsr_context_reserve(gsr_context* c, int64_t n, int32_t width, int32_t height
     // the shared radix scratch at its final size first: a smaller block sized by
     // ensure_scene_buffers would be retired (and, in a caller's workspace, wasted)
     if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(d), radix_tmp_elems(un)), "radix_tmp"))) return rc;
-    if ((rc = ensure_scene_buffers(c, un, s))) return rc;
+    if ((rc = ensure_scene_buffers(c, un))) return rc;
     if ((rc = c->zero.ensure(ZeroLayout(num_tiles).total, "zero block"))) return rc;
     if ((rc = c->tkeys_a.ensure(d, "tile_keys"))) return rc;
     if ((rc = c->tkeys_b.ensure(d, "tile_keys"))) return rc;
@@ -727,7 +763,9 @@ int gsr_context_attach_workspace(gsr_context* c, void* ws_dev, size_t ws_bytes, 
     c->arena.base = reinterpret_cast<char*>(a);
     c->arena.bytes = ws_bytes > skip ? ws_bytes - skip : 0;
     gsr::each_buf(c, [&](auto& b) { b.arena = &c->arena; });
-    return gsr_context_reserve(c, n, width, height, max_instances, stream);
+    const int rc = gsr_context_reserve(c, n, width, height, max_instances, stream);
+    if (rc == GSR_OK) c->arena.sealed = true;  // frames within the bounds reuse; beyond them: GSR_ERR_NOMEM
+    return rc;
 }
 
 int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const gsr_settings* st, float* out,
@@ -743,7 +781,8 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
     if (rc) return rc;
     const size_t n = (size_t)sc->d.n;
     const int num_tiles = u.tiles_x * u.tiles_y;
-    if ((rc = ensure_scene_buffers(c, n, s))) return rc;
+    if ((rc = ensure_scene_buffers(c, n))) return rc;
+    if ((rc = arm_done_ctr(c, s))) return rc;
     const ZeroLayout zl(num_tiles);
     if ((rc = c->zero.ensure(zl.total, "zero block"))) return rc;
     uint32_t* counters = c->zero.p + zl.counters;
@@ -824,7 +863,8 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
         const auto h0 = std::chrono::steady_clock::now();
         if ((rc = build_uniforms(sc, &cams[v], st, u[v]))) return rc;
         const int num_tiles = u[v].tiles_x * u[v].tiles_y;
-        if ((rc = ensure_scene_buffers(c, n, s))) return rc;
+        if ((rc = ensure_scene_buffers(c, n))) return rc;
+        if ((rc = arm_done_ctr(c, s))) return rc;
         const ZeroLayout zl(num_tiles);
         if ((rc = c->zero.ensure(zl.total, "zero block"))) return rc;
         uint32_t* counters = c->zero.p + zl.counters;
@@ -1069,6 +1109,10 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
     size_t max_chunks = 0;
     int rc;
     const auto h1 = std::chrono::steady_clock::now();
+    // From here on the group's frames are consumed whatever happens: a failure
+    // (a wait that timed out, a bound of a caller's workspace exceeded) ends
+    // every view's frame, so each context can begin a new one.
+    for (int v = 0; v < k; ++v) ctxs[v]->pend.active = false;
     // the frames' counts (published together by the shared preprocess, or one by one)
     for (int v = 0; v < k; ++v)
         if (ctxs[v]->pend.n > 0 && (rc = wait_counts(ctxs[v], s))) return rc;
@@ -1076,7 +1120,6 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
     for (int v = 0; v < k; ++v) {
         gsr_context* c = ctxs[v];
         PendingFrame& f = c->pend;
-        f.active = false;
         const uint32_t n_vis = f.n > 0 ? __atomic_load_n(&c->host_counters[0], __ATOMIC_ACQUIRE) : 0u;
         const uint32_t n_dup = f.n > 0 ? __atomic_load_n(&c->host_counters[1], __ATOMIC_ACQUIRE) : 0u;
         n_vis_max = std::max(n_vis_max, n_vis);
@@ -1134,9 +1177,20 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
                 return rc;
     } else {
         if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk_views, c0->len_classes, c0->first_major, s))) return rc;
+        const int gslot = c0->evg_slot;
+        if (c0->prof_group) {
+            prof_group_accumulate(c0, gslot);  // slot reuse: that launch is two groups back
+            GSR_HIP_CHECK(hipEventRecord(c0->evg[gslot][0], s));
+        }
         if ((rc = launch_composite_views(fv, k, (uint32_t)max_chunks, c0->len_classes, c0->first_major, c0->views_interleave, u0,
                                          frag_class_of(u0.render_mod), f0.t_min, f0.bg, f0.out_layout, s)))
             return rc;
+        if (c0->prof_group) {
+            GSR_HIP_CHECK(hipEventRecord(c0->evg[gslot][1], s));
+            c0->evg_pending[gslot] = true;
+            c0->evg_views[gslot] = k;
+            c0->evg_slot = gslot ^ 1;
+        }
         if ((rc = launch_merge_views(fv, k, u0, f0.t_min, f0.bg, f0.out_layout, s))) return rc;
     }
     const auto h3 = std::chrono::steady_clock::now();
@@ -1165,6 +1219,19 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
 
 int gsr_context_set_profiling(gsr_context* c, int32_t enable) {
     if (!c) return set_error(GSR_ERR_INVALID, "null argument");
+    if (enable < 0 || enable > 2) return set_error(GSR_ERR_INVALID, "set_profiling: enable must be 0, 1 or 2");
+    if (enable == 2) {  // group compositing launches (gsr_render_finish_views led by this context)
+        if (!c->evg[0][0])
+            for (auto& row : c->evg)
+                for (auto& e : row) GSR_HIP_CHECK(hipEventCreate(&e));
+        for (int k = 0; k < 2; ++k) prof_group_accumulate(c, k);
+        c->prof_group = true;
+        c->prof_on = false;
+        c->group_comp_ms = 0.0;
+        c->group_launches = c->group_views = 0;
+        return GSR_OK;
+    }
+    c->prof_group = false;
     if (enable && !c->ev[0][0]) {
         for (int a = 0; a < 2; ++a)
             for (int b = 0; b <= EV_COUNT; ++b) GSR_HIP_CHECK(hipEventCreate(&c->ev[a][b]));
@@ -1181,6 +1248,15 @@ int gsr_context_stage_times(gsr_context* c, double* ms_out, int64_t* frames_out)
     for (int k = 0; k < 2; ++k) prof_accumulate(c, (int)((c->frame_idx + k) & 1), true);
     for (int k = 0; k < GSR_NUM_STAGES; ++k) ms_out[k] = c->acc_ms[k];
     if (frames_out) *frames_out = c->prof_frames;
+    return GSR_OK;
+}
+
+int gsr_context_group_times(gsr_context* c, double* composite_ms, int64_t* launches, int64_t* views) {
+    if (!c || !composite_ms || !launches || !views) return set_error(GSR_ERR_INVALID, "null argument");
+    for (int k = 0; k < 2; ++k) prof_group_accumulate(c, (c->evg_slot + k) & 1);
+    *composite_ms = c->group_comp_ms;
+    *launches = c->group_launches;
+    *views = c->group_views;
     return GSR_OK;
 }
 
@@ -1222,7 +1298,7 @@ int gsr_debug_sort_pairs(gsr_context* c, const uint32_t* keys_dev, int64_t n, in
     hipStream_t s = (hipStream_t)stream;
     if (n == 0) return GSR_OK;
     const size_t un = (size_t)n;
-    int rc = ensure_scene_buffers(c, un, s);
+    int rc = ensure_scene_buffers(c, un);
     if (rc) return rc;
     if ((rc = c->zero.ensure(ZeroLayout(0).total, "zero block"))) return rc;
     GSR_HIP_CHECK(hipMemcpyAsync(c->keys_a.p, keys_dev, un * 4, hipMemcpyDeviceToDevice, s));
@@ -1240,7 +1316,7 @@ int gsr_sort_depth(gsr_context* c, const gsr_scene* sc, const float view[16], in
     hipStream_t s = (hipStream_t)stream;
     const size_t n = (size_t)sc->d.n;
     if (n == 0) return GSR_OK;
-    int rc = ensure_scene_buffers(c, n, s);
+    int rc = ensure_scene_buffers(c, n);
     if (rc) return rc;
     if ((rc = c->zero.ensure(ZeroLayout(0).total, "zero block"))) return rc;
     GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * ZeroLayout(0).total, s));

@@ -15,6 +15,7 @@
 // saturated (transmittance < t_min).  Slices a splat's row span misses are
 // skipped with a scalar branch.
 #include <algorithm>
+#include <cstdlib>
 
 #include "gsr_internal.h"
 
@@ -35,6 +36,17 @@ constexpr int kBinBlock = kThreads * kBinItems;  // 1024
 #define GSR_BIN_STAGE 2048
 #endif
 constexpr int kBinStage = GSR_BIN_STAGE;
+
+// Blocks of at most this many instances take the staged write (default and
+// upper bound kBinStage; GSR_BIN_STAGE_LIMIT lowers it, read per launch, so a
+// test can make one frame mix staged and direct blocks).
+uint32_t bin_stage_limit() {
+    if (const char* e = std::getenv("GSR_BIN_STAGE_LIMIT")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 0 && v < kBinStage) return (uint32_t)v;
+    }
+    return (uint32_t)kBinStage;
+}
 
 __device__ __forceinline__ uint32_t rect_tiles(uint2 tr) {
     const uint32_t tx0 = tr.x & 0xffffu, tx1 = tr.x >> 16, ty0 = tr.y & 0xffffu, ty1 = tr.y >> 16;
@@ -99,7 +111,7 @@ __device__ __forceinline__ void bin_write(const uint32_t* __restrict__ sorted_id
                                           const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
                                           const uint32_t* __restrict__ block_sums, int tiles_x,
                                           uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ tile_vals,
-                                          uint32_t blk, uint32_t* lds, uint32_t* stage) {
+                                          uint32_t blk, uint32_t* lds, uint32_t* stage, uint32_t stage_limit) {
     uint32_t pre = 0;  // this thread's share of the earlier blocks' totals
     for (uint32_t b = threadIdx.x; b < blk; b += kThreads) pre += block_sums[b];
     const uint32_t base = blk * kBinBlock + threadIdx.x * kBinItems;  // 4 consecutive per thread
@@ -133,7 +145,7 @@ __device__ __forceinline__ void bin_write(const uint32_t* __restrict__ sorted_id
         block_total += lds[k];
         block_base += lds[kThreads / 64 + k];
     }
-    if (block_total <= (uint32_t)kBinStage) {
+    if (block_total <= stage_limit) {  // (stage_limit <= kBinStage)
         // staged: instances into LDS, then the block's run written coalesced
         // (direct per-thread writes scatter 2 words per instance across lanes)
 #pragma unroll
@@ -174,11 +186,11 @@ __global__ __launch_bounds__(kThreads) void k_bin_write(const uint32_t* __restri
                                                         const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
                                                         const uint32_t* __restrict__ block_sums, int tiles_x,
                                                         uint32_t* __restrict__ tile_keys,
-                                                        uint32_t* __restrict__ tile_vals) {
+                                                        uint32_t* __restrict__ tile_vals, uint32_t stage_limit) {
     __shared__ uint32_t lds[2 * kThreads / 64];
     __shared__ uint32_t stage[2 * kBinStage];
     bin_write<kPacked>(sorted_ids, trect_sorted, rect4_sorted, n_vis, block_sums, tiles_x, tile_keys, tile_vals,
-                       blockIdx.x, lds, stage);
+                       blockIdx.x, lds, stage, stage_limit);
 }
 
 // Views of a group (blockIdx.y = view); the grid covers the largest view.
@@ -206,13 +218,13 @@ __global__ __launch_bounds__(kThreads) void k_bin_reduce_views(BinViews vs) {
 }
 
 template <bool kPacked>
-__global__ __launch_bounds__(kThreads) void k_bin_write_views(BinViews vs, int tiles_x) {
+__global__ __launch_bounds__(kThreads) void k_bin_write_views(BinViews vs, int tiles_x, uint32_t stage_limit) {
     __shared__ uint32_t lds[2 * kThreads / 64];
     __shared__ uint32_t stage[2 * kBinStage];
     const BinView& v = vs.v[blockIdx.y];
     if (blockIdx.x * kBinBlock >= v.n_vis) return;
     bin_write<kPacked>(v.sorted_ids, v.trect_sorted, v.rect4_sorted, v.n_vis, v.block_sums, tiles_x, v.tile_keys,
-                       v.tile_vals, blockIdx.x, lds, stage);
+                       v.tile_vals, blockIdx.x, lds, stage, stage_limit);
 }
 
 // Tile ranges from the tile-sorted keys: kRangeItems consecutive instances per
@@ -1318,10 +1330,10 @@ int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_
     GSR_LAUNCH_CHECK("bin_reduce");
     if (rect4_sorted)
         k_bin_write<true><<<nb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tmp, tiles_x,
-                                                  tile_keys, tile_vals);
+                                                  tile_keys, tile_vals, bin_stage_limit());
     else
         k_bin_write<false><<<nb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tmp, tiles_x,
-                                                   tile_keys, tile_vals);
+                                                   tile_keys, tile_vals, bin_stage_limit());
     GSR_LAUNCH_CHECK("bin_write");
     return GSR_OK;
 }
@@ -1453,9 +1465,9 @@ int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s) {
         k_bin_reduce_views<false><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv);
     GSR_LAUNCH_CHECK("bin_reduce_views");
     if (packed)
-        k_bin_write_views<true><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x);
+        k_bin_write_views<true><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x, bin_stage_limit());
     else
-        k_bin_write_views<false><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x);
+        k_bin_write_views<false><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x, bin_stage_limit());
     GSR_LAUNCH_CHECK("bin_write_views");
     return GSR_OK;
 }

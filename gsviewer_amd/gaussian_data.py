@@ -80,6 +80,29 @@ class GaussianData:
                             [xmin, ymin, zmax], [xmax, ymin, zmax], [xmin, ymax, zmax], [xmax, ymax, zmax]])
         return self.points_min, self.points_max, corners
 
+    @property
+    def compute_obb(self):
+        """util_gau.py:114-138: the oriented box of the positions by PCA.
+        Returns (obb_min, obb_max, U, corners): the box's extreme corners in
+        world coordinates, the principal axes (columns of U from the SVD of the
+        covariance) and the 8 corners in the reference's order.  Same float
+        path as the reference: the float32 column means, float32 centring,
+        np.cov in float64 (what DataFrame.cov runs on NaN-free data), the SVD,
+        projections in float64.  Bit-exact against reference-run fixtures."""
+        xyz = np.asarray(self.xyz)
+        center = xyz.mean(axis=0)
+        centered = xyz - center
+        cov = np.cov(np.asarray(centered, np.float64).T)
+        U, _, _ = np.linalg.svd(cov)
+        proj = centered @ U
+        obb_min = center + proj.min(axis=0) @ U.T
+        obb_max = center + proj.max(axis=0) @ U.T
+        lo, hi = obb_min, obb_max
+        corners = np.array([[lo[0], lo[1], lo[2]], [hi[0], lo[1], lo[2]], [lo[0], hi[1], lo[2]],
+                            [hi[0], hi[1], lo[2]], [lo[0], lo[1], hi[2]], [hi[0], lo[1], hi[2]],
+                            [lo[0], hi[1], hi[2]], [hi[0], hi[1], hi[2]]])
+        return obb_min, obb_max, U, corners
+
     def astype32(self) -> "GaussianData":
         return GaussianData(*(np.ascontiguousarray(np.asarray(a, np.float32))
                               for a in (self.xyz, self.rot, self.scale, self.opacity, self.sh)), path=self.path,

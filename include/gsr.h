@@ -137,7 +137,11 @@ int gsr_context_destroy(gsr_context* ctx);
  * frame (<= 0: 4 n), so that frames within those bounds allocate nothing.
  * The reference sizes its GL buffers once per scene in update_gaussian_data
  * (renderer_ogl.py:235-242) and CUDARenderer keeps its tensors resident
- * (renderer_cuda.py:147-150). */
+ * (renderer_cuda.py:147-150).
+ * Host-side sizing only: nothing is enqueued on `stream` (kept for the ABI),
+ * so frames may begin on any stream right after it returns with no
+ * synchronisation.  The context's first frame zeroes its completion counter
+ * on that frame's own stream. */
 int gsr_context_reserve(gsr_context* ctx, int64_t n, int32_t width, int32_t height, int64_t max_instances,
                         void* stream);
 /* Device bytes the context holds now (retired blocks excluded), or < 0 on
@@ -156,7 +160,10 @@ int64_t gsr_context_workspace(gsr_context* ctx, int64_t* n_allocations);
  * its buffers instead of allocating, sized for the same bounds; GSR_ERR_NOMEM
  * if ws_bytes < gsr_workspace_size(...).  Frames within the bounds then never
  * allocate device memory; a frame beyond them fails with GSR_ERR_NOMEM instead
- * of growing.  Only a context that holds no buffers yet can attach one. */
+ * of growing (spare bytes past gsr_workspace_size are never carved later, so
+ * gsr_context_workspace stays constant).  Only a context that holds no buffers
+ * yet can attach one.  Like gsr_context_reserve it enqueues nothing on
+ * `stream`: the first frame may begin on any stream without a sync. */
 int64_t gsr_workspace_size(int64_t n, int32_t width, int32_t height, int64_t max_instances);
 int gsr_context_attach_workspace(gsr_context* ctx, void* ws_dev, size_t ws_bytes, int64_t n, int32_t width,
                                  int32_t height, int64_t max_instances, void* stream);
@@ -219,7 +226,10 @@ int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream);
  * views interleaved class by class (GSR_VIEWS_INTERLEAVE=0: view after view); a group dispatches
  * every tile's first chunk before any later chunk (GSR_FIRST_MAJOR=0: full chunks first), so a
  * deep tile saturated by its first chunk skips the rest.
- * Results are identical to k gsr_render_finish calls (and independent of the dispatch order). */
+ * Results are identical to k gsr_render_finish calls (and independent of the dispatch order).
+ * Once the arguments are validated every view's frame is consumed: an error
+ * after that point (a wait timeout, GSR_ERR_NOMEM beyond a caller workspace's
+ * bounds) ends all k frames, and each context can begin its next one. */
 int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream);
 
 int gsr_context_stats(const gsr_context* ctx, gsr_frame_stats* out);
@@ -245,10 +255,18 @@ int gsr_debug_sort_pairs(gsr_context* ctx, const uint32_t* keys_dev, int64_t n, 
 enum { GSR_STAGE_CULL = 0, GSR_STAGE_PREPROCESS = 1, GSR_STAGE_DEPTH_SORT = 2, GSR_STAGE_BINNING = 3,
        GSR_STAGE_TILE_SORT = 4, GSR_STAGE_RANGES = 5, GSR_STAGE_COMPOSITE = 6, GSR_STAGE_SYNC = 7,
        GSR_STAGE_MERGE = 8, GSR_NUM_STAGES = 9 };
-int gsr_context_set_profiling(gsr_context* ctx, int32_t enable);   /* resets the accumulators */
+/* enable: 0 off, 1 per-stage events of this context's single-view frames,
+ * 2 events around the compositing launch of every group this context leads
+ * (ctxs[0] of gsr_render_finish_views; gsr_context_group_times).  Resets the
+ * accumulators. */
+int gsr_context_set_profiling(gsr_context* ctx, int32_t enable);
 /* Sum of per-stage milliseconds over the profiled frames since the last reset
  * (waits for the last profiled frame's events). */
 int gsr_context_stage_times(gsr_context* ctx, double* ms_out /* [GSR_NUM_STAGES] */, int64_t* frames_out);
+/* Profiling mode 2: summed milliseconds of the group compositing launches
+ * (k_composite_views, HIP events on the group's stream), the number of
+ * launches and the views they composited (waits for the last launch). */
+int gsr_context_group_times(gsr_context* ctx, double* composite_ms, int64_t* launches, int64_t* views);
 
 /* Host time spent inside gsr_render on this context since creation, in ms:
  * [0] enqueue before the wait for the frame's counts, [1] that wait,

@@ -18,6 +18,13 @@ Functions pinned (reference file:line):
   util_gau.GaussianData.sh_dim / points_center / compute_aabb  :76-111
   renderer_ogl._sort_gaussian_cpu    renderer_ogl.py:16-26
   util.convert_euler_angles_to_rotation_matrix  util.py:453-479
+  util.convert_rotation_matrix_to_euler_angles  util.py:494-501
+  util_gau.GaussianData.compute_obb  util_gau.py:114-138
+  util_gau.export_ply's mask and bbox  util_gau.py:388-413 (the downstream
+      gsconverter call is replaced by a function that records its convertargs;
+      the reference's computation is untouched)
+  gsconverter BaseConverter.crop_by_bbox  tools/gsconverter/utils/base_converter.py:175-191
+      (run on a structured array of the original positions plus a row index)
 """
 import os
 import sys
@@ -115,6 +122,75 @@ def main():
     angles = np.array([[0, 0, 0], [30, 15, 0], [-45, 10, 170], [90, -90, 33.3]], np.float64)
     out["euler_angles"] = angles
     out["euler_R"] = np.stack([util.convert_euler_angles_to_rotation_matrix(a) for a in angles])
+
+    # matrix -> Euler angles (scipy Rotation.as_euler('xyz', degrees=True)), util.py:494-501
+    mats = list(out["euler_R"])
+    rr = np.random.default_rng(77)
+    for _ in range(12):
+        q = rr.normal(size=4)
+        q /= np.linalg.norm(q)
+        w, x, y, z = q
+        mats.append(np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                              [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                              [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]]))
+    out["r2e_R"] = np.stack(mats)
+    out["r2e_euler"] = np.stack([util.convert_rotation_matrix_to_euler_angles(R) for R in mats])
+
+    # compute_obb (pandas mean / cov, SVD), util_gau.py:114-138, on three point sets
+    obb_sets = [xyz, xyz2, (rng.normal(0, 1, (5000, 3)) @ np.array([[3.0, 0.4, 0.1], [0.0, 1.0, -0.5],
+                                                                       [0.2, 0.0, 0.3]])).astype(np.float32)]
+    for k, pts in enumerate(obb_sets):
+        go = util_gau.GaussianData(pts.copy(), rot[: len(pts)].copy() if len(pts) == n else
+                                   np.tile([1, 0, 0, 0], (len(pts), 1)).astype(np.float32),
+                                   np.ones((len(pts), 3), np.float32), np.ones((len(pts), 1), np.float32),
+                                   np.zeros((len(pts), 3), np.float32))
+        omin, omax, U, corners = go.compute_obb
+        out[f"obb{k}_xyz"], out[f"obb{k}_min"], out[f"obb{k}_max"] = pts, omin, omax
+        out[f"obb{k}_U"], out[f"obb{k}_corners"] = U, corners
+
+    # export_ply (util_gau.py:388-431): the mask and bbox, with the box acting on
+    # the current (rescaled) positions and the bbox taken over the original ones
+    captured = {}
+
+    def capture(convertargs):
+        captured["args"] = dict(convertargs)
+        return True
+
+    util_gau.gsconverter = capture
+    from tools.gsconverter.utils.base_converter import BaseConverter  # noqa: E402
+    ne = 20_000
+    er = np.random.default_rng(3)
+    orig = er.normal(0, 2.0, (ne, 3)).astype(np.float32)
+    cur = (orig * np.float32(0.5) + np.float32(0.05)).astype(np.float32)
+    out["export_orig"], out["export_cur"] = orig, cur
+    cases = [(0, 0, [-1, -1, -1], [1, 1, 1], [0, 0, 0]),
+             (1, 0, [-0.8, -0.5, -0.6], [0.7, 0.9, 0.4], [0, 0, 0]),
+             (0, 1, [-0.9, -0.4, -0.7], [0.6, 0.8, 0.5], [30.0, 15.0, 0.0]),
+             (1, 1, [-0.9, -0.4, -0.7], [0.6, 0.8, 0.5], [10.0, -20.0, 45.0]),
+             (1, 0, [50, 50, 50], [60, 60, 60], [0, 0, 0]),
+             (0, 1, [-0.3, -2.0, -0.2], [0.25, 2.0, 0.3], [0.0, 0.0, 90.0])]
+    rec = np.zeros(ne, dtype=[("x", "f4"), ("y", "f4"), ("z", "f4"), ("row", "i8")])
+    rec["x"], rec["y"], rec["z"], rec["row"] = orig[:, 0], orig[:, 1], orig[:, 2], np.arange(ne)
+    ex_params, ex_bbox, ex_rows = [], [], []
+    for aabb, obb, cmin, cmax, erot in cases:
+        ge = util_gau.GaussianData(orig.copy(), np.tile([1, 0, 0, 0], (ne, 1)).astype(np.float32),
+                                   np.ones((ne, 3), np.float32), np.ones((ne, 1), np.float32),
+                                   np.zeros((ne, 3), np.float32))
+        ge.xyz = cur.copy()  # the viewer's current positions (scale_data); the original state stays
+        captured.clear()
+        assert util_gau.export_ply(ge, "unused", aabb, obb, cmin, cmax, erot)
+        bbox = captured["args"]["bbox"]
+        if bbox is None:
+            ex_bbox.append(np.full(6, np.nan))
+            ex_rows.append(np.arange(ne))  # gsconverter skips the crop without a bbox
+        else:
+            ex_bbox.append(np.array(bbox, np.float64))
+            ex_rows.append(BaseConverter(rec.copy()).crop_by_bbox(*bbox)["row"])
+        ex_params.append(np.array([aabb, obb, *cmin, *cmax, *erot], np.float64))
+    out["export_params"] = np.stack(ex_params)
+    out["export_bbox"] = np.stack(ex_bbox)
+    out["export_nrows"] = np.array([len(r) for r in ex_rows])
+    out["export_rows"] = np.concatenate(ex_rows)
 
     np.savez_compressed(OUT, **out)
     print("wrote", OUT, {k: v.shape for k, v in out.items()})

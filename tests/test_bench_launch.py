@@ -60,3 +60,20 @@ def test_world_size_must_match_gpus():
              env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_eight_rank_line_carries_c4_and_batched_views():
+    """The driver's 8-GPU command: rank 0's line carries the batched-views
+    record beside the C4 sub-record (view k on GPU k, one view
+    per GPU), and every rank's view assignment."""
+    r = _run("--gpus", "8", "--dry-run", "--steps", "1", timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 8 and len(d["ranks"]) == 8
+    assert d["views_batched"]["views_per_gpu"] == 20
+    assert all(x["views"] == [x["rank"] + 8 * j for j in range(20)] for x in d["ranks"])
+    c4 = d["c4_one_view_per_gpu"]
+    assert c4["views"] == list(range(8))
+    assert [x["c4_view"] for x in d["ranks"]] == list(range(8))
+    # eight distinct cameras: the default one yawed by k * 45 deg
+    assert len({tuple(x["c4_view_row2"]) for x in d["ranks"]}) == 8

@@ -358,8 +358,7 @@ def test_caller_provided_workspace(gpu):
     ws.fill_(0xAB)  # the context must not rely on zeroed memory
     torch.cuda.synchronize()
     ctx = HipContext()
-    ctx.attach_workspace(ws, n, w, h, max_instances=d)
-    torch.cuda.synchronize()  # the attach zeroes the completion counter on the null stream
+    ctx.attach_workspace(ws, n, w, h, max_instances=d)  # enqueues nothing: no sync before the side stream
     b0, a0 = ctx.workspace()
     assert b0 == held
     st = RenderSettings(out_layout=0)
@@ -380,9 +379,18 @@ def test_caller_provided_workspace(gpu):
     assert int((ws != 0xAB).sum()) > 50_000
     big = HipScene.from_gaussian_data(random_scene(120_000, sh_degree=1, seed=12))
     out = torch.empty((3, h, w), dtype=torch.float32, device="cuda")
-    with pytest.raises(RuntimeError, match="too small"):
+    with pytest.raises(RuntimeError, match="exceeds the bounds"):
         render_into(ctx, big, camera_from(Camera(h, w)), st, out)
     torch.cuda.synchronize()
+    # nothing was carved past the reservation, and a frame within the bounds still renders
+    assert ctx.workspace() == (b0, a0)
+    cam = camera_from(Camera(h, w).yaw(40.0))
+    render_into(ctx, scene, cam, st, out, stream=s)
+    ref = torch.empty_like(out)
+    render_into(ref_ctx, scene, cam, st, ref)
+    s.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
     ctx.close()
     small = HipContext()
     with pytest.raises(RuntimeError, match="too small"):
@@ -431,4 +439,103 @@ def test_wait_for_counts_has_a_deadline(gpu, monkeypatch):
     render_into(ctx2, scene, camera_from(cam), st, out)
     torch.cuda.synchronize()
     ctx2.close()
+    scene.close()
+
+
+@pytest.mark.parametrize("how", ["reserve", "attach"])
+def test_first_frame_on_side_stream_after_sizing(gpu, how):
+    """gsr_context_reserve / gsr_context_attach_workspace on torch's default
+    stream, then the context's first frame at once on a fresh non-blocking
+    stream with no synchronisation (bench.py's order): the sizing calls
+    enqueue nothing, and the first frame zeroes its completion counter on its
+    own stream, so the frame publishes its counts and matches the oracle."""
+    import numpy as np
+    from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into, workspace_size
+    from oracle import gl_oracle as O
+    n, w, h = 3000, 160, 120
+    g = random_scene(n, sh_degree=1, seed=21)
+    scene = HipScene.from_gaussian_data(g)
+    torch.cuda.synchronize()
+    ws = None
+    for yaw in (0.0, 30.0):
+        ctx = HipContext()
+        if how == "reserve":
+            ctx.reserve(n, w, h)
+        else:
+            ws = torch.empty(workspace_size(n, w, h), dtype=torch.uint8, device="cuda")
+            ws.fill_(0xFF)  # a stale all-ones counter would never publish (V, D, seq)
+            ctx.attach_workspace(ws, n, w, h)
+        s = torch.cuda.Stream()
+        cam = Camera(h, w).yaw(yaw)
+        out = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
+        st = RenderSettings(out_layout=1, t_min=0.0)
+        with torch.cuda.stream(s):
+            render_into(ctx, scene, camera_from(cam), st, out, stream=s)
+            render_into(ctx, scene, camera_from(cam), st, out, stream=s)  # the re-armed counter
+        s.synchronize()
+        img = out.cpu().numpy()
+        U = O.default_uniforms(cam.get_view_matrix(), cam.get_project_matrix(),
+                               np.asarray(cam.get_htanfovxy_focal(), np.float32), cam.position, w, h)
+        ref = O.composite(O.vertex_stage(g.flat(), g.sh_dim, U), U)
+        d = np.abs(img - ref)
+        assert (d <= 2e-5).mean() >= 0.999 and d.max() <= 2e-3, (d.max(), (d > 2e-5).sum())
+        ctx.close()
+    scene.close()
+
+
+def test_finish_views_nomem_ends_every_view(gpu):
+    """A group finish that fails with GSR_ERR_NOMEM (a view's instances beyond
+    its caller workspace) ends every view's frame: each context then begins
+    and finishes a frame within its bounds (later contexts of the
+    group used to stay 'active' and refuse their next frame)."""
+    from gsviewer_amd.rasterizer import (HipContext, HipScene, RenderSettings, camera_from, render_begin_sorts,
+                                         render_begin_views, render_finish_views, render_into, workspace_size)
+    n, w, h = 20_000, 320, 240
+    g = random_scene(n, sh_degree=0, seed=5)
+    scene = HipScene.from_gaussian_data(g)
+    st = RenderSettings(out_layout=0)
+    cams = [camera_from(Camera(h, w).yaw(30.0 * v)) for v in range(3)]
+    outs = [torch.empty((3, h, w), dtype=torch.float32, device="cuda") for _ in range(3)]
+    probe = HipContext()
+    render_into(probe, scene, cams[0], st, outs[0])
+    torch.cuda.synchronize()
+    d0 = probe.stats()["n_instances"]
+    probe.close()
+    assert d0 > 1000
+    wss, ctxs = [], []
+    for v in range(3):
+        d = d0 // 4 if v == 0 else 8 * d0  # view 0's workspace holds a quarter of a frame's instances
+        wss.append(torch.empty(workspace_size(n, w, h, d), dtype=torch.uint8, device="cuda"))
+        c = HipContext()
+        c.attach_workspace(wss[-1], n, w, h, max_instances=d)
+        ctxs.append(c)
+    s = torch.cuda.Stream()
+    render_begin_views(ctxs, scene, cams, st, outs, stream=s)
+    render_begin_sorts(ctxs, stream=s)
+    with pytest.raises(RuntimeError, match="exceeds the bounds|too small"):
+        render_finish_views(ctxs, stream=s)
+    s.synchronize()
+    # every context takes a new frame; views 1 and 2 render correctly
+    for v in (1, 2):
+        ref_ctx = HipContext()
+        ref = torch.empty_like(outs[v])
+        render_into(ref_ctx, scene, cams[v], st, ref)
+        render_into(ctxs[v], scene, cams[v], st, outs[v], stream=s)
+        s.synchronize()
+        torch.cuda.synchronize()
+        assert torch.equal(outs[v], ref)
+        ref_ctx.close()
+    # view 0 within its bounds: a scene of 500 Gaussians
+    few = HipScene.from_gaussian_data(random_scene(500, sh_degree=0, seed=6))
+    ref_ctx = HipContext()
+    ref = torch.empty_like(outs[0])
+    render_into(ref_ctx, few, cams[0], st, ref)
+    render_into(ctxs[0], few, cams[0], st, outs[0], stream=s)
+    s.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], ref)
+    ref_ctx.close()
+    few.close()
+    for c in ctxs:
+        c.close()
     scene.close()

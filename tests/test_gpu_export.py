@@ -61,6 +61,22 @@ def test_export_select_matches_oracle(gpu, case):
         assert 0 < len(want_rows) < len(cur)
 
 
+def test_export_select_matches_reference_run(gpu, golden):
+    """gsr_box_select against the reference itself: export_ply's bbox and
+    gsconverter's crop rows recorded by tests/golden/make_golden.py (the
+    reference's export_ply run with its gsconverter call captured, and
+    BaseConverter.crop_by_bbox on the original positions)."""
+    from gsviewer_amd.ply import export_select
+    from test_oracle_golden import export_cases
+    cur, orig = golden["export_cur"], golden["export_orig"]
+    cases = export_cases(golden)
+    assert len(cases) == 6
+    for aabb, obb, cmin, cmax, rot, bbox, rows in cases:
+        got_rows, got_bbox, _ = export_select(_t(cur), _t(orig), aabb, obb, cmin, cmax, rot)
+        assert got_bbox == bbox
+        np.testing.assert_array_equal(got_rows.cpu().numpy(), rows)
+
+
 def test_export_ply_end_to_end(gpu, tmp_path):
     from gsviewer_amd.ply import export_ply, load_ply
     from test_ply import vertex_array

@@ -11,8 +11,10 @@ the batched finish: binning, tile lists, compositing, merge) with planar
 * C5: 1M, SH 3, 3840x2160, no box / AABB / OBB (SURVEY.md 8d C5 settings).
 
 Per view: the image against the oracle with the stated tolerances (helpers.py)
-plus an absolute census of the channels above 2e-5 (+ t_min), bounded at
-1e-3 of all channels; for view 0 of every config: the global depth order and
+plus an absolute census of the channels above 2e-5 (+ t_min), bounded at what
+round 2's census measured with margin (max |d| 9.1e-4 and at most 4 channels
+over per frame, profiles/r2_s58/parity_census.jsonl): per frame max |d| <=
+FULL_MAX and at most FULL_N_OVER channels over; for view 0 of every config: the global depth order and
 every tile's instance list exactly equal to the oracle's (GL draw order
 restricted to the tile).  The census of every case is appended to
 gpurun_out/parity_census.jsonl for DESIGN.md."""
@@ -26,7 +28,7 @@ from gsviewer_amd.camera import Camera, euler_to_rotation_matrix
 from gsviewer_amd.gaussian_data import garden_standin
 from oracle import c_oracle as C
 from oracle import gl_oracle as O
-from helpers import TOL_EXACT, TOL_MAX, TOL_TMIN, batched_frames, compare_images, error_census, uniforms_for
+from helpers import TOL_EXACT, TOL_TMIN, batched_frames, compare_images, error_census, uniforms_for
 from test_gpu_scale import check_frame_order
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
@@ -34,7 +36,8 @@ pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CENSUS = os.path.join(ROOT, "gpurun_out", "parity_census.jsonl")
 THREADS = 16
-CENSUS_MAX_FRAC = 1e-3   # channels above the exact tolerance, absolute bound per frame
+FULL_MAX = 2e-3          # max |GPU - oracle| per frame at full size
+FULL_N_OVER = 16         # channels above the exact tolerance per frame (of 6.2M at 1080p, 24.9M at 4K)
 
 
 def _settings(**kw):
@@ -86,8 +89,8 @@ def _run(case, n, seed, W, H, t_min, box="none", order_check=True):
         with open(CENSUS, "a") as f:
             f.write(json.dumps(cen) + "\n")
         assert r["stats"]["n_gaussians"] == n
-        compare_images(r["image"], ref, tol=tol, tol_max=TOL_MAX)
-        assert cen["frac_over"] <= CENSUS_MAX_FRAC, cen
+        compare_images(r["image"], ref, tol=tol, tol_max=FULL_MAX)
+        assert cen["max"] <= FULL_MAX and cen["n_over"] <= FULL_N_OVER, cen
         if v == 0 and order_check:
             vs = O.vertex_stage(flat, g.sh_dim, U)
             assert r["stats"]["n_visible"] == int(vs["visible"].sum())

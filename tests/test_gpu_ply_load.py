@@ -1,8 +1,11 @@
 """The viewer's "Open ply" straight into a device scene (gsr_scene_load_ply,
-SURVEY.md §8(f) row 2) against the host path it replaces: load_ply's
-activations (util_gau.py:297-303, restated bit-exactly by ply.load_ply), then
-GaussianData.scale_data(5.0) (util_gau.py:44-53) and points_center, as
-gs_elements_control.py:41-44 does.
+SURVEY.md §8(f) row 2) against the oracle of the host path it replaces:
+oracle/ply_oracle.load_ply (the PLY vertex reader and load_ply's activations,
+util_gau.py:236-305, restated in the reference's own NumPy expressions), then
+GaussianData.scale_data(5.0) (util_gau.py:44-53, bit-exact against the
+reference-run fixture in tests/golden) and points_center, as
+gs_elements_control.py:41-44 does.  The product's own host loader is not
+the reference here.
 
 xyz, rot and sh are bit-identical; scale and opacity go through exp, which
 NumPy evaluates with its own float32 SIMD polynomial (up to ~2.5 ulp from the
@@ -12,7 +15,8 @@ import numpy as np
 import pytest
 
 from gsviewer_amd.camera import Camera
-from gsviewer_amd.ply import load_ply
+from gsviewer_amd.gaussian_data import GaussianData
+from oracle import ply_oracle as P
 from helpers import compare_images, TOL_EXACT
 from test_ply import vertex_array, write
 
@@ -22,7 +26,7 @@ EXP_ULPS = 4
 
 
 def _host(path, interval):
-    g = load_ply(path)
+    g = GaussianData(*P.load_ply(path))
     if interval > 0:
         g.scale_data(interval)
     return g

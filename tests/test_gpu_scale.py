@@ -128,3 +128,27 @@ def test_sort_depth_service_1m_with_ties(gpu):
     got = depth_order(scene, V).cpu().numpy().reshape(-1)
     scene.close()
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("limit", ["0", "1700", "1900"])
+def test_binning_mixes_staged_and_direct_blocks(gpu, monkeypatch, limit):
+    """k_bin_write stages a block's instances in LDS only when the block holds
+    at most GSR_BIN_STAGE_LIMIT (default 2048) of them; larger blocks write
+    directly.  The garden stand-in averages ~1.8 instances per splat, so the
+    limits 1700 / 1900 split one frame's 1024-splat blocks between the two
+    paths (0: every block direct).  Single view (k_bin_write) and a group of
+    views (k_bin_write_views): the tile lists must be the oracle's exactly."""
+    from gsviewer_amd.rasterizer import HipScene
+    from helpers import batched_frames
+    monkeypatch.setenv("GSR_BIN_STAGE_LIMIT", limit)
+    g = garden_standin(200_000, seed=1, sh_degree=0)
+    cam = Camera(540, 960).yaw(45)
+    U = uniforms_for(cam)
+    vs = O.vertex_stage(g.flat(), g.sh_dim, U)
+    res = gpu_frame(g, cam, _settings(), with_debug=True)
+    check_frame_order(res, vs, U)
+    scene = HipScene.from_gaussian_data(g)
+    cams = [cam, Camera(540, 960).yaw(135)]
+    got = batched_frames(scene, cams, _settings(), group=2, debug_views=(0,))
+    scene.close()
+    check_frame_order(got[0], vs, U)

@@ -2,9 +2,10 @@
 generated from the reference itself (tests/golden/make_golden.py)."""
 import numpy as np
 
-from gsviewer_amd.camera import Camera, euler_to_rotation_matrix
+from gsviewer_amd.camera import Camera, euler_to_rotation_matrix, rotation_matrix_to_euler
 from gsviewer_amd.gaussian_data import GaussianData, naive_gaussian
 from oracle import gl_oracle as O
+from oracle import ply_oracle as P
 
 
 def test_naive_gaussian_layout(golden):
@@ -70,3 +71,51 @@ def test_camera_yaw_views_orbit_target():
         p = V @ np.array([0, 0, 0, 1], np.float32)
         np.testing.assert_allclose(p[:3], [0, 0, -5], atol=2e-6)
         np.testing.assert_allclose(np.linalg.norm(cam.position), 5, rtol=1e-6)
+
+
+def test_rotation_matrix_to_euler_bit_exact(golden):
+    """util.convert_rotation_matrix_to_euler_angles (util.py:494-501, scipy
+    as_euler('xyz')) on the OBB test rotations, a gimbal-lock case and random
+    rotations: bit-exact, and the inverse of euler_to_rotation_matrix."""
+    for R, e in zip(golden["r2e_R"], golden["r2e_euler"]):
+        np.testing.assert_array_equal(rotation_matrix_to_euler(R), e)
+    for a in golden["euler_angles"][:3]:
+        np.testing.assert_allclose(euler_to_rotation_matrix(rotation_matrix_to_euler(euler_to_rotation_matrix(a))),
+                                   euler_to_rotation_matrix(a), atol=1e-12)
+
+
+def test_compute_obb_bit_exact(golden):
+    """GaussianData.compute_obb (util_gau.py:114-138): min, max, axes and
+    corners bit-exact on three point sets (uniform, rescaled, anisotropic)."""
+    for k in range(3):
+        p = golden[f"obb{k}_xyz"]
+        n = len(p)
+        g = GaussianData(p, np.tile(np.float32([1, 0, 0, 0]), (n, 1)), np.ones((n, 3), np.float32),
+                         np.ones((n, 1), np.float32), np.zeros((n, 3), np.float32))
+        mn, mx, U, corners = g.compute_obb
+        np.testing.assert_array_equal(mn, golden[f"obb{k}_min"])
+        np.testing.assert_array_equal(mx, golden[f"obb{k}_max"])
+        np.testing.assert_array_equal(U, golden[f"obb{k}_U"])
+        np.testing.assert_array_equal(corners, golden[f"obb{k}_corners"])
+
+
+def export_cases(golden):
+    """(aabb, obb, cube_min, cube_max, euler, bbox or None, rows) of the
+    reference-run export_ply + crop_by_bbox fixtures (make_golden.py)."""
+    rows = np.split(golden["export_rows"], np.cumsum(golden["export_nrows"])[:-1])
+    out = []
+    for prm, bbox, r in zip(golden["export_params"], golden["export_bbox"], rows):
+        bb = None if np.isnan(bbox).all() else tuple(bbox.tolist())
+        out.append((int(prm[0]), int(prm[1]), list(prm[2:5]), list(prm[5:8]), list(prm[8:11]), bb, r))
+    return out
+
+
+def test_export_oracle_matches_reference(golden):
+    """oracle/ply_oracle.export_rows == util_gau.export_ply's bbox (util_gau.py:
+    388-413) + gsconverter's crop_by_bbox rows (base_converter.py:175-191),
+    run on the reference itself: the export oracle is pinned."""
+    cur, orig = golden["export_cur"], golden["export_orig"]
+    for aabb, obb, cmin, cmax, rot, bbox, rows in export_cases(golden):
+        got_rows, got_bbox = P.export_rows(cur, orig, aabb, obb, cmin, cmax, euler_to_rotation_matrix(rot))
+        assert got_bbox == bbox
+        np.testing.assert_array_equal(got_rows, rows)
