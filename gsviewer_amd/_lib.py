@@ -132,7 +132,7 @@ SIGNATURES = {
     "gsr_context_set_profiling": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gsr_context_stage_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "gsr_context_group_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
-                                               ctypes.POINTER(ctypes.c_int64)]),
+                                               ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     # gsr_io.h
     "gsr_ply_probe": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(GsrPlyInfo)]),
     "gsr_ply_read": (ctypes.c_int, [ctypes.c_char_p, _P, _P, _P, _P, _P, ctypes.c_int32]),

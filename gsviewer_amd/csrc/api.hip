@@ -128,6 +128,9 @@ struct PendingFrame {
 };
 }  // namespace gsr
 
+// compositing launches whose in-kernel spans one profiling run can record
+constexpr size_t kSpanLaunches = 64;
+
 // depth sort passes of a frame rendered alone (gsr_render; see kDepthPasses)
 constexpr int kDepthPassesAlone = 3;
 
@@ -160,6 +163,7 @@ struct gsr_context {
                                                   // ones in len_classes - 1 length classes, longest first
     bool views_interleave = true;                 // a group's compositing dispatch class-major over its views
     bool first_major = true;                      // ... every tile's first chunk before any later one
+    bool first_major_alone = false;               // the same for a frame finished alone (gsr_render_finish)
     int depth_passes_alone = kDepthPassesAlone;   // depth sort passes of gsr_render's frames
     int depth_passes_now = 0;                     // this frame's (0: kDepthPasses)
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
@@ -193,6 +197,12 @@ struct gsr_context {
     int evg_slot = 0;
     double group_comp_ms = 0.0;
     int64_t group_launches = 0, group_views = 0;
+    // ... and each launch's own span from in-kernel clock stamps (first block
+    // start to last wave end): the kernel's execution, without the time its
+    // dispatch waited on the stream behind other streams' work
+    gsr::DevBuf<uint64_t> stamps;  // not in the workspace (profiling only): the launches' stamps, appended
+    size_t stamp_used = 0;
+    std::vector<std::pair<size_t, size_t>> spans;  // per recorded launch: (offset, blocks) in `stamps`
     bool failed = false;           // a wait timed out or the stream faulted: no further frames
     int64_t wait_timeout_ms = 2000;
     gsr::Arena arena;              // caller workspace (gsr_context_attach_workspace) or sizing pass
@@ -662,6 +672,8 @@ int gsr_context_create(gsr_context** out) {
         if (v >= 3 && v <= 4) (*out)->depth_passes_alone = (int)v;
     }
     if (const char* e = std::getenv("GSR_FIRST_MAJOR")) (*out)->first_major = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("GSR_FIRST_MAJOR_ALONE"))
+        (*out)->first_major_alone = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_VIEWS_INTERLEAVE")) (*out)->views_interleave = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_WAIT_TIMEOUT_MS")) {
         const long v = std::strtol(e, nullptr, 10);
@@ -681,6 +693,7 @@ int gsr_context_destroy(gsr_context* c) {
     for (auto& row : c->evg)
         for (auto& e : row)
             if (e) (void)hipEventDestroy(e);
+    c->stamps.release();
     delete c;
     return GSR_OK;
 }
@@ -1047,7 +1060,7 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
         if ((rc = c->tmax.ensure(max_chunks, "tmax"))) return rc;
         if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->len_classes, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
-                                c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s)))
+                                c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s, c->first_major_alone)))
             return rc;
         if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
         if ((rc = launch_composite(c->chunk_desc.p, c->chunk_order.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
@@ -1182,8 +1195,21 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
             prof_group_accumulate(c0, gslot);  // slot reuse: that launch is two groups back
             GSR_HIP_CHECK(hipEventRecord(c0->evg[gslot][0], s));
         }
+        // in-kernel clock stamps of the launch (profiling): room for kSpanLaunches
+        // launches of this size is reserved at the first one, so recording
+        // never reallocates inside a profiled region
+        uint64_t* stamps = nullptr;
+        const size_t blocks = composite_views_blocks((uint32_t)max_chunks, k);
+        if (c0->prof_group) {
+            if (!c0->stamps.p && (rc = c0->stamps.ensure(kSpanLaunches * blocks * 5, "stamps"))) return rc;
+            if (c0->stamp_used + blocks * 5 <= c0->stamps.cap) {
+                stamps = c0->stamps.p + c0->stamp_used;
+                c0->spans.emplace_back(c0->stamp_used, blocks);
+                c0->stamp_used += blocks * 5;
+            }
+        }
         if ((rc = launch_composite_views(fv, k, (uint32_t)max_chunks, c0->len_classes, c0->first_major, c0->views_interleave, u0,
-                                         frag_class_of(u0.render_mod), f0.t_min, f0.bg, f0.out_layout, s)))
+                                         frag_class_of(u0.render_mod), f0.t_min, f0.bg, f0.out_layout, s, stamps)))
             return rc;
         if (c0->prof_group) {
             GSR_HIP_CHECK(hipEventRecord(c0->evg[gslot][1], s));
@@ -1229,6 +1255,8 @@ int gsr_context_set_profiling(gsr_context* c, int32_t enable) {
         c->prof_on = false;
         c->group_comp_ms = 0.0;
         c->group_launches = c->group_views = 0;
+        c->stamp_used = 0;
+        c->spans.clear();
         return GSR_OK;
     }
     c->prof_group = false;
@@ -1251,12 +1279,30 @@ int gsr_context_stage_times(gsr_context* c, double* ms_out, int64_t* frames_out)
     return GSR_OK;
 }
 
-int gsr_context_group_times(gsr_context* c, double* composite_ms, int64_t* launches, int64_t* views) {
+int gsr_context_group_times(gsr_context* c, double* composite_ms, int64_t* launches, int64_t* views,
+                            double* span_ms) {
     if (!c || !composite_ms || !launches || !views) return set_error(GSR_ERR_INVALID, "null argument");
     for (int k = 0; k < 2; ++k) prof_group_accumulate(c, (c->evg_slot + k) & 1);
     *composite_ms = c->group_comp_ms;
     *launches = c->group_launches;
     *views = c->group_views;
+    if (span_ms) {
+        *span_ms = 0.0;
+        if (!c->spans.empty()) {
+            std::vector<uint64_t> st(c->stamp_used);
+            GSR_HIP_CHECK(hipDeviceSynchronize());
+            GSR_HIP_CHECK(hipMemcpy(st.data(), c->stamps.p, c->stamp_used * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            uint64_t sum = 0;
+            for (const auto& sp : c->spans) {
+                const uint64_t* b = st.data() + sp.first;
+                uint64_t lo = ~0ull, hi = 0;
+                for (size_t i = 0; i < sp.second; ++i) lo = std::min(lo, b[i]);
+                for (size_t i = 0; i < 4 * sp.second; ++i) hi = std::max(hi, b[sp.second + i]);
+                sum += hi > lo ? hi - lo : 0;
+            }
+            *span_ms = (double)sum * 1e-5;  // 100 MHz constant clock
+        }
+    }
     return GSR_OK;
 }
 

@@ -394,9 +394,9 @@ __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, in
 
 __global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restrict__ ranges, int num_tiles,
                                                           uint32_t chunk, uint32_t classes,
-                                                          uint32_t* __restrict__ tot) {
+                                                          uint32_t* __restrict__ tot, uint32_t first_major) {
     __shared__ uint32_t lds[1 + kMaxLenClasses][kThreads / 64];
-    chunk_count(ranges, num_tiles, chunk, classes, false, tot, lds);
+    chunk_count(ranges, num_tiles, chunk, classes, first_major != 0, tot, lds);
 }
 
 struct ChunkWriteLds {
@@ -514,10 +514,10 @@ __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restric
                                                           uint32_t* __restrict__ chunk_base,
                                                           uint32_t* __restrict__ n_extra_dev,
                                                           uint4* __restrict__ desc, uint32_t* __restrict__ order,
-                                                          float4* __restrict__ tmax) {
+                                                          float4* __restrict__ tmax, uint32_t first_major) {
     __shared__ ChunkWriteLds sh;
-    chunk_write(ranges, num_tiles, chunk, classes, false, tot, chunk_cnt, chunk_base, n_extra_dev, desc, order, tmax,
-                sh);
+    chunk_write(ranges, num_tiles, chunk, classes, first_major != 0, tot, chunk_cnt, chunk_base, n_extra_dev, desc,
+                order, tmax, sh);
 }
 
 struct ChunkView {
@@ -995,6 +995,7 @@ struct CompViews {
     uint32_t k, classes;      // views; length classes (k * classes <= 64 when interleaved)
     uint32_t view_blocks;     // view-major: blocks per view
     uint32_t interleave;
+    uint64_t* stamps;         // profiling (else null): [grid] block starts, then [grid * waves] wave ends
 };
 
 // Interleaved dispatch: the (view, position) of the group's p-th chunk, or
@@ -1025,9 +1026,8 @@ __device__ __forceinline__ int interleaved_chunk(const CompViews& vs, uint32_t p
 }
 
 template <int FRAG>
-__global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite_views(CompViews vs, CompositeArgs a) {
-    __shared__ float4 lds[kCompWaves][kBatch * 3];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+__device__ __forceinline__ void composite_views_wave(const CompViews& vs, const CompositeArgs& a, float4* lds,
+                                                     int wave) {
     int view;
     uint32_t pos;
     if (vs.interleave) {
@@ -1042,8 +1042,19 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite_views(C
     if (pos >= (uint32_t)a.num_tiles + v.n_chunks_dev[0]) return;
     const uint32_t slot = v.order[pos];
     const uint4 d = v.desc[slot];
-    composite_chunk<FRAG>(d, slot, lds[wave], v.list, v.recs, a, v.out, v.partial, v.sat, v.tmax);
+    composite_chunk<FRAG>(d, slot, lds, v.list, v.recs, a, v.out, v.partial, v.sat, v.tmax);
 }
+
+template <int FRAG>
+__global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite_views(CompViews vs, CompositeArgs a) {
+    __shared__ float4 lds[kCompWaves][kBatch * 3];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (vs.stamps && threadIdx.x == 0) vs.stamps[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    composite_views_wave<FRAG>(vs, a, lds[wave], wave);
+    if (vs.stamps && __lane_id() == 0)
+        vs.stamps[gridDim.x + blockIdx.x * kCompWaves + wave] = __builtin_amdgcn_s_memrealtime();
+}
+
 
 // Fold the partial results of multi-chunk tiles in depth order: one block per
 // tile of 4 x P waves (P = kMergeParts); wave w folds slice (w & 3) over the
@@ -1371,7 +1382,7 @@ const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uin
 
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
-                  hipStream_t s) {
+                  hipStream_t s, bool first_major) {
 #ifndef GSR_COMP_BOUND
     tmax = nullptr;  // the published maxima are only read by the bound variant
 #endif
@@ -1379,10 +1390,10 @@ int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t c
     const unsigned g = (unsigned)((num_tiles + kThreads - 1) / kThreads);
     // the per-block totals live in chunk_cnt past its num_tiles entries
     uint32_t* tot = chunk_cnt + num_tiles;
-    k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot);
+    k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot, first_major ? 1u : 0u);
     GSR_LAUNCH_CHECK("chunk_count");
     k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot, chunk_cnt, chunk_base, n_extra_dev,
-                                         desc, order, tmax);
+                                         desc, order, tmax, first_major ? 1u : 0u);
     GSR_LAUNCH_CHECK("chunk_write");
     return GSR_OK;
 }
@@ -1511,7 +1522,7 @@ int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk,
 
 int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32_t classes, bool first_major,
                            bool interleave, const FrameUniforms& u, int frag_class, float t_min, const float* bg,
-                           int out_layout, hipStream_t s) {
+                           int out_layout, hipStream_t s, uint64_t* stamps) {
     const CompositeArgs a = make_args(u, t_min, bg, out_layout);
     CompViews cv{};
     for (int i = 0; i < k; ++i) {
@@ -1523,6 +1534,7 @@ int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32
     cv.classes = classes + (first_major ? 1u : 0u);  // first-major: the later chunks as one more class
     cv.view_blocks = (max_chunks + kCompWaves - 1) / kCompWaves;
     cv.interleave = interleave && (uint32_t)k * cv.classes <= 64u;
+    cv.stamps = stamps;
     const dim3 grid(cv.view_blocks * (unsigned)k);
     switch (frag_class) {
         case kFragGauss: k_composite_views<kFragGauss><<<grid, kCompThreads, 0, s>>>(cv, a); break;
@@ -1532,6 +1544,10 @@ int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32
     }
     GSR_LAUNCH_CHECK("composite_views");
     return GSR_OK;
+}
+
+size_t composite_views_blocks(uint32_t max_chunks, int k) {
+    return (size_t)((max_chunks + kCompWaves - 1) / kCompWaves) * (size_t)k;
 }
 
 int launch_merge_views(FinishView* views, int k, const FrameUniforms& u, float t_min, const float* bg,

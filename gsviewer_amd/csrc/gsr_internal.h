@@ -320,7 +320,7 @@ size_t chunk_cnt_elems(int num_tiles);
 // of each class lands at chunk_class_totals(chunk_cnt, num_tiles, classes)
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
-                  hipStream_t s);
+                  hipStream_t s, bool first_major = false);
 const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes);
 int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n_chunks_dev, uint32_t max_chunks,
                      const uint32_t* chunk_cnt, const uint32_t* chunk_base, uint32_t* sat,
@@ -369,9 +369,14 @@ int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s);
 int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, uint32_t classes, bool first_major,
                         hipStream_t s);
 // interleave: dispatch class-major over the views (k * classes <= 64), else view after view
+// stamps (nullable, profiling): the launch writes, by plain stores, every
+// block's start clock ([blocks]) and then every wave's end clock
+// ([blocks * 4]) of the 100 MHz constant clock (s_memrealtime).
 int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32_t classes, bool first_major,
                            bool interleave, const FrameUniforms& u, int frag_class, float t_min, const float* bg,
-                           int out_layout, hipStream_t s);
+                           int out_layout, hipStream_t s, uint64_t* stamps = nullptr);
+// Blocks of one launch_composite_views launch (stamps: 5 words per block).
+size_t composite_views_blocks(uint32_t max_chunks, int k);
 int launch_merge_views(FinishView* views, int k, const FrameUniforms& u, float t_min, const float* bg,
                        int out_layout, hipStream_t s);
 

@@ -264,9 +264,14 @@ int gsr_context_set_profiling(gsr_context* ctx, int32_t enable);
  * (waits for the last profiled frame's events). */
 int gsr_context_stage_times(gsr_context* ctx, double* ms_out /* [GSR_NUM_STAGES] */, int64_t* frames_out);
 /* Profiling mode 2: summed milliseconds of the group compositing launches
- * (k_composite_views, HIP events on the group's stream), the number of
- * launches and the views they composited (waits for the last launch). */
-int gsr_context_group_times(gsr_context* ctx, double* composite_ms, int64_t* launches, int64_t* views);
+ * (k_composite_views) measured by HIP events on the group's stream, the
+ * number of launches and the views they composited, and (span_ms, nullable)
+ * the summed in-kernel spans of the same launches: first block start to last
+ * wave end by the 100 MHz constant clock (s_memrealtime), i.e. the kernel's
+ * execution without the time its dispatch waited behind other streams'
+ * work.  Synchronises the device. */
+int gsr_context_group_times(gsr_context* ctx, double* composite_ms, int64_t* launches, int64_t* views,
+                            double* span_ms);
 
 /* Host time spent inside gsr_render on this context since creation, in ms:
  * [0] enqueue before the wait for the frame's counts, [1] that wait,

@@ -3,6 +3,7 @@
 # build, parity tests, smoke, bench, rocprofv3 kernel stats, HBM PMC passes.
 # usage: gpurun --timeout 1100 -- bash tools/gpu_round.sh TAG [quick|full]
 #   quick: build, parity tests, smoke, bench (no CPU baseline), kernel stats
+#   full: + the CPU baseline and the PMC traffic passes (tools/pmc.sh TAG traffic)
 # Every step has its own time limit; the first failing step ends the script.
 TAG=${1:-run}
 MODE=${2:-full}
@@ -24,7 +25,7 @@ step() {  # step NAME SECONDS CMD...
 }
 
 step build 300 bash -c "python -c 'import __graft_entry__ as g; g.build()' > $O/build.log 2>&1"
-step pytest_gpu 500 bash -c "python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1"
+step pytest_gpu 600 bash -c "python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1"
 step smoke 120 bash -c "python -c 'import __graft_entry__ as g; g.smoke()' > $O/smoke.log 2>&1"
 if [ "$MODE" = quick ]; then
     step bench 300 bash -c "python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err"
@@ -34,10 +35,6 @@ fi
 step rocprof_stats 240 bash -c "rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- $B > $O/bench_under_rocprof.json 2> $O/rocprof.err"
 find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \;
 if [ "$MODE" != quick ]; then
-    step pmc_fetch 240 bash -c "rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o pmc --output-format csv -- $B > $O/pmc_fetch.log 2>&1"
-    step pmc_write 240 bash -c "rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o pmc --output-format csv -- $B > $O/pmc_write.log 2>&1"
-    step pmc_valu 240 bash -c "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_WAVES -d $O/pmc_valu -o pmc --output-format csv -- $B > $O/pmc_valu.log 2>&1"
-    python profiles/summarize_pmc.py $O/pmc_summary.csv \
-        $(find $O/pmc_fetch $O/pmc_write $O/pmc_valu -name '*counter_collection.csv' -printf '%h\n' | sort -u)
+    step pmc 800 bash tools/pmc.sh $TAG traffic
 fi
 echo "[gpu_round] done"
