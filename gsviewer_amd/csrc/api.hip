@@ -164,6 +164,7 @@ struct gsr_context {
     bool views_interleave = true;                 // a group's compositing dispatch class-major over its views
     bool first_major = true;                      // ... every tile's first chunk before any later one
     bool first_major_alone = false;               // the same for a frame finished alone (gsr_render_finish)
+    bool bin_fused = true;                        // the tile sort's pass 0 fused into the binning (k_bin_scatter)
     int depth_passes_alone = kDepthPassesAlone;   // depth sort passes of gsr_render's frames
     int depth_passes_now = 0;                     // this frame's (0: kDepthPasses)
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
@@ -423,8 +424,9 @@ int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const 
 
 int sort_pairs(gsr_context* c, uint32_t** ka, uint32_t** va, uint32_t** kb, uint32_t** vb, bool ident, size_t n,
                const uint32_t* n_dev, int bits, int passes, const uint32_t* key_range, uint32_t* totals,
-               hipStream_t s) {
-    return radix_sort_pairs(ka, va, kb, vb, ident, n, n_dev, bits, passes, key_range, c->radix_tmp.p, totals, s);
+               hipStream_t s, int first_pass = 0) {
+    return radix_sort_pairs(ka, va, kb, vb, ident, n, n_dev, bits, passes, key_range, c->radix_tmp.p, totals, s,
+                            nullptr, nullptr, nullptr, first_pass);
 }
 
 bool rects_packable(const FrameUniforms& u) {
@@ -672,6 +674,7 @@ int gsr_context_create(gsr_context** out) {
         if (v >= 3 && v <= 4) (*out)->depth_passes_alone = (int)v;
     }
     if (const char* e = std::getenv("GSR_FIRST_MAJOR")) (*out)->first_major = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("GSR_BIN_FUSED")) (*out)->bin_fused = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_FIRST_MAJOR_ALONE"))
         (*out)->first_major_alone = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_VIEWS_INTERLEAVE")) (*out)->views_interleave = std::strtol(e, nullptr, 10) != 0;
@@ -718,14 +721,16 @@ int gsr_context_reserve(gsr_context* c, int64_t n, int32_t width, int32_t height
     int rc;
     // the shared radix scratch at its final size first: a smaller block sized by
     // ensure_scene_buffers would be retired (and, in a caller's workspace, wasted)
-    if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(d), radix_tmp_elems(un)), "radix_tmp"))) return rc;
+    const int rtbits = bits_for((uint32_t)num_tiles);
+    const size_t rhist = bin_hist_elems(un, rtbits > 0 ? rtbits : 1, std::max(1, radix_passes_for(rtbits)));
+    if ((rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(d), radix_tmp_elems(un), rhist}), "radix_tmp"))) return rc;
     if ((rc = ensure_scene_buffers(c, un))) return rc;
     if ((rc = c->zero.ensure(ZeroLayout(num_tiles).total, "zero block"))) return rc;
     if ((rc = c->tkeys_a.ensure(d, "tile_keys"))) return rc;
     if ((rc = c->tkeys_b.ensure(d, "tile_keys"))) return rc;
     if ((rc = c->tvals_a.ensure(d, "tile_vals"))) return rc;
     if ((rc = c->tvals_b.ensure(d, "tile_vals"))) return rc;
-    if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(d), radix_tmp_elems(un)), "radix_tmp"))) return rc;
+    if ((rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(d), radix_tmp_elems(un), rhist}), "radix_tmp"))) return rc;
     const size_t mc = (size_t)num_tiles + d / std::min(c->chunk, c->chunk_views) + 1;
     if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
     if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
@@ -1018,25 +1023,34 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     if (n_vis > 0) c->last_depth_order = f.va;
 
     uint32_t* tile_list = c->tvals_a.p;
+    const int tbits = bits_for((uint32_t)num_tiles);
+    const int tpasses = radix_passes_for(tbits);
+    const bool fused = c->bin_fused;
     if (n_dup > 0) {
         if ((rc = c->tkeys_a.ensure(n_dup, "tile_keys"))) return rc;
         if ((rc = c->tkeys_b.ensure(n_dup, "tile_keys"))) return rc;
         if ((rc = c->tvals_a.ensure(n_dup, "tile_vals"))) return rc;
         if ((rc = c->tvals_b.ensure(n_dup, "tile_vals"))) return rc;
-        if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(n_dup), radix_tmp_elems(n)), "radix_tmp")))
+        if ((rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(n_dup), radix_tmp_elems(n),
+                                                bin_hist_elems(n_vis, tbits > 0 ? tbits : 1, tpasses > 0 ? tpasses : 1)}),
+                                      "radix_tmp")))
             return rc;
-        if ((rc = launch_binning(f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, u.tiles_x, c->bin_tmp.p, c->trect_sorted.p, c->tkeys_a.p,
-                                 c->tvals_a.p, s)))
-            return rc;
+        if (fused)  // the tile sort's pass 0 in the binning: instances leave it ordered by digit 0
+            rc = launch_binning_sorted(f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, u.tiles_x, tbits, tpasses,
+                                       c->radix_tmp.p, c->zero.p + zl.totals_tile, c->trect_sorted.p, c->tkeys_a.p,
+                                       c->tvals_a.p, s);
+        else
+            rc = launch_binning(f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, u.tiles_x, c->bin_tmp.p,
+                                c->trect_sorted.p, c->tkeys_a.p, c->tvals_a.p, s);
+        if (rc) return rc;
     }
     if ((rc = prof_record(c, slot, EV_COUNTS, s))) return rc;
     if ((rc = prof_record(c, slot, EV_AFTER_SYNC2, s))) return rc;
     if ((rc = prof_record(c, slot, EV_DUPW, s))) return rc;
     uint32_t *tka = c->tkeys_a.p, *tkb = c->tkeys_b.p, *tva = c->tvals_a.p, *tvb = c->tvals_b.p;
     if (n_dup > 0) {
-        const int tbits = bits_for((uint32_t)num_tiles);
-        if (tbits > 0 && (rc = sort_pairs(c, &tka, &tva, &tkb, &tvb, false, n_dup, nullptr, tbits,
-                                          radix_passes_for(tbits), nullptr, c->zero.p + zl.totals_tile, s)))
+        if (tbits > 0 && (rc = sort_pairs(c, &tka, &tva, &tkb, &tvb, false, n_dup, nullptr, tbits, tpasses, nullptr,
+                                          c->zero.p + zl.totals_tile, s, fused ? 1 : 0)))
             return rc;
         tile_list = tva;
         c->last_tile_list = tva;
@@ -1164,17 +1178,29 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
                               c->zero.p + zl.totals_tile};
     }
     // every view's sort temporaries cover the largest view (the grids do)
+    const int tbits = bits_for((uint32_t)num_tiles);
+    const int tpasses = radix_passes_for(tbits);
+    const bool fused = c0->bin_fused;
+    uint32_t* hist[GSR_MAX_VIEWS];
+    uint32_t* ttot[GSR_MAX_VIEWS];
     for (int v = 0; v < k && n_dup_max > 0; ++v) {
         gsr_context* c = ctxs[v];
-        if ((rc = c->radix_tmp.ensure(std::max(radix_tmp_elems(n_dup_max), radix_tmp_elems(c->pend.n)),
+        if ((rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(n_dup_max), radix_tmp_elems(c->pend.n),
+                                                bin_hist_elems(n_vis_max, tbits > 0 ? tbits : 1,
+                                                               tpasses > 0 ? tpasses : 1)}),
                                       "radix_tmp")))
             return rc;
         rv[v].tmp = c->radix_tmp.p;
+        hist[v] = c->radix_tmp.p;
+        ttot[v] = c->zero.p + zl.totals_tile;
     }
-    if (n_vis_max > 0 && (rc = launch_binning_views(fv, k, u0.tiles_x, s))) return rc;
-    const int tbits = bits_for((uint32_t)num_tiles);
+    if (n_vis_max > 0 && n_dup_max > 0) {
+        rc = fused ? launch_binning_sorted_views(fv, hist, ttot, k, u0.tiles_x, tbits, tpasses, s)
+                   : launch_binning_views(fv, k, u0.tiles_x, s);
+        if (rc) return rc;
+    }
     if (n_dup_max > 0 && tbits > 0 &&
-        (rc = radix_sort_pairs_views(rv, k, false, n_dup_max, tbits, radix_passes_for(tbits), s)))
+        (rc = radix_sort_pairs_views(rv, k, false, n_dup_max, tbits, tpasses, s, fused ? 1 : 0)))
         return rc;
     for (int v = 0; v < k; ++v) {
         fv[v].tile_keys = tka[v];

@@ -227,6 +227,284 @@ __global__ __launch_bounds__(kThreads) void k_bin_write_views(BinViews vs, int t
                        v.tile_vals, blockIdx.x, lds, stage, stage_limit);
 }
 
+// ------------------------------------------------------------------------
+// The tile sort's first radix pass fused into the binning (the default).
+// The tile sort is a stable LSD radix over the instances in binning order
+// (depth order, then row-major tiles of each splat).  Its first pass orders
+// the instances by digit 0 of the tile id; the binning produces them anyway,
+// so it writes each one straight to that pass's position:
+//   k_bin_hist:    per block of 1024 depth-sorted splats, its instances per
+//                  digit 0 (LDS atomics), digit-major hist[d * blocks + b];
+//   radix_offsets: the per-digit exclusive prefix over the blocks (the radix
+//                  sort's own offsets kernel) and the digit totals;
+//   k_bin_scatter: the block's instances in generation order staged in LDS
+//                  (windows of kBinStage), ranked stably by digit (ballot
+//                  matching, per-wave digit counts), restaged in digit order
+//                  and written as contiguous runs to their pass-0 positions.
+// The instances leave the binning already sorted by digit 0: the tile sort's
+// pass-0 upsweep and scatter launches and one read + write of every instance
+// are gone.  The remaining passes run as before (radix_sort_pairs from pass 1).
+template <int kCB>
+struct BinScatterLds {
+    uint32_t k[kBinStage], v[kBinStage];    // a window of the block's instances, generation order
+    uint32_t k2[kBinStage], v2[kBinStage];  // ... restaged in digit order
+    uint16_t wcnt[kThreads / 64][1 << kCB];  // per-wave digit counts, then per-wave prefixes
+    uint32_t dbase[1 << kCB];                // window-local digit offsets
+    uint32_t gbase[1 << kCB];                // global position of the digit's next instance
+    uint32_t scan[2][kThreads / 64];
+};
+
+// (sorted rect of depth-sorted splat r)
+template <bool kPacked>
+__device__ __forceinline__ uint2 sorted_rect(const uint32_t* __restrict__ sorted_ids, const uint2* __restrict__ trect,
+                                             const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis, uint32_t r,
+                                             uint2* __restrict__ trect_sorted) {
+    if constexpr (kPacked) {
+        return unpack_rect(rect4_sorted[r]);
+    } else {
+        const uint32_t id = sorted_ids[r];
+        const uint2 tr = id < n_vis ? trect[id] : make_uint2(0xffffu, 0u);
+        trect_sorted[r] = tr;
+        return tr;
+    }
+}
+
+template <bool kPacked, int kCB>
+__device__ __forceinline__ void bin_hist(const uint32_t* __restrict__ sorted_ids, const uint2* __restrict__ trect,
+                                         const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis, int tiles_x,
+                                         const PassArgs& pa, uint32_t* __restrict__ hist, uint32_t nbb,
+                                         uint2* __restrict__ trect_sorted, uint32_t blk, uint32_t* h) {
+    const Digit dg = digit_params(pa);
+    const uint32_t radix = dg.mask + 1u;
+    for (uint32_t d = threadIdx.x; d < radix; d += kThreads) h[d] = 0u;
+    __syncthreads();
+    const uint32_t base = blk * kBinBlock + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kBinItems; ++k) {
+        const uint32_t r = base + k * kThreads;
+        if (r >= n_vis) continue;
+        const uint2 tr = sorted_rect<kPacked>(sorted_ids, trect, rect4_sorted, n_vis, r, trect_sorted);
+        const uint32_t tx0 = tr.x & 0xffffu, tx1 = tr.x >> 16, ty0 = tr.y & 0xffffu, ty1 = tr.y >> 16;
+        if (tx0 > tx1) continue;
+        for (uint32_t ty = ty0; ty <= ty1; ++ty)
+            for (uint32_t tx = tx0; tx <= tx1; ++tx) atomicAdd(&h[dg.of(ty * (uint32_t)tiles_x + tx)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < radix; d += kThreads) hist[(size_t)d * nbb + blk] = h[d];
+}
+
+template <bool kPacked, int kCB>
+__global__ __launch_bounds__(kThreads) void k_bin_hist(const uint32_t* __restrict__ sorted_ids,
+                                                       const uint2* __restrict__ trect,
+                                                       const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
+                                                       int tiles_x, PassArgs pa, uint32_t* __restrict__ hist,
+                                                       uint32_t nbb, uint2* __restrict__ trect_sorted) {
+    __shared__ uint32_t h[1 << kCB];
+    bin_hist<kPacked, kCB>(sorted_ids, trect, rect4_sorted, n_vis, tiles_x, pa, hist, nbb, trect_sorted, blockIdx.x,
+                           h);
+}
+
+template <bool kPacked, int kCB>
+__device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_ids,
+                                            const uint2* __restrict__ trect_sorted,
+                                            const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis, int tiles_x,
+                                            const PassArgs& pa, const uint32_t* __restrict__ hist_off,
+                                            const uint32_t* __restrict__ totals, uint32_t nbb,
+                                            uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ tile_vals,
+                                            uint32_t blk, BinScatterLds<kCB>& L) {
+    constexpr int kCap = 1 << kCB;
+    constexpr int kDpt = kCap / kThreads > 0 ? kCap / kThreads : 1;  // digits per thread
+    constexpr int kWaveItems = kBinStage / (kThreads / 64);           // window items per wave
+    constexpr int kRounds = kWaveItems / 64;
+    const Digit dg = digit_params(pa);
+    const uint32_t radix = dg.mask + 1u;
+    const int w = threadIdx.x >> 6;
+    // digits of this thread: [d0, d0 + q); their totals and this block's offsets
+    const uint32_t q = (radix + kThreads - 1) / kThreads;
+    const uint32_t d0 = threadIdx.x * q;
+    uint32_t gt[kDpt], ho[kDpt];
+#pragma unroll
+    for (int j = 0; j < kDpt; ++j) {
+        const uint32_t d = d0 + j;
+        const bool mine = j < (int)q && d < radix;
+        gt[j] = mine ? totals[d] : 0u;
+        ho[j] = mine ? hist_off[(size_t)d * nbb + blk] : 0u;
+    }
+    // this thread's 4 consecutive depth-sorted splats
+    const uint32_t base = blk * kBinBlock + threadIdx.x * kBinItems;
+    uint32_t id[kBinItems];
+    uint2 tr[kBinItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kBinItems; ++k) {
+        const uint32_t r = base + k;
+        id[k] = r < n_vis ? sorted_ids[r] : 0u;
+        if constexpr (kPacked)
+            tr[k] = r < n_vis ? unpack_rect(rect4_sorted[r]) : make_uint2(0xffffu, 0u);
+        else
+            tr[k] = r < n_vis ? trect_sorted[r] : make_uint2(0xffffu, 0u);
+        s += rect_tiles(tr[k]);
+    }
+    {  // global start of each digit's run of this block: digit base + the earlier blocks' counts
+        uint32_t sg = 0;
+#pragma unroll
+        for (int j = 0; j < kDpt; ++j) sg += gt[j];
+        uint32_t tg;
+        uint32_t eg = block_exclusive<kThreads>(sg, L.scan[0], tg);
+#pragma unroll
+        for (int j = 0; j < kDpt; ++j) {
+            const uint32_t d = d0 + j;
+            if (j < (int)q && d < radix) L.gbase[d] = eg + ho[j];
+            eg += gt[j];
+        }
+    }
+    uint32_t total;
+    const uint32_t o = block_exclusive<kThreads>(s, L.scan[1], total);  // (its barrier publishes gbase)
+    for (uint32_t c0 = 0; c0 < total; c0 += (uint32_t)kBinStage) {
+        // 1. this window's instances, in generation order
+        if (o < c0 + (uint32_t)kBinStage && o + s > c0) {
+            uint32_t idx = o;
+#pragma unroll
+            for (int k = 0; k < kBinItems; ++k) {
+                const uint32_t tx0 = tr[k].x & 0xffffu, tx1 = tr[k].x >> 16, ty0 = tr[k].y & 0xffffu,
+                               ty1 = tr[k].y >> 16;
+                if (tx0 > tx1) continue;
+                for (uint32_t ty = ty0; ty <= ty1; ++ty)
+                    for (uint32_t tx = tx0; tx <= tx1; ++tx, ++idx)
+                        if (idx >= c0 && idx < c0 + (uint32_t)kBinStage) {
+                            L.k[idx - c0] = ty * (uint32_t)tiles_x + tx;
+                            L.v[idx - c0] = id[k];
+                        }
+            }
+        }
+        {
+            uint32_t* wz = reinterpret_cast<uint32_t*>(&L.wcnt[0][0]);
+            for (uint32_t i = threadIdx.x; i < (uint32_t)(kThreads / 64 * kCap / 2); i += kThreads) wz[i] = 0u;
+        }
+        __syncthreads();
+        const uint32_t cnt = min((uint32_t)kBinStage, total - c0);
+        // 2. stable ranks: wave w owns window items [w * kWaveItems, (w + 1) * kWaveItems)
+        uint32_t key[kRounds], rank[kRounds];
+#pragma unroll
+        for (int r = 0; r < kRounds; ++r) {
+            const uint32_t j = (uint32_t)(w * kWaveItems + r * 64) + __lane_id();
+            const bool valid = j < cnt;
+            key[r] = valid ? L.k[j] : 0u;
+            const uint32_t d = dg.of(key[r]);
+            const uint64_t peers = match_digit(d, dg.w, valid);
+            uint32_t rk = 0xffffffffu;
+            if (valid) {
+                const uint32_t old = L.wcnt[w][d];
+                const uint32_t below =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+                rk = old + below;
+                if (below == 0) L.wcnt[w][d] = (uint16_t)(old + __popcll(peers));
+            }
+            rank[r] = rk;
+        }
+        __syncthreads();
+        // 3. per owned digit: wave prefixes, the window-local digit offsets
+        uint32_t tot[kDpt];
+        {
+            uint32_t sl = 0;
+#pragma unroll
+            for (int j = 0; j < kDpt; ++j) {
+                const uint32_t d = d0 + j;
+                tot[j] = 0u;
+                if (j < (int)q && d < radix) {
+                    uint32_t run = 0;
+#pragma unroll
+                    for (int k = 0; k < kThreads / 64; ++k) {
+                        const uint32_t c = L.wcnt[k][d];
+                        L.wcnt[k][d] = (uint16_t)run;
+                        run += c;
+                    }
+                    tot[j] = run;
+                }
+                sl += tot[j];
+            }
+            uint32_t tl;
+            uint32_t el = block_exclusive<kThreads>(sl, L.scan[0], tl);
+#pragma unroll
+            for (int j = 0; j < kDpt; ++j) {
+                const uint32_t d = d0 + j;
+                if (j < (int)q && d < radix) L.dbase[d] = el;
+                el += tot[j];
+            }
+        }
+        __syncthreads();
+        // 4. restage in digit order
+#pragma unroll
+        for (int r = 0; r < kRounds; ++r) {
+            if (rank[r] != 0xffffffffu) {
+                const uint32_t j = (uint32_t)(w * kWaveItems + r * 64) + __lane_id();
+                const uint32_t d = dg.of(key[r]);
+                const uint32_t p = L.dbase[d] + L.wcnt[w][d] + rank[r];
+                L.k2[p] = key[r];
+                L.v2[p] = L.v[j];
+            }
+        }
+        __syncthreads();
+        // 5. contiguous runs to the pass-0 positions
+        for (uint32_t j = threadIdx.x; j < cnt; j += kThreads) {
+            const uint32_t kk = L.k2[j];
+            const uint32_t d = dg.of(kk);
+            const uint32_t g = L.gbase[d] + (j - L.dbase[d]);
+            tile_keys[g] = kk;
+            tile_vals[g] = L.v2[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kDpt; ++j) {
+            const uint32_t d = d0 + j;
+            if (j < (int)q && d < radix) L.gbase[d] += tot[j];  // the next window continues each run
+        }
+        __syncthreads();
+    }
+}
+
+template <bool kPacked, int kCB>
+__global__ __launch_bounds__(kThreads) void k_bin_scatter(const uint32_t* __restrict__ sorted_ids,
+                                                          const uint2* __restrict__ trect_sorted,
+                                                          const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
+                                                          int tiles_x, PassArgs pa,
+                                                          const uint32_t* __restrict__ hist_off,
+                                                          const uint32_t* __restrict__ totals, uint32_t nbb,
+                                                          uint32_t* __restrict__ tile_keys,
+                                                          uint32_t* __restrict__ tile_vals) {
+    __shared__ BinScatterLds<kCB> L;
+    bin_scatter<kPacked, kCB>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tiles_x, pa, hist_off, totals, nbb,
+                              tile_keys, tile_vals, blockIdx.x, L);
+}
+
+// Views of a group (blockIdx.y = view): hist / totals per view.
+struct BinSortViews {
+    BinView v[kMaxViews];
+    uint32_t* hist[kMaxViews];
+    const uint32_t* totals[kMaxViews];
+};
+
+// Every view's count matrix has nbb (the largest view's blocks) columns; a
+// view's blocks past its own splats count zeros, so its offsets are exact.
+template <bool kPacked, int kCB>
+__global__ __launch_bounds__(kThreads) void k_bin_hist_views(BinSortViews vs, int tiles_x, PassArgs pa,
+                                                             uint32_t nbb) {
+    __shared__ uint32_t h[1 << kCB];
+    const BinView& v = vs.v[blockIdx.y];
+    bin_hist<kPacked, kCB>(v.sorted_ids, v.trect, v.rect4_sorted, v.n_vis, tiles_x, pa, vs.hist[blockIdx.y], nbb,
+                           v.trect_sorted, blockIdx.x, h);
+}
+
+template <bool kPacked, int kCB>
+__global__ __launch_bounds__(kThreads) void k_bin_scatter_views(BinSortViews vs, int tiles_x, PassArgs pa,
+                                                                uint32_t nbb) {
+    __shared__ BinScatterLds<kCB> L;
+    const BinView& v = vs.v[blockIdx.y];
+    if (blockIdx.x * kBinBlock >= v.n_vis) return;
+    bin_scatter<kPacked, kCB>(v.sorted_ids, v.trect_sorted, v.rect4_sorted, v.n_vis, tiles_x, pa, vs.hist[blockIdx.y],
+                              vs.totals[blockIdx.y], nbb, v.tile_keys, v.tile_vals, blockIdx.x, L);
+}
+
 // Tile ranges from the tile-sorted keys: kRangeItems consecutive instances per
 // thread (four dwordx4 loads plus the two neighbours), a write at each tile
 // boundary only.  (One instance per thread meant 7K blocks per view at 1080p,
@@ -1349,6 +1627,47 @@ int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_
     return GSR_OK;
 }
 
+size_t bin_hist_elems(size_t n_vis, int tbits, int passes) {
+    if (tbits <= 0 || passes <= 0) return 0;
+    return ((n_vis + kBinBlock - 1) / kBinBlock) * ((size_t)1 << ((tbits + passes - 1) / passes));
+}
+
+int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted,
+                          uint32_t n_vis, int tiles_x, int tbits, int passes, uint32_t* hist, uint32_t* totals,
+                          uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s) {
+    if (n_vis == 0) return GSR_OK;
+    const int tb = tbits > 0 ? tbits : 1;  // one tile: a single digit value, generation order kept
+    const int ps = passes > 0 ? passes : 1;
+    const int w = (tb + ps - 1) / ps;
+    if (w > 11) return set_error(GSR_ERR_INVALID, "binning: tile digit wider than 11 bits");
+    const uint32_t nbb = (n_vis + kBinBlock - 1) / kBinBlock;
+    const PassArgs pa{nullptr, (uint32_t)tb, (uint32_t)ps, 0u};
+    const bool packed = rect4_sorted != nullptr;
+#define GSR_BIN_HIST(P, CB)                                                                                 \
+    k_bin_hist<P, CB><<<nbb, kThreads, 0, s>>>(sorted_ids, trect, rect4_sorted, n_vis, tiles_x, pa, hist, nbb, \
+                                               trect_sorted)
+#define GSR_BIN_SCATTER(P, CB)                                                                              \
+    k_bin_scatter<P, CB><<<nbb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tiles_x, pa, \
+                                                  hist, totals, nbb, tile_keys, tile_vals)
+    if (w <= 8) {
+        if (packed) GSR_BIN_HIST(true, 8); else GSR_BIN_HIST(false, 8);
+    } else {
+        if (packed) GSR_BIN_HIST(true, 11); else GSR_BIN_HIST(false, 11);
+    }
+    GSR_LAUNCH_CHECK("bin_hist");
+    int rc;
+    if ((rc = radix_offsets(hist, nbb, tb, ps, 0, totals, s))) return rc;
+    if (w <= 8) {
+        if (packed) GSR_BIN_SCATTER(true, 8); else GSR_BIN_SCATTER(false, 8);
+    } else {
+        if (packed) GSR_BIN_SCATTER(true, 11); else GSR_BIN_SCATTER(false, 11);
+    }
+    GSR_LAUNCH_CHECK("bin_scatter");
+#undef GSR_BIN_HIST
+#undef GSR_BIN_SCATTER
+    return GSR_OK;
+}
+
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, hipStream_t s) {
     if (n_dup == 0) return GSR_OK;
     const uint32_t per_block = kThreads * kRangeItems;
@@ -1480,6 +1799,49 @@ int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s) {
     else
         k_bin_write_views<false><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x, bin_stage_limit());
     GSR_LAUNCH_CHECK("bin_write_views");
+    return GSR_OK;
+}
+
+int launch_binning_sorted_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
+                                int tbits, int passes, hipStream_t s) {
+    BinSortViews bv{};
+    uint32_t nbb = 0;
+    for (int i = 0; i < k; ++i) {
+        const FinishView& f = views[i];
+        bv.v[i] = BinView{f.sorted_ids, f.trect, f.rect4_sorted, f.trect_sorted, f.bin_tmp, f.tile_keys, f.tile_vals,
+                          f.n_vis};
+        bv.hist[i] = hist[i];
+        bv.totals[i] = totals[i];
+        if ((f.rect4_sorted != nullptr) != (views[0].rect4_sorted != nullptr))
+            return set_error(GSR_ERR_INVALID, "binning: packed rectangles on some views only");
+        nbb = std::max(nbb, (f.n_vis + kBinBlock - 1) / kBinBlock);
+    }
+    if (nbb == 0) return GSR_OK;
+    const int tb = tbits > 0 ? tbits : 1;
+    const int ps = passes > 0 ? passes : 1;
+    const int w = (tb + ps - 1) / ps;
+    if (w > 11) return set_error(GSR_ERR_INVALID, "binning: tile digit wider than 11 bits");
+    const PassArgs pa{nullptr, (uint32_t)tb, (uint32_t)ps, 0u};
+    const bool packed = views[0].rect4_sorted != nullptr;
+    const dim3 grid(nbb, (unsigned)k);
+    if (w <= 8) {
+        if (packed) k_bin_hist_views<true, 8><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+        else k_bin_hist_views<false, 8><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+    } else {
+        if (packed) k_bin_hist_views<true, 11><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+        else k_bin_hist_views<false, 11><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+    }
+    GSR_LAUNCH_CHECK("bin_hist_views");
+    int rc;
+    if ((rc = radix_offsets_views(hist, totals, k, nbb, tb, ps, 0, s))) return rc;
+    if (w <= 8) {
+        if (packed) k_bin_scatter_views<true, 8><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+        else k_bin_scatter_views<false, 8><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+    } else {
+        if (packed) k_bin_scatter_views<true, 11><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+        else k_bin_scatter_views<false, 11><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+    }
+    GSR_LAUNCH_CHECK("bin_scatter_views");
     return GSR_OK;
 }
 

@@ -185,6 +185,55 @@ __device__ __forceinline__ uint32_t block_exclusive(uint32_t v, uint32_t* lds_wa
     return woff + inc - v;
 }
 
+// ---------------------------------------------------------------- radix digits
+// One pass of the LSD radix sort (radix_sort.hip; also the tile sort's pass 0
+// fused into the binning, composite.hip).
+struct PassArgs {
+    const uint32_t* key_range;  // device {~kmin, kmax} or null (then kmin = 0 and B = bits)
+    uint32_t bits;
+    uint32_t passes;
+    uint32_t pass;
+};
+
+struct Digit {
+    uint32_t kmin, shift, w, mask;
+    __device__ __forceinline__ uint32_t of(uint32_t key) const { return ((key - kmin) >> shift) & mask; }
+};
+
+__device__ __forceinline__ Digit digit_params(const PassArgs& p) {
+    Digit d;
+    uint32_t B;
+    if (p.key_range) {
+        d.kmin = ~p.key_range[0];
+        const uint32_t kmax = p.key_range[1];
+        B = kmax > d.kmin ? 32u - (uint32_t)__clz(kmax - d.kmin) : 0u;
+    } else {
+        d.kmin = 0u;
+        B = p.bits;
+    }
+    d.w = max(1u, (B + p.passes - 1u) / p.passes);
+    d.shift = p.pass * d.w;
+    d.mask = (1u << d.w) - 1u;
+    return d;
+}
+
+// Lanes of the wave holding the same w-bit digit (only `valid` lanes).
+// Per digit bit: the ballot m, then each lane keeps the lanes that agree with
+// it: p &= ~(m ^ t), t = the lane's bit as 0 / all ones (a sign-extended bit
+// field; one 3-input bit op per 32-bit half: 4 VALU per bit, against 8 for
+// `p &= bit ? m : ~m` as the compiler emitted it).
+__device__ __forceinline__ uint64_t match_digit(uint32_t digit, uint32_t w, bool valid) {
+    const uint64_t v = __ballot(valid);
+    uint32_t plo = (uint32_t)v, phi = (uint32_t)(v >> 32);
+    for (uint32_t b = 0; b < w; ++b) {
+        const uint32_t t = (uint32_t)__builtin_amdgcn_sbfe((int)digit, (int)b, 1);
+        const uint64_t m = __ballot(t != 0u);
+        plo &= ~((uint32_t)m ^ t);
+        phi &= ~((uint32_t)(m >> 32) ^ t);
+    }
+    return ((uint64_t)phi << 32) | plo;
+}
+
 // ---------------------------------------------------------------- host launchers
 // scan.hip: exclusive scan of n uint32 (in may equal out). Writes the total to
 // *total_dev (device) when non-null. tmp must hold scan_tmp_elems(n) uint32.
@@ -225,7 +274,15 @@ struct RadixViewArgs {
     uint32_t** pay_alt = nullptr;
 };
 int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
-                           hipStream_t s);
+                           hipStream_t s, int first_pass = 0);
+// Pass p's digit offsets from a digit-major count matrix hist[d * ntiles + tile]
+// produced by another kernel (the tile sort's pass 0 counted by the binning):
+// exclusive per-digit prefix over tiles in place, digit totals to `totals`.
+int radix_offsets(uint32_t* hist, uint32_t ntiles, int bits, int passes, int pass, uint32_t* totals,
+                  hipStream_t s);
+// The same for k views (hist[v], totals[v]; each view's ntiles rows).
+int radix_offsets_views(uint32_t* const* hist, uint32_t* const* totals, int k, uint32_t ntiles, int bits,
+                        int passes, int pass, hipStream_t s);
 size_t radix_tmp_elems(size_t n);
 size_t radix_totals_elems();
 int radix_passes_for(int bits);
@@ -233,7 +290,7 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
                      uint32_t** vals_alt, bool identity_vals, size_t n, const uint32_t* n_dev,
                      int bits, int passes, const uint32_t* key_range, uint32_t* tmp,
                      uint32_t* totals, hipStream_t s, const uint2* rect_in = nullptr,
-                     uint32_t** pay_io = nullptr, uint32_t** pay_alt = nullptr);
+                     uint32_t** pay_io = nullptr, uint32_t** pay_alt = nullptr, int first_pass = 0);
 // Payload (rect_in non-null): the tile rectangles rect_in[n] (uint2, in the
 // input order) travel with the pairs packed to 32 bits (pack_rect: frames of
 // at most 256 x 256 tiles); the sorted packed rectangles end in *pay_io.
@@ -312,6 +369,16 @@ int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_
                    hipStream_t s);
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
                        hipStream_t s);
+// The binning with the tile sort's first radix pass fused in (composite.hip,
+// k_bin_hist / k_bin_scatter): the instances end in (tile_keys, tile_vals)
+// ordered by digit 0 of the tile sort (tbits bits in `passes` passes); the
+// sort then continues from pass 1 (radix_sort_pairs first_pass = 1).  hist
+// holds bin_hist_elems(n_vis, tbits, passes) uint32, totals
+// radix_totals_elems().  tbits = 0 (one tile): generation order.
+size_t bin_hist_elems(size_t n_vis, int tbits, int passes);
+int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted,
+                          uint32_t n_vis, int tiles_x, int tbits, int passes, uint32_t* hist, uint32_t* totals,
+                          uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s);
 // chunk_cnt must hold chunk_cnt_elems(num_tiles) entries (block totals after the tiles);
 // order: one entry per chunk (dispatch position -> chunk slot)
 size_t chunk_cnt_elems(int num_tiles);
@@ -364,6 +431,9 @@ struct FinishView {
 };
 // binning: bin_tmp of each view holds its per-block instance counts
 int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s);
+// ... and with the tile sort's pass 0 fused in (hist[v], totals[v] per view)
+int launch_binning_sorted_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
+                                int tbits, int passes, hipStream_t s);
 int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s);
 // first_major: every tile's first chunk dispatched before any later chunk
 int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, uint32_t classes, bool first_major,

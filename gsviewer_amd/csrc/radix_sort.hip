@@ -63,54 +63,8 @@ constexpr int radix_cap() { return 1 << kCB; }
 template <int kCB>
 constexpr int digits_per_thread() { return radix_cap<kCB>() / kThreads; }
 
-struct PassArgs {
-    const uint32_t* key_range;  // device {~kmin, kmax} or null (then kmin = 0 and B = bits)
-    uint32_t bits;
-    uint32_t passes;
-    uint32_t pass;
-};
-
-struct Digit {
-    uint32_t kmin, shift, w, mask;
-    __device__ __forceinline__ uint32_t of(uint32_t key) const { return ((key - kmin) >> shift) & mask; }
-};
-
-__device__ __forceinline__ Digit digit_params(const PassArgs& p) {
-    Digit d;
-    uint32_t B;
-    if (p.key_range) {
-        d.kmin = ~p.key_range[0];
-        const uint32_t kmax = p.key_range[1];
-        B = kmax > d.kmin ? 32u - (uint32_t)__clz(kmax - d.kmin) : 0u;
-    } else {
-        d.kmin = 0u;
-        B = p.bits;
-    }
-    d.w = max(1u, (B + p.passes - 1u) / p.passes);
-    d.shift = p.pass * d.w;
-    d.mask = (1u << d.w) - 1u;
-    return d;
-}
-
 __device__ __forceinline__ uint32_t count_of(const uint32_t* n_dev, uint32_t n_host) {
     return n_dev ? min(n_host, n_dev[0]) : n_host;
-}
-
-// Lanes of the wave holding the same w-bit digit (only `valid` lanes).
-// Per digit bit: the ballot m, then each lane keeps the lanes that agree with
-// it: p &= ~(m ^ t), t = the lane's bit as 0 / all ones (a sign-extended bit
-// field; one 3-input bit op per 32-bit half: 4 VALU per bit, against 8 for
-// `p &= bit ? m : ~m` as the compiler emitted it).
-__device__ __forceinline__ uint64_t match_digit(uint32_t digit, uint32_t w, bool valid) {
-    const uint64_t v = __ballot(valid);
-    uint32_t plo = (uint32_t)v, phi = (uint32_t)(v >> 32);
-    for (uint32_t b = 0; b < w; ++b) {
-        const uint32_t t = (uint32_t)__builtin_amdgcn_sbfe((int)digit, (int)b, 1);
-        const uint64_t m = __ballot(t != 0u);
-        plo &= ~((uint32_t)m ^ t);
-        phi &= ~((uint32_t)(m >> 32) ^ t);
-    }
-    return ((uint64_t)phi << 32) | plo;
 }
 
 // Per-tile digit counts: one LDS histogram per block, counted with LDS atomics
@@ -426,13 +380,13 @@ template <int kR, int kCB>
 static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
                        bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
                        const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s,
-                       const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt) {
+                       const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt, int first_pass) {
     constexpr int kTileItems = kThreads * kR;
     const uint32_t nt = (uint32_t)((n + kTileItems - 1) / kTileItems);
     // upper bound of the radix over the passes (device-chosen widths never exceed it)
     const uint32_t radix_max = 1u << ((bits + passes - 1) / passes);
     bool ident = identity_vals;
-    for (int p = 0; p < passes; ++p) {
+    for (int p = first_pass; p < passes; ++p) {
         const PassArgs pa{key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p};
         k_rs_upsweep<kR, kCB><<<nt, kThreads, 0, s>>>(*keys_io, n_dev, (uint32_t)n, pa, tmp, nt);
         GSR_LAUNCH_CHECK("rs_upsweep");
@@ -440,7 +394,7 @@ static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_a
         GSR_LAUNCH_CHECK("rs_offsets");
         if (rect_in) {
             k_rs_scatter<kR, true, kCB><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev,
-                                                           (uint32_t)n, pa, tmp, totals, nt, p == 0 ? rect_in : nullptr,
+                                                           (uint32_t)n, pa, tmp, totals, nt, p == first_pass ? rect_in : nullptr,
                                                            *pay_io, *pay_alt);
         } else {
             k_rs_scatter<kR, false, kCB><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev,
@@ -460,18 +414,18 @@ static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_a
 
 template <int kR, int kCB>
 static int sort_passes_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
-                             hipStream_t s) {
+                             hipStream_t s, int first_pass) {
     constexpr int kTileItems = kThreads * kR;
     const uint32_t nt = (uint32_t)((n + kTileItems - 1) / kTileItems);
     const uint32_t radix_max = 1u << ((bits + passes - 1) / passes);
     bool ident = identity_vals;
-    for (int p = 0; p < passes; ++p) {
+    for (int p = first_pass; p < passes; ++p) {
         SortViews sv{};
         for (int v = 0; v < k; ++v) {
             RadixViewArgs& a = views[v];
             sv.v[v] = SortView{*a.keys_io, *a.vals_io, *a.keys_alt, *a.vals_alt, a.n_dev, a.tmp, a.totals,
                                PassArgs{a.key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p},
-                               p == 0 ? a.rect_in : nullptr, a.rect_in ? *a.pay_io : nullptr,
+                               p == first_pass ? a.rect_in : nullptr, a.rect_in ? *a.pay_io : nullptr,
                                a.rect_in ? *a.pay_alt : nullptr};
         }
         const bool pay = views[0].rect_in != nullptr;  // all views or none (radix_sort_pairs_views)
@@ -497,9 +451,39 @@ static int sort_passes_views(RadixViewArgs* views, int k, bool identity_vals, si
     return GSR_OK;
 }
 
+int radix_offsets(uint32_t* hist, uint32_t ntiles, int bits, int passes, int pass, uint32_t* totals,
+                  hipStream_t s) {
+    if (ntiles == 0 || passes == 0) return GSR_OK;
+    if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
+        return set_error(GSR_ERR_INVALID, "radix offsets: digit width out of range");
+    const uint32_t radix_max = 1u << ((bits + passes - 1) / passes);
+    const PassArgs pa{nullptr, (uint32_t)bits, (uint32_t)passes, (uint32_t)pass};
+    k_rs_offsets<<<(radix_max + kOffWaves - 1) / kOffWaves, 64 * kOffWaves, 0, s>>>(hist, ntiles, pa, totals);
+    GSR_LAUNCH_CHECK("rs_offsets");
+    return GSR_OK;
+}
+
+int radix_offsets_views(uint32_t* const* hist, uint32_t* const* totals, int k, uint32_t ntiles, int bits,
+                        int passes, int pass, hipStream_t s) {
+    if (ntiles == 0 || passes == 0) return GSR_OK;
+    if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "radix offsets: view count out of range");
+    if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
+        return set_error(GSR_ERR_INVALID, "radix offsets: digit width out of range");
+    const uint32_t radix_max = 1u << ((bits + passes - 1) / passes);
+    SortViews sv{};
+    for (int v = 0; v < k; ++v) {
+        sv.v[v].hist = hist[v];
+        sv.v[v].totals = totals[v];
+        sv.v[v].pa = PassArgs{nullptr, (uint32_t)bits, (uint32_t)passes, (uint32_t)pass};
+    }
+    k_rs_offsets_views<<<dim3((radix_max + kOffWaves - 1) / kOffWaves, k), 64 * kOffWaves, 0, s>>>(sv, ntiles);
+    GSR_LAUNCH_CHECK("rs_offsets_views");
+    return GSR_OK;
+}
+
 int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
-                           hipStream_t s) {
-    if (n == 0 || passes == 0) return GSR_OK;
+                           hipStream_t s, int first_pass) {
+    if (n == 0 || passes == 0 || first_pass >= passes) return GSR_OK;
     if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "radix sort: view count out of range");
     if (n > 0xffffffffull - 4 * kMinTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
     if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
@@ -508,16 +492,17 @@ int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size
         if ((views[v].rect_in != nullptr) != (views[0].rect_in != nullptr))
             return set_error(GSR_ERR_INVALID, "radix sort: payload on some views only");
     if ((bits + passes - 1) / passes <= 8)
-        return views[0].key_range ? sort_passes_views<kRDepth, 8>(views, k, identity_vals, n, bits, passes, s)
-                                  : sort_passes_views<kRTile, 8>(views, k, identity_vals, n, bits, passes, s);
-    return sort_passes_views<kRWide, kMaxBits>(views, k, identity_vals, n, bits, passes, s);
+        return views[0].key_range
+                   ? sort_passes_views<kRDepth, 8>(views, k, identity_vals, n, bits, passes, s, first_pass)
+                   : sort_passes_views<kRTile, 8>(views, k, identity_vals, n, bits, passes, s, first_pass);
+    return sort_passes_views<kRWide, kMaxBits>(views, k, identity_vals, n, bits, passes, s, first_pass);
 }
 
 int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
                      bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
                      const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s,
-                     const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt) {
-    if (n == 0 || passes == 0) return GSR_OK;
+                     const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt, int first_pass) {
+    if (n == 0 || passes == 0 || first_pass >= passes) return GSR_OK;
     if (n > 0xffffffffull - 4 * kMinTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
     if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
         return set_error(GSR_ERR_INVALID, "radix sort: digit width out of range");
@@ -526,12 +511,12 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
     if ((bits + passes - 1) / passes <= 8) {
         if (key_range)
             return sort_passes<kRDepth, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
-                                     key_range, tmp, totals, s, rect_in, pay_io, pay_alt);
+                                     key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass);
         return sort_passes<kRTile, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
-                                  key_range, tmp, totals, s, rect_in, pay_io, pay_alt);
+                                  key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass);
     }
     return sort_passes<kRWide, kMaxBits>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
-                                         key_range, tmp, totals, s, rect_in, pay_io, pay_alt);
+                                         key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass);
 }
 
 }  // namespace gsr

@@ -1,0 +1,54 @@
+"""The binning with the tile sort's first radix pass fused in
+(GSR_BIN_FUSED=1, the default: k_bin_hist + k_bin_scatter) gives the same
+frames as the separate binning and full tile sort (k_bin_reduce +
+k_bin_write, then every radix pass).  It is integer index work, so images,
+tile lists and tile ranges must be bit-identical, on a frame rendered alone (gsr_render) and on a group of
+views (gsr_render_finish_views), for frame sizes whose tile ids take one
+radix pass (<= 2048 tiles) and two, plus the full-size C2 frame."""
+import numpy as np
+import pytest
+
+from gsviewer_amd.camera import Camera
+from gsviewer_amd.gaussian_data import garden_standin
+from helpers import batched_frames, gpu_frame
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = [{}, {"GSR_BIN_FUSED": "0"}]
+
+
+def _settings(**kw):
+    from gsviewer_amd.rasterizer import RenderSettings
+    return RenderSettings(**kw)
+
+
+def _frames(monkeypatch, env, g, scene, cams):
+    monkeypatch.delenv("GSR_BIN_FUSED", raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    alone = gpu_frame(g, cams[0], _settings(), with_debug=True)
+    group = batched_frames(scene, cams, _settings(), group=len(cams), debug_views=(0,))
+    return alone, group
+
+
+@pytest.mark.parametrize("h,w,n", [(360, 640, 60_000), (720, 1280, 200_000), (1080, 1920, 1_000_000)])
+def test_stage_variants_identical(gpu, monkeypatch, h, w, n):
+    from gsviewer_amd.rasterizer import HipScene
+    g = garden_standin(n, seed=1, sh_degree=0 if n < 1_000_000 else 3)
+    scene = HipScene.from_gaussian_data(g)
+    cams = [Camera(h, w).yaw(45.0 * v) for v in range(3)]
+    ref = None
+    for env in VARIANTS:
+        alone, group = _frames(monkeypatch, env, g, scene, cams)
+        got = (alone, group)
+        if ref is None:
+            ref = got
+            assert alone["stats"]["n_instances"] > 0
+            continue
+        for a, b in ((ref[0], alone), (ref[1][0], group[0])):
+            for key in ("tile_list", "ranges", "depth_order"):
+                np.testing.assert_array_equal(a[key], b[key], err_msg=f"{env} {key}")
+            np.testing.assert_array_equal(a["image"], b["image"], err_msg=f"{env} image")
+        for v in range(1, len(cams)):
+            np.testing.assert_array_equal(ref[1][v]["image"], group[v]["image"], err_msg=f"{env} view {v}")
+    scene.close()
