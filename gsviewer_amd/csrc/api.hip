@@ -305,8 +305,9 @@ int bits_for(uint32_t v) {  // bits needed to represent values < v
 // Per-frame scratch block: [0,4) counters {V, D, extra chunks, -} are
 // overwritten every frame; from `cleared` on, the depth-key range
 // {~kmin, kmax}, the radix digit totals (depth sort, tile sort), the tile
-// ranges (uint2, 16-B aligned) and the saturation words (4 per tile) are
-// zeroed by k_cull.
+// ranges (uint2, 16-B aligned), the saturation words (4 per tile) and the
+// chunk completion counters of the tail merge (1 per tile, right after the
+// saturation words) are zeroed by k_cull.
 struct ZeroLayout {
     size_t counters = 0, cleared = 4, key_range = 4, totals_depth = 8, totals_tile = 0, ranges = 0, sat = 0,
            total = 0;
@@ -315,7 +316,7 @@ struct ZeroLayout {
         totals_tile = totals_depth + tot;
         ranges = (totals_tile + tot + 3) & ~(size_t)3;
         sat = ranges + 2 * (size_t)num_tiles;
-        total = sat + 4 * (size_t)num_tiles;
+        total = sat + 5 * (size_t)num_tiles;
     }
 };
 

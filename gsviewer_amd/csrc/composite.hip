@@ -562,11 +562,13 @@ struct CompositeArgs {
     float t_min;
     float bg[3];
     int out_layout;
+    int tail_merge;  // a multi-chunk tile's last chunk to finish folds the tile (no merge launch)
 };
 
 constexpr int kBatch = 64;  // records staged per wave per LDS batch
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // kFragGauss keep test in two VALU ops, with no compare and lane-mask select
 // (whose VCC hand-off also costs an s_nop on gfx950).  With m = -mid > 0 and
@@ -920,7 +922,8 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                                                 const uint32_t* __restrict__ list,
                                                 const SplatRec* __restrict__ recs, const CompositeArgs& a,
                                                 float* __restrict__ out, float4* __restrict__ partial,
-                                                uint32_t* __restrict__ sat, float4* __restrict__ tmax) {
+                                                uint32_t* __restrict__ sat, float4* __restrict__ tmax,
+                                                const uint32_t* __restrict__ chunk_base) {
     const int tile = (int)d.x;
     const uint32_t begin = d.y, end = d.z;
     const uint32_t nchunks = d.w >> 16;
@@ -1174,11 +1177,67 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
     }
 #endif
     if (nchunks > 1) {
-        // partial (C, T) per pixel, folded by k_merge; layout [slot][k][lane]
+        // partial (C, T) per pixel, folded by k_merge or by the tile's last
+        // chunk to finish (tail merge); layout [slot][k][lane]
         float4* p = partial + (size_t)slot * 256;
+        if (!a.tail_merge) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) p[k * 64 + lane] = make_float4(rg[k].x, rg[k].y, bt[k].x, bt[k].y);
-        return;
+            for (int k = 0; k < 4; ++k) p[k * 64 + lane] = make_float4(rg[k].x, rg[k].y, bt[k].x, bt[k].y);
+            return;
+        }
+        // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the
+        // partials are stored `sc1` (16-B vector stores that write through
+        // past the XCD's L2, so no release fence: an agent release writes back
+        // the whole L2's dirty lines, and thousands of them serialised the
+        // launch), the wave waits for them, then one agent-scope add to the
+        // tile's counter (zeroed by k_cull every frame).  The wave whose add
+        // returns nchunks - 1 is the last: after an agent-scope acquire it
+        // reads every other chunk's partial and folds the tile in chunk order.
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const f32x4 v = f32x4{rg[k].x, rg[k].y, bt[k].x, bt[k].y};
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p + k * 64 + lane), "v"(v) : "memory");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t old = 0;
+        if (lane == 0)
+            old = __hip_atomic_fetch_add(sat + 4 * (size_t)a.num_tiles + tile, 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+        old = (uint32_t)__builtin_amdgcn_readlane((int)old, 0);
+        if (old != nchunks - 1u) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t cbase = kk > 0 ? slot - kk + 1 : chunk_base[tile];  // slot of chunk c >= 1: cbase + c - 1
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            // chunks past the first one to saturate the slice add < t_min: k_merge's bound
+            const uint32_t last = min(nchunks - 1u, 0xffffffffu - ld_relaxed(sat + (size_t)tile * 4 + k));
+            float r = 0.f, g = 0.f, b = 0.f, T = 1.f;
+            for (uint32_t c0 = 0; c0 <= last; c0 += 8) {
+                float4 v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t c = c0 + j;
+                    if (c > last) {
+                        v[j] = make_float4(0.f, 0.f, 0.f, 1.f);
+                    } else if (c == kk) {
+                        v[j] = make_float4(rg[k].x, rg[k].y, bt[k].x, bt[k].y);
+                    } else {
+                        const uint32_t cs = c == 0 ? (uint32_t)tile : cbase + c - 1;
+                        v[j] = partial[(size_t)cs * 256 + k * 64 + lane];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    r += T * v[j].x;
+                    g += T * v[j].y;
+                    b += T * v[j].z;
+                    T *= v[j].w;
+                }
+            }
+            rg[k] = f32x2{r, g};
+            bt[k] = f32x2{b, T};
+        }
     }
     if (x >= a.width) return;
     const size_t plane = (size_t)a.width * a.height;
@@ -1227,7 +1286,8 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
                                                         const uint32_t* __restrict__ list,
                                                         const SplatRec* __restrict__ recs, CompositeArgs a,
                                                         float* __restrict__ out, float4* __restrict__ partial,
-                                                        uint32_t* __restrict__ sat, float4* __restrict__ tmax) {
+                                                        uint32_t* __restrict__ sat, float4* __restrict__ tmax,
+                                                        const uint32_t* __restrict__ chunk_base) {
     __shared__ float4 lds[kCompWaves][kBatch * 3];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t pos = blockIdx.x * kCompWaves + wave;
@@ -1237,7 +1297,7 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const uint4 d = desc[slot];
-    composite_chunk<FRAG>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax);
+    composite_chunk<FRAG>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax, chunk_base);
 #ifdef GSR_COMP_TRACE
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if (__lane_id() == 0 && slot < kTraceMax) {
@@ -1267,6 +1327,7 @@ struct CompView {
     float4* partial;
     uint32_t* sat;
     float4* tmax;
+    const uint32_t* chunk_base;
 };
 struct CompViews {
     CompView v[kMaxViews];
@@ -1320,7 +1381,7 @@ __device__ __forceinline__ void composite_views_wave(const CompViews& vs, const 
     if (pos >= (uint32_t)a.num_tiles + v.n_chunks_dev[0]) return;
     const uint32_t slot = v.order[pos];
     const uint4 d = v.desc[slot];
-    composite_chunk<FRAG>(d, slot, lds, v.list, v.recs, a, v.out, v.partial, v.sat, v.tmax);
+    composite_chunk<FRAG>(d, slot, lds, v.list, v.recs, a, v.out, v.partial, v.sat, v.tmax, v.chunk_base);
 }
 
 template <int FRAG>
@@ -1676,7 +1737,21 @@ int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
     return GSR_OK;
 }
 
-static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float* bg, int out_layout) {
+// Multi-chunk tiles folded by their last chunk inside the compositing launch.
+// A group's frames (3072-instance chunks: few multi-chunk tiles) do it by
+// default, which drops one launch per group (GSR_TAIL_MERGE=0: k_merge_views).
+// A frame alone (192-instance chunks: ~2500 multi-chunk tiles at C2) keeps
+// k_merge: a deep tile's last chunk folding ~40 partials alone put the fold on
+// the launch's tail, composite 120 -> 170 us (profiles/r3_s9); its four waves
+// per tile in k_merge take 15 (GSR_TAIL_MERGE_ALONE=1 to A/B).
+bool env_flag(const char* name, bool dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::strtol(e, nullptr, 10) != 0 : dflt;
+}
+bool tail_merge_on(bool group) { return group ? env_flag("GSR_TAIL_MERGE", true) : env_flag("GSR_TAIL_MERGE_ALONE", false); }
+
+static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float* bg, int out_layout,
+                               bool group = false) {
     CompositeArgs a;
     a.width = u.width;
     a.height = u.height;
@@ -1687,6 +1762,7 @@ static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float*
     a.bg[1] = bg[1];
     a.bg[2] = bg[2];
     a.out_layout = out_layout;
+    a.tail_merge = tail_merge_on(group) ? 1 : 0;
     return a;
 }
 
@@ -1727,19 +1803,19 @@ int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n
     switch (frag_class) {
         case kFragGauss:
             k_composite<kFragGauss><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial, sat,
-                                                              tmax);
+                                                              tmax, chunk_base);
             break;
         case kFragBillboard:
             k_composite<kFragBillboard><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
-                                                                  sat, tmax);
+                                                                  sat, tmax, chunk_base);
             break;
         case kFragFlatBall:
             k_composite<kFragFlatBall><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
-                                                                 sat, tmax);
+                                                                 sat, tmax, chunk_base);
             break;
         default:
             k_composite<kFragGaussBall><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
-                                                                  sat, tmax);
+                                                                  sat, tmax, chunk_base);
             break;
     }
     GSR_LAUNCH_CHECK("composite");
@@ -1768,6 +1844,7 @@ int launch_composite_unorm8(const uint2* ranges, const uint32_t* tile_list, cons
 int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const float4* partial, const uint32_t* sat,
                  const FrameUniforms& u, float t_min, const float* bg, int out_layout, float* out, hipStream_t s) {
     const CompositeArgs a = make_args(u, t_min, bg, out_layout);
+    if (a.tail_merge) return GSR_OK;  // the compositing launch folded its multi-chunk tiles
     k_merge<<<(unsigned)a.num_tiles, kMergeThreads, 0, s>>>(chunk_cnt, chunk_base, partial, sat, a, out);
     GSR_LAUNCH_CHECK("merge");
     return GSR_OK;
@@ -1885,12 +1962,12 @@ int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk,
 int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32_t classes, bool first_major,
                            bool interleave, const FrameUniforms& u, int frag_class, float t_min, const float* bg,
                            int out_layout, hipStream_t s, uint64_t* stamps) {
-    const CompositeArgs a = make_args(u, t_min, bg, out_layout);
+    const CompositeArgs a = make_args(u, t_min, bg, out_layout, true);
     CompViews cv{};
     for (int i = 0; i < k; ++i) {
         const FinishView& f = views[i];
         cv.v[i] = CompView{f.desc, f.order, f.n_extra_dev, chunk_class_totals(f.chunk_cnt, a.num_tiles, classes),
-                           f.tile_vals, f.recs, f.out, f.partial, f.sat, f.tmax};
+                           f.tile_vals, f.recs, f.out, f.partial, f.sat, f.tmax, f.chunk_base};
     }
     cv.k = (uint32_t)k;
     cv.classes = classes + (first_major ? 1u : 0u);  // first-major: the later chunks as one more class
@@ -1914,7 +1991,8 @@ size_t composite_views_blocks(uint32_t max_chunks, int k) {
 
 int launch_merge_views(FinishView* views, int k, const FrameUniforms& u, float t_min, const float* bg,
                        int out_layout, hipStream_t s) {
-    const CompositeArgs a = make_args(u, t_min, bg, out_layout);
+    const CompositeArgs a = make_args(u, t_min, bg, out_layout, true);
+    if (a.tail_merge) return GSR_OK;  // the compositing launch folded its multi-chunk tiles
     MergeViews mv{};
     for (int i = 0; i < k; ++i) {
         const FinishView& f = views[i];

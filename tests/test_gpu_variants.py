@@ -1,8 +1,15 @@
-"""The binning with the tile sort's first radix pass fused in
-(GSR_BIN_FUSED=1, the default: k_bin_hist + k_bin_scatter) gives the same
-frames as the separate binning and full tile sort (k_bin_reduce +
-k_bin_write, then every radix pass).  It is integer index work, so images,
-tile lists and tile ranges must be bit-identical, on a frame rendered alone (gsr_render) and on a group of
+"""The pipeline's alternative stage forms give identical frames:
+
+* GSR_BIN_FUSED (default 1): the binning with the tile sort's first radix
+  pass fused in (k_bin_hist + k_bin_scatter) against the separate binning and
+  full tile sort (k_bin_reduce + k_bin_write, then every radix pass): integer
+  index work;
+* GSR_TAIL_MERGE (groups, default 1) / GSR_TAIL_MERGE_ALONE (a frame alone,
+  default 0): a multi-chunk tile folded by its last chunk to finish, inside
+  the compositing launch, against the k_merge launch: the same fold in the
+  same chunk order.
+
+Images, tile lists and tile ranges must be bit-identical, on a frame rendered alone (gsr_render) and on a group of
 views (gsr_render_finish_views), for frame sizes whose tile ids take one
 radix pass (<= 2048 tiles) and two, plus the full-size C2 frame."""
 import numpy as np
@@ -14,7 +21,7 @@ from helpers import batched_frames, gpu_frame
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [{}, {"GSR_BIN_FUSED": "0"}]
+VARIANTS = [{}, {"GSR_BIN_FUSED": "0"}, {"GSR_TAIL_MERGE": "0", "GSR_TAIL_MERGE_ALONE": "1"}]
 
 
 def _settings(**kw):
@@ -23,7 +30,8 @@ def _settings(**kw):
 
 
 def _frames(monkeypatch, env, g, scene, cams):
-    monkeypatch.delenv("GSR_BIN_FUSED", raising=False)
+    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE"):
+        monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     alone = gpu_frame(g, cams[0], _settings(), with_debug=True)
