@@ -563,6 +563,7 @@ struct CompositeArgs {
     float bg[3];
     int out_layout;
     int tail_merge;  // a multi-chunk tile's last chunk to finish folds the tile (no merge launch)
+    uint32_t pos_begin, pos_end;  // k_composite: the dispatch positions [pos_begin, pos_end) of this launch
 };
 
 constexpr int kBatch = 64;  // records staged per wave per LDS batch
@@ -1290,8 +1291,8 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
                                                         const uint32_t* __restrict__ chunk_base) {
     __shared__ float4 lds[kCompWaves][kBatch * 3];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t pos = blockIdx.x * kCompWaves + wave;
-    if (pos >= (uint32_t)a.num_tiles + n_chunks_dev[0]) return;  // device count of extra chunks
+    const uint32_t pos = a.pos_begin + blockIdx.x * kCompWaves + wave;
+    if (pos >= min(a.pos_end, (uint32_t)a.num_tiles + n_chunks_dev[0])) return;  // device count of extra chunks
     const uint32_t slot = order[pos];
 #ifdef GSR_COMP_TRACE
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
@@ -1763,6 +1764,8 @@ static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float*
     a.bg[2] = bg[2];
     a.out_layout = out_layout;
     a.tail_merge = tail_merge_on(group) ? 1 : 0;
+    a.pos_begin = 0u;
+    a.pos_end = 0xffffffffu;
     return a;
 }
 
@@ -1797,9 +1800,13 @@ int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n
                      const uint32_t* chunk_cnt,
                      const uint32_t* chunk_base, uint32_t* sat, const uint32_t* tile_vals, const SplatRec* recs,
                      const FrameUniforms& u, int frag_class, float t_min, const float* bg, int out_layout, float* out,
-                     float4* partial, float4* tmax, hipStream_t s) {
-    const CompositeArgs a = make_args(u, t_min, bg, out_layout);
-    const unsigned grid = (unsigned)((max_chunks + kCompWaves - 1) / kCompWaves);
+                     float4* partial, float4* tmax, hipStream_t s, uint32_t pos_begin, uint32_t pos_end) {
+    CompositeArgs a = make_args(u, t_min, bg, out_layout);
+    a.pos_begin = pos_begin;
+    a.pos_end = pos_end;
+    const uint32_t last = std::min(max_chunks, pos_end);
+    if (last <= pos_begin) return GSR_OK;
+    const unsigned grid = (unsigned)((last - pos_begin + kCompWaves - 1) / kCompWaves);
     switch (frag_class) {
         case kFragGauss:
             k_composite<kFragGauss><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial, sat,

@@ -393,7 +393,8 @@ int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n
                      const uint32_t* chunk_cnt, const uint32_t* chunk_base, uint32_t* sat,
                      const uint32_t* tile_vals, const SplatRec* recs, const FrameUniforms& u,
                      int frag_class, float t_min, const float* bg, int out_layout, float* out,
-                     float4* partial, float4* tmax, hipStream_t s);
+                     float4* partial, float4* tmax, hipStream_t s, uint32_t pos_begin = 0,
+                     uint32_t pos_end = 0xffffffffu);
 // GSR_BLEND_UNORM8: one wave per tile, back to front, 8-bit rounding after every blend
 int launch_composite_unorm8(const uint2* ranges, const uint32_t* tile_list, const SplatRec* recs,
                             const FrameUniforms& u, int frag_class, const float* bg, int out_layout, float* out,

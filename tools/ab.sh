@@ -1,8 +1,9 @@
 #!/bin/bash
 # A/B the bench across variants on one box, interleaved to spread drift:
 #   bash tools/ab.sh TAG ROUNDS VARIANT [VARIANT ...] [-- extra bench.py args]
-# A VARIANT is "-" (the tree as is) or space-separated environment settings,
-# e.g. "GSR_FIRST_MAJOR_ALONE=1" or "GSR_LIB_PATH=build/variant.so GSR_CHUNK=128".
+# A VARIANT is "-" (the tree as is) or space-separated environment settings
+# and bench.py flags, e.g. "GSR_FIRST_MAJOR_ALONE=1", "GSR_LIB_PATH=varlib/x.so
+# GSR_CHUNK=128" or "--inflight 20 --share 10".
 # Each run: python bench.py --no-cpu-baseline (+ extra args) under its own time
 # limit; results in gpurun_out/TAG/<variant index>_<round>.json and one summary
 # line per run on stdout.  The first failing run ends the script.
@@ -22,9 +23,15 @@ for r in $(seq 1 "$ROUNDS"); do
     for i in "${!VARIANTS[@]}"; do
         v=${VARIANTS[$i]}
         envs=()
-        [ "$v" != "-" ] && read -r -a envs <<< "$v"
+        args=()
+        if [ "$v" != "-" ]; then
+            read -r -a toks <<< "$v"
+            for t in "${toks[@]}"; do
+                if [[ "$t" == --* ]] || [ ${#args[@]} -gt 0 ]; then args+=("$t"); else envs+=("$t"); fi
+            done
+        fi
         out=$O/${i}_$r.json
-        timeout -k 10 240 env "${envs[@]}" python bench.py --no-cpu-baseline $EXTRA > $out 2> $O/${i}_$r.err
+        timeout -k 10 240 env "${envs[@]}" python bench.py --no-cpu-baseline $EXTRA "${args[@]}" > $out 2> $O/${i}_$r.err
         rc=$?
         if [ $rc -ne 0 ]; then
             echo "[ab] variant $i ($v) round $r FAILED rc=$rc"
