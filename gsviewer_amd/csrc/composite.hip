@@ -1071,6 +1071,63 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                 }
             st_records += 1;
 #endif
+#ifdef GSR_COMP_DENSE
+            if (FRAG == kFragGauss) {
+                // Dense evaluation (an experiment build, profiles/r3_s13): the
+                // record's covered pixels of the tile are packed onto the wave's
+                // lanes, one evaluation per 64 of them instead of one 64-lane
+                // evaluation per touched 16x4 slice, and each alpha is handed to
+                // the lane that owns its pixel by ds_bpermute.  The falloff, keep
+                // test and blend are the expressions below, so the alphas and
+                // the image are the same bit for bit.  The record's rectangle
+                // terms are wave-uniform (scalar registers).
+                const uint32_t cov = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(q0.w));
+                const uint32_t covx = cov & 0xffffu, covy = cov >> 16;
+                const int x0 = (int)__builtin_ctz(covx), x1 = 31 - (int)__builtin_clz(covx);
+                const int y0 = (int)__builtin_ctz(covy), y1 = 31 - (int)__builtin_clz(covy);
+                const int rw = x1 - x0 + 1, rh = y1 - y0 + 1;
+                const int cnt = rw * rh;
+                const float inv_w = __builtin_amdgcn_rcpf((float)rw);
+                const float mid = q1.w;
+                const float km = -mid * kKeepScaleWide;
+                const f32x2 c_rg = f32x2{q2.x, q2.y};
+                const f32x2 c_bt = f32x2{q2.z, q2.w};
+                // this lane's pixel of slice k sits at rect index lidx + (4k - y0) rw (if covered)
+                const uint32_t cc = (uint32_t)(lcol - x0);
+                const bool col_in = cc < (uint32_t)rw;
+                const int lidx = lrow * rw + (int)cc;
+                const float pxe0 = (float)(col_base + x0) + 0.5f;
+                const float pye0 = (float)(a.height - 1 - (row_base + y0)) + 0.5f;
+                for (int e0 = 0; e0 < cnt; e0 += 64) {
+                    const int qq = e0 + lane;
+                    const int row = (int)(((float)qq + 0.5f) * inv_w);  // exact: qq < 256, rw <= 16
+                    const int col = qq - row * rw;
+                    const float dx = (pxe0 + (float)col) - q0.x;
+                    const float p0 = fmaf(q1.x * dx, dx, -mid);
+                    const float p1 = q1.y * dx;
+                    const float dy = (pye0 - (float)row) - q0.y;
+                    const float pw = (q1.z * dy + p1) * dy + p0;
+                    const float ee = __builtin_amdgcn_exp2f(pw);
+                    const float a1 = __builtin_amdgcn_fmed3f(q0.z * ee, 0.f, 1.f);
+                    const float al = __builtin_amdgcn_fmed3f(fmaf(-kKeepScale, fabsf(pw), km), 0.f, a1);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (!((sb[k] >> j) & 1ull)) continue;
+                        const int rk = 4 * k - y0;                       // uniform
+                        const uint32_t r = (uint32_t)(lrow + rk);        // row within the rect
+                        const uint32_t src = (uint32_t)(lidx + rk * rw - e0);
+                        const bool mine = col_in & (r < (uint32_t)rh) & (src < 64u);
+                        const float ak =
+                            __int_as_float(__builtin_amdgcn_ds_bpermute((int)(src << 2), __float_as_int(al)));
+                        const float wgt = (mine ? ak : 0.f) * bt[k].y;
+                        const f32x2 ww = f32x2{wgt, wgt};
+                        rg[k] = __builtin_elementwise_fma(c_rg, ww, rg[k]);
+                        bt[k] = __builtin_elementwise_fma(c_bt, ww, bt[k]);
+                    }
+                }
+                continue;
+            }
+#endif
             // lane coverage: bit 4k = this lane's pixel of slice k is inside the splat's quad
             // (all-zero when the column is not: bfe_i32 gives 0 or ~0)
             const uint32_t cov = __float_as_uint(q0.w);
