@@ -213,6 +213,25 @@ def pmc_counters(kernel, args):
     return {r[1]: float(r[4]) for r in rows if r[0].strip('"') == kernel}, f"profiles/{d}/pmc_summary.csv ({kernel})"
 
 
+def rocprof_avg_ms(kernel, args):
+    """Average duration (ms) of `kernel` in the committed rocprofv3 --stats
+    summary of this same bench command (profiles/<LATEST>/kernel_stats.csv),
+    the cross-check of the live launch time."""
+    if args.config != "c2" or args.n or args.width or args.height or args.box != "none":
+        return None
+    import csv
+    try:
+        d = open(PMC_PROFILE).read().strip()
+        with open(os.path.join(ROOT, "profiles", d, "kernel_stats.csv")) as fh:
+            for row in csv.DictReader(fh):
+                if kernel in row["Name"]:
+                    return {"ms": float(row["AverageNs"]) * 1e-6, "calls": int(row["Calls"]),
+                            "source": f"profiles/{d}/kernel_stats.csv"}
+    except (OSError, KeyError, ValueError):
+        return None
+    return None
+
+
 def pmc_traffic(kernel, args):
     """HBM bytes per launch (FETCH_SIZE + WRITE_SIZE) of `kernel`."""
     got, src = pmc_counters(kernel, args)
@@ -652,6 +671,7 @@ def main():
                          "traffic": gt[0] if gt else None, "traffic_per_view": gt[0] / vpl if gt else None,
                          "traffic_source": gt[1] if gt else None,
                          "event_ms_per_launch": group_comp["event_ms_per_launch"],
+                         "rocprof": rocprof_avg_ms("k_composite_views<0>", args),
                          "timing": f"in-kernel span of every k_composite_views launch (first block start to last "
                                    f"wave end, s_memrealtime), {group_comp['launches']} launches over a repeat of the "
                                    f"timed pipeline ({group_comp['instrumented_ms_per_frame']:.4f} ms/frame "
