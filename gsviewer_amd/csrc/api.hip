@@ -165,6 +165,7 @@ struct gsr_context {
     bool first_major = true;                      // ... every tile's first chunk before any later one
     bool first_major_alone = false;               // the same for a frame finished alone (gsr_render_finish)
     bool bin_fused = true;                        // the tile sort's pass 0 fused into the binning (k_bin_scatter)
+    bool fused_cull = true;                       // culling inside the preprocess (launch_preprocess_fc)
     int depth_passes_alone = kDepthPassesAlone;   // depth sort passes of gsr_render's frames
     int depth_passes_now = 0;                     // this frame's (0: kDepthPasses)
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
@@ -326,11 +327,13 @@ struct ZeroLayout {
 int ensure_scene_buffers(gsr_context* c, size_t n) {
     const size_t nw = (n + 63) / 64 + 4;
     int rc;
-    if ((rc = c->vis_mask.ensure(nw, "vis_mask"))) return rc;
-    if ((rc = c->wave_counts.ensure(nw, "wave_counts"))) return rc;
-    if ((rc = c->block_ranges.ensure(n / kCullBlock + 1, "block_ranges"))) return rc;
-    const size_t scan_need = std::max(scan_tmp_elems(nw), scan_tmp_elems(n));
-    if ((rc = c->scan_tmp.ensure(scan_need, "scan_tmp"))) return rc;
+    if (!c->fused_cull) {  // the separate cull's visibility masks and compaction scan
+        if ((rc = c->vis_mask.ensure(nw, "vis_mask"))) return rc;
+        if ((rc = c->wave_counts.ensure(nw, "wave_counts"))) return rc;
+        if ((rc = c->block_ranges.ensure(n / kCullBlock + 1, "block_ranges"))) return rc;
+        const size_t scan_need = std::max(scan_tmp_elems(nw), scan_tmp_elems(n));
+        if ((rc = c->scan_tmp.ensure(scan_need, "scan_tmp"))) return rc;
+    }
     if ((rc = c->recs.ensure(n, "recs"))) return rc;
     if ((rc = c->keys_a.ensure(n, "keys"))) return rc;
     if ((rc = c->keys_b.ensure(n, "keys"))) return rc;
@@ -342,7 +345,7 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
     if ((rc = c->rect4_b.ensure(n, "rect4"))) return rc;
     if ((rc = c->bin_tmp.ensure(bin_tmp_elems(n), "bin_tmp"))) return rc;
     if ((rc = c->radix_tmp.ensure(radix_tmp_elems(n), "radix_tmp"))) return rc;
-    if ((rc = c->done_ctr.ensure(1, "done_ctr"))) return rc;
+    if ((rc = c->done_ctr.ensure(kDoneCtrWords, "done_ctr"))) return rc;
     if (c->has_arena && c->arena.measure) return GSR_OK;  // gsr_workspace_size: sizes only, no HIP call
     if (!c->host_counters) {
         if (hipHostMalloc(&c->host_counters, 4 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
@@ -366,7 +369,7 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
 // context's next frame begins.
 int arm_done_ctr(gsr_context* c, hipStream_t s) {
     if (c->done_armed) return GSR_OK;
-    GSR_HIP_CHECK(hipMemsetAsync(c->done_ctr.p, 0, sizeof(unsigned long long), s));
+    GSR_HIP_CHECK(hipMemsetAsync(c->done_ctr.p, 0, kDoneCtrWords * sizeof(unsigned long long), s));
     c->done_armed = true;
     return GSR_OK;
 }
@@ -443,7 +446,8 @@ int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const 
     if (f.n == 0) return GSR_OK;
     return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32,
                             c->depth_passes_now ? c->depth_passes_now : kDepthPasses, key_range,
-                            c->radix_tmp.p, totals, s, f.packed ? c->trect.p : nullptr, &f.pa, &f.pb);
+                            c->radix_tmp.p, totals, s, f.packed ? c->trect.p : nullptr, &f.pa, &f.pb, 0,
+                            c->fused_cull);
 }
 
 // Wait until the last preprocess block has stored this frame's (V, D, seq) to
@@ -676,6 +680,7 @@ int gsr_context_create(gsr_context** out) {
     }
     if (const char* e = std::getenv("GSR_FIRST_MAJOR")) (*out)->first_major = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_BIN_FUSED")) (*out)->bin_fused = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("GSR_FUSED_CULL")) (*out)->fused_cull = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_FIRST_MAJOR_ALONE"))
         (*out)->first_major_alone = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_VIEWS_INTERLEAVE")) (*out)->views_interleave = std::strtol(e, nullptr, 10) != 0;
@@ -818,7 +823,14 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
 
     if ((rc = prof_record(c, slot, EV_START, s))) return rc;
     if (n == 0) GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * zl.total, s));
-    if (n > 0) {
+    if (n > 0 && c->fused_cull) {
+        // one launch: cull, preprocess, V / D / key range, and the zero block's clearing
+        if ((rc = prof_record(c, slot, EV_CULL, s))) return rc;
+        if ((rc = launch_preprocess_fc(sc->d, u, c->recs.p, c->keys_a.p, c->trect.p, counters, c->zero.p + zl.key_range,
+                                       c->zero.p + zl.ranges, (uint32_t)(zl.total - zl.ranges), c->done_ctr.p,
+                                       c->host_counters_dev, ++c->seq, radii, s)))
+            return rc;
+    } else if (n > 0) {
         const size_t nw = (n + 63) / 64;
         // k_cull clears the tile ranges and saturation words; every other word
         // of the zero block is overwritten (not accumulated) before it is read
@@ -830,8 +842,8 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
                                  c->block_ranges.p, (n + kCullBlock - 1) / kCullBlock, c->zero.p + zl.key_range)))
             return rc;
     }
-    if ((rc = prof_record(c, slot, EV_CULL, s))) return rc;
-    if (n > 0 && (rc = launch_preprocess(sc->d, u, c->vis_mask.p, c->wave_counts.p, counters + 0, c->recs.p,
+    if (!(n > 0 && c->fused_cull) && (rc = prof_record(c, slot, EV_CULL, s))) return rc;
+    if (n > 0 && !c->fused_cull && (rc = launch_preprocess(sc->d, u, c->vis_mask.p, c->wave_counts.p, counters + 0, c->recs.p,
                                          c->keys_a.p, c->trect.p, counters, c->done_ctr.p, c->host_counters_dev,
                                          ++c->seq, radii, s)))
         return rc;
@@ -876,6 +888,11 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
     FrameUniforms u[GSR_MAX_VIEWS];
     ViewCullArgs cull[GSR_MAX_VIEWS];
     ViewPreArgs pre[GSR_MAX_VIEWS];
+    ViewPreFcArgs pfc[GSR_MAX_VIEWS];
+    const bool fc = ctxs[0]->fused_cull;
+    for (int v = 1; v < k; ++v)
+        if (ctxs[v]->fused_cull != fc)
+            return set_error(GSR_ERR_INVALID, "render_begin_views: contexts differ in the cull mode (GSR_FUSED_CULL)");
     int rc;
     for (int v = 0; v < k; ++v) {
         gsr_context* c = ctxs[v];
@@ -900,6 +917,9 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
         pre[v] = ViewPreArgs{&u[v], c->vis_mask.p, c->wave_counts.p, counters + 0, c->recs.p, c->keys_a.p,
                              c->trect.p, counters, c->done_ctr.p, c->host_counters_dev, radii ? radii[v] : nullptr,
                              ++c->seq};
+        pfc[v] = ViewPreFcArgs{&u[v], c->recs.p, c->keys_a.p, c->trect.p, counters, c->zero.p + zl.key_range,
+                               c->zero.p + zl.ranges, c->done_ctr.p, c->host_counters_dev,
+                               radii ? radii[v] : nullptr, (uint32_t)(zl.total - zl.ranges), c->seq};
         PendingFrame& f = c->pend;
         f.u = u[v];
         f.t_min = st->t_min;
@@ -911,7 +931,9 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
         f.slot = (int)(c->frame_idx & 1);
         c->host_ms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
     }
-    if (n > 0) {
+    if (n > 0 && fc) {
+        if ((rc = launch_preprocess_fc_views(sc->d, pfc, k, s))) return rc;
+    } else if (n > 0) {
         if ((rc = launch_cull_views(sc->d, cull, k, s))) return rc;
         const size_t nw = (n + 63) / 64;
         const size_t n_kr = (n + kCullBlock - 1) / kCullBlock;
@@ -984,7 +1006,7 @@ int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream) {
             return set_error(GSR_ERR_INVALID, "render_begin_sorts: views differ in frame size");
         views[v] = RadixViewArgs{&f.ka, &f.va, &f.kb, &f.vb, c->zero.p + zl.counters, c->zero.p + zl.key_range,
                                  c->radix_tmp.p, c->zero.p + zl.totals_depth, f.packed ? c->trect.p : nullptr,
-                                 &f.pa, &f.pb};
+                                 &f.pa, &f.pb, c->fused_cull};
     }
     int rc;
     if (n > 0 && (rc = radix_sort_pairs_views(views, k, true, n, 32, kDepthPasses, s))) return rc;
@@ -1353,7 +1375,11 @@ int64_t gsr_debug_copy(const gsr_context* c, int32_t what, void* dst, int64_t ma
     const void* src = nullptr;
     int64_t bytes = 0;
     switch (what) {
-        case GSR_DEBUG_RECORDS: src = c->recs.p; bytes = c->stats.n_visible * (int64_t)sizeof(SplatRec); break;
+        case GSR_DEBUG_RECORDS:  // the fused cull's slots are not compacted: all n (slot n-1-i)
+            src = c->recs.p;
+            bytes = (c->fused_cull && c->stats.n_visible > 0 ? c->stats.n_gaussians : c->stats.n_visible) *
+                    (int64_t)sizeof(SplatRec);
+            break;
         case GSR_DEBUG_DEPTH_ORDER: src = c->last_depth_order; bytes = c->stats.n_visible * 4; break;
         case GSR_DEBUG_TILE_RANGES: src = c->last_ranges; bytes = c->last_tiles * 8; break;
         case GSR_DEBUG_TILE_LIST: src = c->last_tile_list; bytes = c->stats.n_instances * 4; break;

@@ -193,11 +193,17 @@ struct PassArgs {
     uint32_t bits;
     uint32_t passes;
     uint32_t pass;
+    // the first pass over the fused cull's slots (launch_preprocess_fc): all n
+    // keys are read (not the device count) and keys outside {kmin, kmax}
+    // (culled slots, key 0xffffffff) are dropped; later passes see only V
+    uint32_t drop = 0;
 };
 
 struct Digit {
     uint32_t kmin, shift, w, mask;
+    uint32_t lim;  // kept keys: key - kmin <= lim (PassArgs::drop)
     __device__ __forceinline__ uint32_t of(uint32_t key) const { return ((key - kmin) >> shift) & mask; }
+    __device__ __forceinline__ bool keep(uint32_t key) const { return key - kmin <= lim; }
 };
 
 __device__ __forceinline__ Digit digit_params(const PassArgs& p) {
@@ -207,8 +213,12 @@ __device__ __forceinline__ Digit digit_params(const PassArgs& p) {
         d.kmin = ~p.key_range[0];
         const uint32_t kmax = p.key_range[1];
         B = kmax > d.kmin ? 32u - (uint32_t)__clz(kmax - d.kmin) : 0u;
+        // an empty range ({0, 0}: nothing visible) keeps no key: every slot is then culled (0xffffffff)
+        d.lim = kmax >= d.kmin ? kmax - d.kmin : 0xfffffffeu;
+        if (kmax < d.kmin) d.kmin = 0u;
     } else {
         d.kmin = 0u;
+        d.lim = 0xffffffffu;
         B = p.bits;
     }
     d.w = max(1u, (B + p.passes - 1u) / p.passes);
@@ -272,6 +282,7 @@ struct RadixViewArgs {
     const uint2* rect_in = nullptr;  // payload (see radix_sort_pairs): on every view or none
     uint32_t** pay_io = nullptr;
     uint32_t** pay_alt = nullptr;
+    bool drop_first = false;  // see radix_sort_pairs
 };
 int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
                            hipStream_t s, int first_pass = 0);
@@ -290,7 +301,11 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
                      uint32_t** vals_alt, bool identity_vals, size_t n, const uint32_t* n_dev,
                      int bits, int passes, const uint32_t* key_range, uint32_t* tmp,
                      uint32_t* totals, hipStream_t s, const uint2* rect_in = nullptr,
-                     uint32_t** pay_io = nullptr, uint32_t** pay_alt = nullptr, int first_pass = 0);
+                     uint32_t** pay_io = nullptr, uint32_t** pay_alt = nullptr, int first_pass = 0,
+                     bool drop_first = false);
+// drop_first (needs key_range): the keys are the fused cull's n slots; the
+// first pass reads all n and drops the culled ones (PassArgs::drop), later
+// passes run over the device count n_dev = V.
 // Payload (rect_in non-null): the tile rectangles rect_in[n] (uint2, in the
 // input order) travel with the pairs packed to 32 bits (pack_rect: frames of
 // at most 256 x 256 tiles); the sorted packed rectangles end in *pay_io.
@@ -358,6 +373,33 @@ struct ViewPreArgs {
 };
 int launch_cull_views(const SceneData& sd, const ViewCullArgs* views, int k, hipStream_t s);
 int launch_preprocess_views(const SceneData& sd, const ViewPreArgs* views, int k, hipStream_t s);
+
+// Culling fused into the preprocess (no k_cull, no scan): Gaussian i owns
+// slot n-1-i (a culled slot: key 0xffffffff, empty rect); the last block
+// writes counters[0] = V, counters[1] = D and key_range {~kmin, kmax} of the
+// visible keys, publishes (V, D, seq) to host_counters and re-arms done_ctr
+// (kDoneCtrWords words: completion, then key-range and count shards).
+// Every block also clears zero_words[0, n_zero) (sc1 stores).
+constexpr size_t kDoneCtrWords = 1 + 3 * 64;
+int launch_preprocess_fc(const SceneData& sd, const FrameUniforms& u, SplatRec* recs, uint32_t* depth_keys,
+                         uint2* trect, uint32_t* counters, uint32_t* key_range, uint32_t* zero_words, uint32_t n_zero,
+                         unsigned long long* done_ctr, uint32_t* host_counters, uint32_t seq, int32_t* radii,
+                         hipStream_t s);
+struct ViewPreFcArgs {
+    const FrameUniforms* u;
+    SplatRec* recs;
+    uint32_t* depth_keys;
+    uint2* trect;
+    uint32_t* counters;
+    uint32_t* key_range;
+    uint32_t* zero_words;
+    unsigned long long* done_ctr;
+    uint32_t* host_counters;
+    int32_t* radii;
+    uint32_t n_zero;
+    uint32_t seq;
+};
+int launch_preprocess_fc_views(const SceneData& sd, const ViewPreFcArgs* views, int k, hipStream_t s);
 
 // composite.hip
 size_t bin_tmp_elems(size_t n_vis);

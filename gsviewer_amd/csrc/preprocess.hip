@@ -406,7 +406,8 @@ template <int DEG>
 __device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, const Cov3& S3, const FrameUniforms& u,
                                                        uint64_t m, int64_t i, uint32_t slot_base,
                                                        SplatRec* __restrict__ recs, uint32_t* __restrict__ depth_keys,
-                                                       uint2* __restrict__ trect, int32_t* __restrict__ radii);
+                                                       uint2* __restrict__ trect, int32_t* __restrict__ radii,
+                                                       uint32_t& key);
 
 // Per-Gaussian body of k_preprocess for a visible lane; returns the number of
 // 16x16 tiles its covered pixel rectangle touches.
@@ -425,7 +426,8 @@ __device__ __forceinline__ uint32_t preprocess_one(const float4* __restrict__ po
     // otherwise wait for pos/rot/scale before issuing the SH planes: two
     // dependent memory round trips per wave instead of one)
     __builtin_amdgcn_sched_barrier(0);
-    return preprocess_compute<DEG>(g, cov3d(g.q1, g.sc4, u), u, m, i, slot_base, recs, depth_keys, trect, radii);
+    uint32_t key;
+    return preprocess_compute<DEG>(g, cov3d(g.q1, g.sc4, u), u, m, i, slot_base, recs, depth_keys, trect, radii, key);
 }
 
 // Everything after the loads: the vertex stage of one view for a visible lane
@@ -434,7 +436,8 @@ template <int DEG>
 __device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, const Cov3& S3, const FrameUniforms& u,
                                                        uint64_t m, int64_t i, uint32_t slot_base,
                                                        SplatRec* __restrict__ recs, uint32_t* __restrict__ depth_keys,
-                                                       uint2* __restrict__ trect, int32_t* __restrict__ radii) {
+                                                       uint2* __restrict__ trect, int32_t* __restrict__ radii,
+                                                       uint32_t& key) {
     const float4 po = g.po;
     const float x = po.x, y = po.y, z = po.z;
     const Projected pr = project(x, y, z, u);
@@ -552,7 +555,8 @@ __device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, 
     dst[0] = make_float4(rec.cx, rec.cy, rec.opacity, __uint_as_float(rec.xspan));
     dst[1] = make_float4(rec.qa, rec.qb, rec.qc, __uint_as_float(rec.yspan));
     dst[2] = make_float4(rec.r, rec.g, rec.b, rec.mid);
-    depth_keys[slot] = float_order_key(-pr.pv[2]);
+    key = float_order_key(-pr.pv[2]);
+    depth_keys[slot] = key;
     if (radii) {
         const float rr = ceilf(fmaxf(qs[0], qs[1]));
         radii[i] = (rr >= 0.f && rr < 2147483520.f) ? (int32_t)rr : 0;
@@ -678,7 +682,9 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_views(const
             uint32_t tiles = 0;
             if ((m >> lane) & 1ull) {
                 const uint32_t slot_base = V.n_vis_dev[0] - 1u - V.wave_off[i >> 6];
-                tiles = preprocess_compute<DEG>(g, S3, V.u, m, i, slot_base, V.recs, V.depth_keys, V.trect, V.radii);
+                uint32_t key;
+                tiles = preprocess_compute<DEG>(g, S3, V.u, m, i, slot_base, V.recs, V.depth_keys, V.trect, V.radii,
+                                                key);
             } else if (i < n && V.radii) {
                 V.radii[i] = 0;
             }
@@ -701,6 +707,212 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_views(const
             __hip_atomic_store(V.done_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+
+// ------------------------------------------------------------ culling fused in
+// The frame in one launch, without k_cull and the scan (GSR_FUSED_CULL): each
+// lane projects its Gaussian itself and loads the rest of the scene data only
+// when it is visible.  Slots are not compacted: Gaussian i owns slot n-1-i in
+// recs / depth_keys / trect (the same descending-index order as the compacted
+// slots, so the stable depth sort still resolves ties front to back), and a
+// culled slot holds the key 0xffffffff and an empty rectangle; the depth
+// sort's first pass runs over all n slots and drops every key outside the
+// frame's key range (PassArgs::drop), later passes see only the V visible.
+// Per frame, beside the completion word done_ctr[0] (blocks << 40 | D), in
+// 64 shards (block b updates shard b mod 64: at most 16 blocks per address
+// instead of the whole grid; a single word under 1024 blocks' atomics cost
+// ~9 us of the frame):
+//   done_ctr[kKeyShards0 + s]         (seq << 32) | kmax
+//   done_ctr[kKeyShards0 + 64 + s]    (seq << 32) | ~kmin
+//   done_ctr[kKeyShards0 + 128 + s]   the shard's visible count
+// The key shards are tagged with the frame's sequence number, so they never
+// need clearing: a frame's first max replaces any older frame's entry.  The
+// block completing the grid reduces all of them with one wave, publishes as
+// before, and zeroes the count shards and the completion word.  (Completion
+// counted in two levels, per shard then per grid, measured no faster.)
+constexpr int kKeyShards = 64;
+constexpr int kKeyShards0 = 1;
+
+// The rest of Gaussian i's data (its position is already loaded).
+template <int DEG>
+__device__ __forceinline__ void load_attrs(GaussLoad<DEG>& g, const float4 po, const float4* __restrict__ rot,
+                                           const float4* __restrict__ scale, const float4* __restrict__ sh, int64_t n,
+                                           int64_t i) {
+    g.po = po;
+    g.q1 = rot[i];
+    g.sc4 = scale[i];
+#pragma unroll
+    for (int p = 0; p < 12; ++p) {
+        if (p < sh_planes_for<DEG>()) {
+            const float4 t = load_plane(sh, n, p, i);
+            g.f[4 * p + 0] = t.x;
+            g.f[4 * p + 1] = t.y;
+            g.f[4 * p + 2] = t.z;
+            g.f[4 * p + 3] = t.w;
+        } else {
+            g.f[4 * p + 0] = g.f[4 * p + 1] = g.f[4 * p + 2] = g.f[4 * p + 3] = 0.f;
+        }
+    }
+}
+
+__device__ __forceinline__ void culled_slot(uint32_t slot, uint32_t* __restrict__ depth_keys,
+                                            uint2* __restrict__ trect) {
+    depth_keys[slot] = 0xffffffffu;
+    trect[slot] = make_uint2(0xffffu, 0u);
+}
+
+// One frame's block results: counts and the key range of its visible
+// Gaussians.  Thread 0 only; returns true in the block that completed the grid.
+__device__ __forceinline__ bool block_done(unsigned long long* __restrict__ done_ctr, uint32_t seq, uint32_t tiles,
+                                           uint32_t nvis, uint32_t kmax, uint32_t nkmin, uint32_t& n_dup) {
+    if (nvis) {
+        const int sh = kKeyShards0 + (int)(blockIdx.x % kKeyShards);
+        const unsigned long long tag = (unsigned long long)seq << 32;
+        const unsigned long long r0 =
+            __hip_atomic_fetch_max(done_ctr + sh, tag | kmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long r1 =
+            __hip_atomic_fetch_max(done_ctr + sh + kKeyShards, tag | nkmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long r2 = __hip_atomic_fetch_add(done_ctr + sh + 2 * kKeyShards, (unsigned long long)nvis,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // Returned (so performed at the coherence point, where device-scope
+        // atomics act) before the completion add below is issued: the block
+        // that completes the grid sees every block's contributions, with no
+        // cache write-back.  (The asm consumes the results: the atomics stay
+        // the returning kind, and the compiler waits for them here.)
+        asm volatile("" ::"v"(r0), "v"(r1), "v"(r2) : "memory");
+    }
+    const unsigned long long old = atomicAdd(done_ctr, (1ull << 40) | (unsigned long long)tiles);
+    n_dup = (uint32_t)(old & ((1ull << 40) - 1)) + tiles;
+    return (old >> 40) == (unsigned long long)(gridDim.x - 1);
+}
+
+// The completing block's publication, by one whole wave: the frame's key
+// range from the shards, V and D to the device counters and (V, D, seq) to
+// host-mapped memory; the counters are re-armed for the next frame.
+__device__ __forceinline__ void publish_frame(unsigned long long* __restrict__ done_ctr, uint32_t seq, uint32_t n_dup,
+                                              uint32_t* __restrict__ key_range, uint32_t* __restrict__ counters,
+                                              uint32_t* __restrict__ host_counters) {
+    const int lane = __lane_id();
+    const unsigned long long a =
+        __hip_atomic_load(done_ctr + kKeyShards0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long b =
+        __hip_atomic_load(done_ctr + kKeyShards0 + kKeyShards + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long c =
+        __hip_atomic_load(done_ctr + kKeyShards0 + 2 * kKeyShards + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t kmax = wave_reduce_max((uint32_t)(a >> 32) == seq ? (uint32_t)a : 0u);
+    const uint32_t nkmin = wave_reduce_max((uint32_t)(b >> 32) == seq ? (uint32_t)b : 0u);
+    const uint32_t n_vis = wave_reduce_sum((uint32_t)c);
+    __hip_atomic_store(done_ctr + kKeyShards0 + 2 * kKeyShards + lane, 0ull, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) {
+        key_range[0] = nkmin;  // {0, 0} when nothing is visible, like the scan's
+        key_range[1] = kmax;
+        counters[0] = n_vis;
+        counters[1] = n_dup;
+        __hip_atomic_store(host_counters + 0, n_vis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_counters + 1, n_dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_counters + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(done_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// One launch for the views of a group (k = 1: a frame alone): a position is
+// projected for every view and the rest of the Gaussian loaded once when any
+// view sees it.  (A separate one-view kernel with the uniforms as a plain
+// kernel argument needed 164 VGPRs at DEG 3 against 119 here: the compiler
+// hoisted every uniform out of the grid-stride loop and, out of SGPRs, kept
+// them in VGPRs; indexed by the runtime view they are re-read each iteration.)
+struct ViewPreFc {
+    FrameUniforms u;
+    SplatRec* recs;
+    uint32_t* depth_keys;
+    uint2* trect;
+    uint32_t* counters;
+    uint32_t* key_range;
+    uint32_t* zero_words;
+    unsigned long long* done_ctr;
+    uint32_t* host_counters;
+    int32_t* radii;
+    uint32_t n_zero;
+    uint32_t seq;
+};
+struct ViewsPreFc {
+    ViewPreFc v[kMaxViews];
+    int32_t k;
+};
+static_assert(sizeof(ViewsPreFc) <= 3584, "kernel argument size");
+
+template <int DEG>
+__global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_fc_views(const float4* __restrict__ pos_op,
+                                                                              const float4* __restrict__ rot,
+                                                                              const float4* __restrict__ scale,
+                                                                              const float4* __restrict__ sh,
+                                                                              int64_t n, ViewsPreFc vs) {
+    static_assert(kMaxViews * 4 * (kThreads / 64) <= kThreads, "one thread per LDS word");
+    __shared__ uint32_t s_red[kMaxViews][4][kThreads / 64];
+    __shared__ uint32_t s_last[kMaxViews], s_dup[kMaxViews];
+    const int wave = threadIdx.x >> 6;
+    const int lane = __lane_id();
+    for (int v = 0; v < vs.k; ++v) clear_words(vs.v[v].zero_words, vs.v[v].n_zero);
+    if (threadIdx.x < kMaxViews * 4 * (kThreads / 64)) (&s_red[0][0][0])[threadIdx.x] = 0u;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * kThreads;
+    const int64_t first = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    float4 pnext = first < n ? pos_op[first] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = first; i - threadIdx.x < n; i += stride) {
+        const float4 p = pnext;
+        pnext = i + stride < n ? pos_op[i + stride] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const bool in = i < n;
+        uint32_t vm = 0;  // the views that see Gaussian i
+#pragma unroll 1
+        for (int v = 0; v < vs.k; ++v)
+            if (in && project(p.x, p.y, p.z, vs.v[v].u).vis) vm |= 1u << v;
+        GaussLoad<DEG> g;
+        Cov3 S3;
+        if (vm) {
+            load_attrs<DEG>(g, p, rot, scale, sh, n, i);
+            S3 = cov3d(g.q1, g.sc4, vs.v[0].u);  // (the group shares rot_modifier and the scale factor)
+        }
+        const uint32_t slot = (uint32_t)(n - 1 - i);
+#pragma unroll 1
+        for (int v = 0; v < vs.k; ++v) {
+            const ViewPreFc& V = vs.v[v];
+            uint32_t tiles = 0, key = 0;
+            const bool vis = (vm >> v) & 1u;
+            if (vis) {
+                tiles =
+                    preprocess_compute<DEG>(g, S3, V.u, 0ull, i, slot, V.recs, V.depth_keys, V.trect, V.radii, key);
+            } else if (in) {
+                culled_slot(slot, V.depth_keys, V.trect);
+                if (V.radii) V.radii[i] = 0;
+            }
+            const uint32_t a = wave_reduce_sum(tiles);
+            const uint32_t b = (uint32_t)__popcll(__ballot(vis));
+            const uint32_t c = wave_reduce_max(vis ? key : 0u), d = wave_reduce_max(vis ? ~key : 0u);
+            if (lane == 0) {
+                s_red[v][0][wave] += a;
+                s_red[v][1][wave] += b;
+                s_red[v][2][wave] = max(s_red[v][2][wave], c);
+                s_red[v][3][wave] = max(s_red[v][3][wave], d);
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)vs.k) {  // one thread per view: the block's results
+        const int v = threadIdx.x;
+        uint32_t t = 0, nv = 0, kx = 0, kn = 0;
+#pragma unroll
+        for (int w = 0; w < kThreads / 64; ++w)
+            t += s_red[v][0][w], nv += s_red[v][1][w], kx = max(kx, s_red[v][2][w]), kn = max(kn, s_red[v][3][w]);
+        uint32_t n_dup;
+        s_last[v] = block_done(vs.v[v].done_ctr, vs.v[v].seq, t, nv, kx, kn, n_dup) ? 1u : 0u;
+        s_dup[v] = n_dup;
+    }
+    __syncthreads();
+    for (int v = wave; v < vs.k; v += kThreads / 64)
+        if (s_last[v])
+            publish_frame(vs.v[v].done_ctr, vs.v[v].seq, s_dup[v], vs.v[v].key_range, vs.v[v].counters,
+                          vs.v[v].host_counters);
 }
 
 __global__ __launch_bounds__(kThreads) void k_depth_keys_all(const float4* __restrict__ pos_op, int64_t n, float v8,
@@ -798,6 +1010,43 @@ int launch_preprocess_views(const SceneData& sd, const ViewPreArgs* views, int k
     }
 #undef GSR_PREV
     GSR_LAUNCH_CHECK("preprocess_views");
+    return GSR_OK;
+}
+
+static_assert(kDoneCtrWords >= (size_t)(kKeyShards0 + 3 * kKeyShards), "completion words");
+
+int launch_preprocess_fc(const SceneData& sd, const FrameUniforms& u, SplatRec* recs, uint32_t* depth_keys,
+                         uint2* trect, uint32_t* counters, uint32_t* key_range, uint32_t* zero_words, uint32_t n_zero,
+                         unsigned long long* done_ctr, uint32_t* host_counters, uint32_t seq, int32_t* radii,
+                         hipStream_t s) {
+    const ViewPreFcArgs a{&u, recs, depth_keys, trect, counters, key_range, zero_words, done_ctr, host_counters, radii,
+                          n_zero, seq};
+    return launch_preprocess_fc_views(sd, &a, 1, s);
+}
+
+int launch_preprocess_fc_views(const SceneData& sd, const ViewPreFcArgs* views, int k, hipStream_t s) {
+    if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "preprocess_views: view count out of range");
+    if ((uint64_t)sd.n > 0xffffffffull) return set_error(GSR_ERR_OVERFLOW, "preprocess: too many Gaussians");
+    ViewsPreFc vp{};
+    vp.k = k;
+    const int deg = effective_deg(*views[0].u);
+    for (int v = 0; v < k; ++v) {
+        const ViewPreFcArgs& a = views[v];
+        if (effective_deg(*a.u) != deg) return set_error(GSR_ERR_INVALID, "preprocess_views: views differ in SH degree");
+        vp.v[v] = ViewPreFc{*a.u,         a.recs,      a.depth_keys, a.trect,         a.counters, a.key_range,
+                            a.zero_words, a.done_ctr,  a.host_counters, a.radii,      a.n_zero,   a.seq};
+    }
+    const unsigned grid = preprocess_grid(sd.n);
+#define GSR_PREV(D) k_preprocess_fc_views<D><<<grid, kThreads, 0, s>>>(sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, vp)
+    switch (deg) {
+        case -1: GSR_PREV(-1); break;
+        case 0: GSR_PREV(0); break;
+        case 1: GSR_PREV(1); break;
+        case 2: GSR_PREV(2); break;
+        default: GSR_PREV(3); break;
+    }
+#undef GSR_PREV
+    GSR_LAUNCH_CHECK("preprocess_fc_views");
     return GSR_OK;
 }
 

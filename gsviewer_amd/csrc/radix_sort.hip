@@ -63,8 +63,8 @@ constexpr int radix_cap() { return 1 << kCB; }
 template <int kCB>
 constexpr int digits_per_thread() { return radix_cap<kCB>() / kThreads; }
 
-__device__ __forceinline__ uint32_t count_of(const uint32_t* n_dev, uint32_t n_host) {
-    return n_dev ? min(n_host, n_dev[0]) : n_host;
+__device__ __forceinline__ uint32_t count_of(const uint32_t* n_dev, uint32_t n_host, const PassArgs& pa) {
+    return n_dev && !pa.drop ? min(n_host, n_dev[0]) : n_host;
 }
 
 // Per-tile digit counts: one LDS histogram per block, counted with LDS atomics
@@ -80,7 +80,7 @@ __device__ __forceinline__ void rs_upsweep(const uint32_t* __restrict__ keys, co
     __shared__ uint32_t h[kCap];
     const Digit dg = digit_params(pa);
     const uint32_t radix = dg.mask + 1u;
-    const uint32_t n = count_of(n_dev, n_host);
+    const uint32_t n = count_of(n_dev, n_host, pa);
     const uint32_t tile0 = tile * kTileItems;
 #pragma unroll
     for (int i = 0; i < (kCap + kThreads - 1) / kThreads; ++i)
@@ -97,7 +97,7 @@ __device__ __forceinline__ void rs_upsweep(const uint32_t* __restrict__ keys, co
     if (tile0 < n) {
 #pragma unroll
         for (int r = 0; r < kR; ++r)
-            if (base + r * 64 < n) atomicAdd(&h[dg.of(k[r])], 1u);
+            if (base + r * 64 < n && (!pa.drop || dg.keep(k[r]))) atomicAdd(&h[dg.of(k[r])], 1u);
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < radix; d += kThreads) hist[(size_t)d * ntiles + tile] = h[d];
@@ -196,7 +196,7 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
     __shared__ uint32_t dbase[kCap];              // tile-local exclusive digit offsets
     __shared__ uint32_t wsum[2][kWaves];
 
-    const uint32_t n = count_of(n_dev, n_host);
+    const uint32_t n = count_of(n_dev, n_host, pa);
     const uint32_t tile0 = tile * kTileItems;
     if (tile0 >= n) return;
     const Digit dg = digit_params(pa);
@@ -234,7 +234,7 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-        const bool valid = base + r * 64 < n;
+        const bool valid = base + r * 64 < n && (!pa.drop || dg.keep(k_reg[r]));
         const uint32_t d = dg.of(k_reg[r]);
         const uint64_t peers = match_digit(d, dg.w, valid);
         uint32_t rk = 0xffffffffu;
@@ -250,6 +250,7 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
     }
     __syncthreads();
 
+    uint32_t t_loc;  // the tile's items kept (all of them unless pa.drop)
     {
         // per owned digit: wave prefixes, then two block scans over digits
         // (tile-local offsets, global digit bases)
@@ -272,7 +273,7 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
             s_loc += tot[j];
             s_glob += gt[j];
         }
-        uint32_t t_loc, t_glob;
+        uint32_t t_glob;
         uint32_t e_loc = block_exclusive<kThreads>(s_loc, wsum[0], t_loc);
         uint32_t e_glob = block_exclusive<kThreads>(s_glob, wsum[1], t_glob);
 #pragma unroll
@@ -306,8 +307,7 @@ __device__ __forceinline__ void rs_scatter(const uint32_t* __restrict__ keys_in,
     }
     __syncthreads();
 
-    const uint32_t cnt = min(n - tile0, (uint32_t)kTileItems);
-    for (uint32_t j = threadIdx.x; j < cnt; j += kThreads) {
+    for (uint32_t j = threadIdx.x; j < t_loc; j += kThreads) {
         const uint32_t key = s_keys[j];
         const uint32_t g = gbase[dg.of(key)] + j;
         keys_out[g] = key;
@@ -380,14 +380,16 @@ template <int kR, int kCB>
 static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
                        bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
                        const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s,
-                       const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt, int first_pass) {
+                       const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt, int first_pass,
+                       bool drop_first) {
     constexpr int kTileItems = kThreads * kR;
     const uint32_t nt = (uint32_t)((n + kTileItems - 1) / kTileItems);
     // upper bound of the radix over the passes (device-chosen widths never exceed it)
     const uint32_t radix_max = 1u << ((bits + passes - 1) / passes);
     bool ident = identity_vals;
     for (int p = first_pass; p < passes; ++p) {
-        const PassArgs pa{key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p};
+        const PassArgs pa{key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p,
+                          drop_first && p == first_pass ? 1u : 0u};
         k_rs_upsweep<kR, kCB><<<nt, kThreads, 0, s>>>(*keys_io, n_dev, (uint32_t)n, pa, tmp, nt);
         GSR_LAUNCH_CHECK("rs_upsweep");
         k_rs_offsets<<<(radix_max + kOffWaves - 1) / kOffWaves, 64 * kOffWaves, 0, s>>>(tmp, nt, pa, totals);
@@ -424,7 +426,8 @@ static int sort_passes_views(RadixViewArgs* views, int k, bool identity_vals, si
         for (int v = 0; v < k; ++v) {
             RadixViewArgs& a = views[v];
             sv.v[v] = SortView{*a.keys_io, *a.vals_io, *a.keys_alt, *a.vals_alt, a.n_dev, a.tmp, a.totals,
-                               PassArgs{a.key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p},
+                               PassArgs{a.key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p,
+                                        a.drop_first && p == first_pass ? 1u : 0u},
                                p == first_pass ? a.rect_in : nullptr, a.rect_in ? *a.pay_io : nullptr,
                                a.rect_in ? *a.pay_alt : nullptr};
         }
@@ -501,8 +504,10 @@ int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size
 int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt, uint32_t** vals_alt,
                      bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
                      const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s,
-                     const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt, int first_pass) {
+                     const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt, int first_pass,
+                     bool drop_first) {
     if (n == 0 || passes == 0 || first_pass >= passes) return GSR_OK;
+    if (drop_first && !key_range) return set_error(GSR_ERR_INVALID, "radix sort: dropping needs the key range");
     if (n > 0xffffffffull - 4 * kMinTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
     if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
         return set_error(GSR_ERR_INVALID, "radix sort: digit width out of range");
@@ -511,12 +516,12 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
     if ((bits + passes - 1) / passes <= 8) {
         if (key_range)
             return sort_passes<kRDepth, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
-                                     key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass);
+                                     key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first);
         return sort_passes<kRTile, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
-                                  key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass);
+                                  key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first);
     }
     return sort_passes<kRWide, kMaxBits>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
-                                         key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass);
+                                         key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first);
 }
 
 }  // namespace gsr

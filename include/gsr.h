@@ -287,8 +287,12 @@ int gsr_debug_stall(void* stream, uint32_t microseconds);
 /* Test hook: copy an internal array of the last gsr_render on `ctx` into
  * dst_dev (device memory, at most max_bytes). Returns the number of bytes
  * copied (>= 0) or a negative gsr_status.  what:
- *   GSR_DEBUG_RECORDS      48-B splat records in compacted slot order
- *                          (slot s = the s-th visible Gaussian in DESCENDING id order)
+ *   GSR_DEBUG_RECORDS      48-B splat records by slot.  Culling fused into the
+ *                          preprocess (the default; GSR_FUSED_CULL=0 at context
+ *                          creation selects the separate cull): one slot per
+ *                          Gaussian, slot n-1-id, N records (culled slots hold
+ *                          no record).  Separate cull: compacted, slot s = the
+ *                          s-th visible Gaussian in DESCENDING id order, V records.
  *   GSR_DEBUG_DEPTH_ORDER  uint32 record slots, front-to-back
  *   GSR_DEBUG_TILE_RANGES  uint32 pairs [begin, end) per 16x16 tile (row-major tiles)
  *   GSR_DEBUG_TILE_LIST    uint32 record slots of all (tile, splat) instances, by tile then depth */

@@ -86,10 +86,21 @@ def grab_debug(ctx, st):
         torch.cuda.synchronize()
         return buf.cpu().numpy().view(np.uint8)[:got].view(dtype)
 
-    return dict(records=grab(_lib.GSR_DEBUG_RECORDS, nv * 48, np.uint8).reshape(nv, 48),
-                depth_order=grab(_lib.GSR_DEBUG_DEPTH_ORDER, nv * 4, np.uint32),
+    n_all = max(int(st.get("n_gaussians", nv)), nv)
+    records = grab(_lib.GSR_DEBUG_RECORDS, n_all * 48, np.uint8)
+    depth_order = grab(_lib.GSR_DEBUG_DEPTH_ORDER, nv * 4, np.uint32)
+    tile_list = grab(_lib.GSR_DEBUG_TILE_LIST, nd * 4, np.uint32)
+    if records.size == n_all * 48 and n_all != nv:
+        # culling fused into the preprocess (GSR_FUSED_CULL, the default):
+        # Gaussian i owns slot n-1-i.  The compacted slots of the separate
+        # cull keep the same order, so the visible slots map to them by rank.
+        vis_slots = np.sort(depth_order)
+        records = records.reshape(n_all, 48)[vis_slots]
+        depth_order = np.searchsorted(vis_slots, depth_order).astype(np.uint32)
+        tile_list = np.searchsorted(vis_slots, tile_list).astype(np.uint32)
+    return dict(records=records.reshape(nv, 48), depth_order=depth_order,
                 ranges=grab(_lib.GSR_DEBUG_TILE_RANGES, nt * 8, np.uint32).reshape(nt, 2),
-                tile_list=grab(_lib.GSR_DEBUG_TILE_LIST, nd * 4, np.uint32))
+                tile_list=tile_list)
 
 
 def batched_frames(scene, cams, settings, group=4, debug_views=()):

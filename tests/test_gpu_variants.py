@@ -21,7 +21,8 @@ from helpers import batched_frames, gpu_frame
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [{}, {"GSR_BIN_FUSED": "0"}, {"GSR_TAIL_MERGE": "0", "GSR_TAIL_MERGE_ALONE": "1"}]
+VARIANTS = [{}, {"GSR_BIN_FUSED": "0"}, {"GSR_TAIL_MERGE": "0", "GSR_TAIL_MERGE_ALONE": "1"},
+            {"GSR_FUSED_CULL": "0"}]
 
 
 def _settings(**kw):
@@ -30,7 +31,7 @@ def _settings(**kw):
 
 
 def _frames(monkeypatch, env, g, scene, cams):
-    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE"):
+    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE", "GSR_FUSED_CULL"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -54,7 +55,7 @@ def test_stage_variants_identical(gpu, monkeypatch, h, w, n):
             assert alone["stats"]["n_instances"] > 0
             continue
         for a, b in ((ref[0], alone), (ref[1][0], group[0])):
-            for key in ("tile_list", "ranges", "depth_order"):
+            for key in ("tile_list", "ranges", "depth_order", "records"):
                 np.testing.assert_array_equal(a[key], b[key], err_msg=f"{env} {key}")
             np.testing.assert_array_equal(a["image"], b["image"], err_msg=f"{env} image")
         for v in range(1, len(cams)):

@@ -22,7 +22,7 @@ def short(n):
 qkey = "Queue_Id" if "Queue_Id" in rows[0] else ("Stream_Id" if "Stream_Id" in rows[0] else None)
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
              r.get(qkey, "?") if qkey else "?", enq.get(r["Correlation_Id"])) for r in rows)
-culls = [e for e in ev if e[2].startswith("k_cull_views")]
+culls = [e for e in ev if e[2].startswith(("k_cull_views", "k_preprocess_fc_views"))]
 merges = [e for e in ev if e[2].startswith("k_merge_views")]
 t0 = culls[-groups][0]
 t1 = max(e[1] for e in merges[-groups:])

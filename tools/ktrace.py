@@ -8,7 +8,8 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 name = lambda r: re.sub(r"\(.*", "", r["Kernel_Name"].replace("gsr::(anonymous namespace)::", "").replace("void ", ""))
-starts = [i for i, r in enumerate(rows) if name(r).startswith("k_cull")]
+# frames start at k_cull, or (fused cull) at a k_preprocess_fc_views launch
+starts = [i for i, r in enumerate(rows) if name(r).startswith("k_cull") or name(r).startswith("k_preprocess_fc")]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else len(starts) // 2
 a, b = starts[k], starts[k + 1] if k + 1 < len(starts) else len(rows)
 t0 = int(rows[a]["Start_Timestamp"])

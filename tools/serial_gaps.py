@@ -1,5 +1,5 @@
-"""GPU idle gaps of single-view frames (tooling): per frame (k_cull ... k_merge,
-non-batched kernels) the span, the kernel busy time and the idle gaps between
+"""GPU idle gaps of single-view frames (tooling): per frame (k_cull or the fused preprocess ... k_merge,
+non-batched kernels; k_preprocess_fc_views with k = 1 for the fused cull) the span, the kernel busy time and the idle gaps between
 consecutive kernels, by the kernel that follows the gap.
 usage: python tools/serial_gaps.py prof_kernel_trace.csv [frames]"""
 import csv
@@ -18,8 +18,12 @@ def short(n):
 
 
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in rows)
+# a frame alone with the fused cull starts with k_preprocess_fc_views (k = 1),
+# followed by the single-view depth sort
+ev = [(e[0], e[1], "k_preprocess_fc") if e[2].startswith("k_preprocess_fc_views") and i + 1 < len(ev)
+      and ev[i + 1][2].startswith("k_rs_upsweep<") else e for i, e in enumerate(ev)]
 ev = [e for e in ev if "_views" not in e[2] and "rocclr" not in e[2] and "repack" not in e[2]]
-starts = [i for i, e in enumerate(ev) if e[2] == "k_cull"]
+starts = [i for i, e in enumerate(ev) if e[2] in ("k_cull", "k_preprocess_fc")]
 frames = []
 for a, b in zip(starts, starts[1:] + [len(ev)]):
     fr = ev[a:b]

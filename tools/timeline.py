@@ -19,7 +19,7 @@ views = [e for e in ev if "_views" in e[2]]
 # the timed region: the last `groups` groups of views (default 13 = 50 frames of 4-view groups)
 groups = int(sys.argv[2]) if len(sys.argv) > 2 else 13
 vpg = int(sys.argv[3]) if len(sys.argv) > 3 else 4
-culls = [e for e in views if e[2].startswith("k_cull_views")]
+culls = [e for e in views if e[2].startswith(("k_cull_views", "k_preprocess_fc_views"))]
 merges = [e for e in views if e[2].startswith("k_merge_views")]
 t0, t1 = culls[-groups][0], merges[-1][1]
 seg = [e for e in ev if e[0] >= t0 and e[1] <= t1]
