@@ -192,7 +192,7 @@ def cpu_baseline(g, cam, seconds):
 
 
 # stage name -> kernel symbol in rocprofv3 summaries
-KERNEL_SYMBOL = {"composite": "k_composite<0>", "preprocess": "k_preprocess_fc_views<3>", "merge": "k_merge"}
+KERNEL_SYMBOL = {"composite": "k_composite<0>", "preprocess": "k_preprocess_fc_views<3, true>", "merge": "k_merge"}
 PMC_PROFILE = os.path.join(ROOT, "profiles", "LATEST")
 
 

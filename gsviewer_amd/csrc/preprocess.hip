@@ -842,7 +842,9 @@ struct ViewsPreFc {
 };
 static_assert(sizeof(ViewsPreFc) <= 3584, "kernel argument size");
 
-template <int DEG>
+// kAlone: the same code, instantiated separately for the launches of a frame
+// alone (k = 1) so that profiles tell them from the groups' launches.
+template <int DEG, bool kAlone>
 __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_fc_views(const float4* __restrict__ pos_op,
                                                                               const float4* __restrict__ rot,
                                                                               const float4* __restrict__ scale,
@@ -1037,7 +1039,9 @@ int launch_preprocess_fc_views(const SceneData& sd, const ViewPreFcArgs* views, 
                             a.zero_words, a.done_ctr,  a.host_counters, a.radii,      a.n_zero,   a.seq};
     }
     const unsigned grid = preprocess_grid(sd.n);
-#define GSR_PREV(D) k_preprocess_fc_views<D><<<grid, kThreads, 0, s>>>(sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, vp)
+#define GSR_PREV(D)                                                                                             \
+    (k == 1 ? k_preprocess_fc_views<D, true> : k_preprocess_fc_views<D, false>)<<<grid, kThreads, 0, s>>>(        \
+        sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, vp)
     switch (deg) {
         case -1: GSR_PREV(-1); break;
         case 0: GSR_PREV(0); break;

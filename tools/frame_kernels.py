@@ -1,6 +1,6 @@
 """Median per-kernel duration and gap of single-view frames (gsr_render) in a
 rocprofv3 kernel_trace.csv; a frame runs from its cull (k_cull, or the fused
-preprocess k_preprocess_fc_views launched for one view) to its k_merge.
+preprocess k_preprocess_fc_views<DEG, true> of a frame alone) to its k_merge.
 usage: python tools/frame_kernels.py KERNEL_TRACE.csv"""
 import csv
 import re
@@ -14,13 +14,12 @@ name = lambda r: re.sub(r"\(.*", "", r["Kernel_Name"].replace("gsr::(anonymous n
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name(r)) for r in rows)
 frames, cur = [], None
 for i, e in enumerate(ev):
-    single_fc = e[2].startswith("k_preprocess_fc_views") and i + 1 < len(ev) and ev[i + 1][2].startswith("k_rs_upsweep<")
-    if e[2] == "k_cull" or single_fc:
+    if e[2] == "k_cull" or (e[2].startswith("k_preprocess_fc_views<") and e[2].endswith(", true>")):
         cur = [e]
         continue
     if cur is None:
         continue
-    if "_views" in e[2]:
+    if "_views" in e[2] and not e[2].endswith(", true>"):
         cur = None
         continue
     cur.append(e)

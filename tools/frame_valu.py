@@ -17,7 +17,7 @@ frame_ms = float(sys.argv[3]) if len(sys.argv) > 3 else None
 valu, trans, disp = defaultdict(float), defaultdict(float), {}
 for r in csv.DictReader(open(path)):
     k = r["kernel"]
-    if "_views" not in k:
+    if "_views" not in k or k.endswith(", true>"):  # (<DEG, true>: the fused preprocess of a frame alone)
         continue
     if r["counter"] == "SQ_INSTS_VALU":
         valu[k] = float(r["value_per_dispatch"])

@@ -18,10 +18,9 @@ def short(n):
 
 
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in rows)
-# a frame alone with the fused cull starts with k_preprocess_fc_views (k = 1),
-# followed by the single-view depth sort
-ev = [(e[0], e[1], "k_preprocess_fc") if e[2].startswith("k_preprocess_fc_views") and i + 1 < len(ev)
-      and ev[i + 1][2].startswith("k_rs_upsweep<") else e for i, e in enumerate(ev)]
+# a frame alone with the fused cull starts with k_preprocess_fc_views<DEG, true>
+ev = [(e[0], e[1], "k_preprocess_fc") if e[2].startswith("k_preprocess_fc_views<") and e[2].endswith(", true>")
+      else e for e in ev]
 ev = [e for e in ev if "_views" not in e[2] and "rocclr" not in e[2] and "repack" not in e[2]]
 starts = [i for i, e in enumerate(ev) if e[2] in ("k_cull", "k_preprocess_fc")]
 frames = []
