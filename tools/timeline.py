@@ -15,13 +15,15 @@ def short(n):
 
 
 ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in rows)
-views = [e for e in ev if "_views" in e[2]]
-# the timed region: the last `groups` groups of views (default 13 = 50 frames of 4-view groups)
-groups = int(sys.argv[2]) if len(sys.argv) > 2 else 13
-vpg = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+# group launches (the <DEG, true> preprocess is a frame alone's)
+views = [e for e in ev if "_views" in e[2] and not e[2].endswith(", true>")]
+# the timed region: the last `groups` groups of views (default 10 = 50 frames of 5-view groups)
+groups = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+vpg = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 culls = [e for e in views if e[2].startswith(("k_cull_views", "k_preprocess_fc_views"))]
-merges = [e for e in views if e[2].startswith("k_merge_views")]
-t0, t1 = culls[-groups][0], merges[-1][1]
+# a group ends with its merge launch, or with its compositing launch (tail merge)
+ends = [e for e in views if e[2].startswith(("k_merge_views", "k_composite_views"))]
+t0, t1 = culls[-groups][0], ends[-1][1]
 seg = [e for e in ev if e[0] >= t0 and e[1] <= t1]
 busy, cs, ce = 0, None, None
 for s, e, n in seg:
