@@ -517,10 +517,16 @@ def main():
     # barrier + synchronize on both sides; MAX over ranks.  No instrumentation
     # inside: every HIP event record stalls the stream for several us.  Every
     # begun frame is finished (drain) before the closing synchronize.
+    host_step_s = []  # host time of each step() call in the timed region (perf_counter only: no GPU effect)
+
     def pipelined(steps):
         for _ in range(steps):
+            h = time.perf_counter()
             pipe.step()
+            host_step_s.append(time.perf_counter() - h)
+        h = time.perf_counter()
         pipe.drain()
+        host_step_s.append(time.perf_counter() - h)
 
     own = []
     if share == 1:
@@ -538,6 +544,7 @@ def main():
         pipe.next = 0
         elapsed = timed_region(lambda: pipelined(calls), 1, dev, own) * args.steps / timed_frames
         own[0] *= args.steps / timed_frames
+    host_steps = list(host_step_s)  # (the timed region's calls only)
     # single-view latency: the same number of frames of view 0, one at a time
     latency = timed_region(serial_frame, args.steps, dev) if K > 1 else elapsed
     # SURVEY 8(d)'s GPU timing: the median of per-frame times, one frame at a
@@ -695,6 +702,10 @@ def main():
         "ms_per_step": ms_per_step,
         "fps_per_gpu": fps,
         "latency_ms_per_frame": 1e3 * latency / args.steps,
+        "host_ms_per_call": {"calls": len(host_steps), "mean": 1e3 * sum(host_steps) / max(1, len(host_steps)),
+                             "max": 1e3 * max(host_steps, default=0.0),
+                             "note": "host time of each pipeline step (one group's finish + begin) and of the "
+                                     "closing drain in the timed region"},
         "latency_ms_median": latency_median_ms,
         "views_in_flight": K,
         "splats_per_s_per_gpu": value / world,
