@@ -77,8 +77,9 @@ __device__ __forceinline__ void bin_reduce(const uint32_t* __restrict__ sorted_i
                 s += rect_tiles(unpack_rect(rect4_sorted[r]));
             } else {
                 const uint32_t id = sorted_ids[r];
-                // (ids are < n_vis by construction)
-                const uint2 tr = id < n_vis ? trect[id] : make_uint2(0xffffu, 0u);
+                // (ids are record slots the depth sort produced: always in range, and
+                // not below n_vis with the fused cull's uncompacted slots)
+                const uint2 tr = trect[id];
                 trect_sorted[r] = tr;
                 s += rect_tiles(tr);
             }
@@ -262,8 +263,7 @@ __device__ __forceinline__ uint2 sorted_rect(const uint32_t* __restrict__ sorted
     if constexpr (kPacked) {
         return unpack_rect(rect4_sorted[r]);
     } else {
-        const uint32_t id = sorted_ids[r];
-        const uint2 tr = id < n_vis ? trect[id] : make_uint2(0xffffu, 0u);
+        const uint2 tr = trect[sorted_ids[r]];  // (a record slot: not below n_vis with the fused cull)
         trect_sorted[r] = tr;
         return tr;
     }

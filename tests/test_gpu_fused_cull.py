@@ -75,11 +75,15 @@ def test_group_views_of_mixed_visibility(gpu, monkeypatch):
     scene.close()
 
 
-def test_context_alternating_key_ranges(gpu):
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_context_alternating_key_ranges(gpu, monkeypatch, split):
     """One context renders frames whose visible depth ranges differ (wide,
     narrow, none, wide again, ...): each frame bit-identical to a fresh
     context's render of it.  A stale key-range shard of an earlier frame that
-    counted would widen or, worse, narrow the range the depth sort keeps."""
+    counted would widen or, worse, narrow the range the depth sort keeps.
+    split = 1: frames alone in two branches (GSR_SPLIT_ALONE), whose depth
+    keys and key range come from k_depth_fc's own completion words."""
+    monkeypatch.setenv("GSR_SPLIT_ALONE", split)
     import torch
 
     from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into

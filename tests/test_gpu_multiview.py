@@ -273,18 +273,23 @@ def test_rect_payload_matches_gathered_rects(gpu, monkeypatch):
     """The depth sort carrying the packed tile rectangles (default for frames
     of <= 256 x 256 tiles) bins exactly as the by-id gather of the rectangles
     (GSR_NO_RECT_PAYLOAD): same images and counts, single view and a batched
-    group."""
+    group.  One view sits inside the scene (part of it visible): with the
+    fused cull's uncompacted slots the gathered ids reach past V."""
     import torch
 
     from gsviewer_amd.multiview import ViewBatchPipeline
-    from gsviewer_amd.rasterizer import render_into
+    from gsviewer_amd.rasterizer import camera_from, render_into
     scene, st, cams, ctxs, streams, outs = _setup(4)
+    near = Camera(180, 320)
+    near.target_dist = 0.4
+    cams[3] = camera_from(near)
     got = {}
     for mode in ("payload", "gather"):
         if mode == "gather":
             monkeypatch.setenv("GSR_NO_RECT_PAYLOAD", "1")
         o = torch.empty_like(outs[0])
-        render_into(ctxs[0], scene, cams[1], st, o)
+        render_into(ctxs[0], scene, cams[3], st, o)
+        assert 0 < ctxs[0].stats()["n_visible"] < scene.n
         # the context moves to another stream: its frame on this one must be done
         torch.cuda.synchronize()
         pipe = ViewBatchPipeline([(ctxs, cams, outs, streams[0])], scene, st)

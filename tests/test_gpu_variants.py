@@ -7,9 +7,16 @@
 * GSR_TAIL_MERGE (groups, default 1) / GSR_TAIL_MERGE_ALONE (a frame alone,
   default 0): a multi-chunk tile folded by its last chunk to finish, inside
   the compositing launch, against the k_merge launch: the same fold in the
-  same chunk order.
+  same chunk order;
+* GSR_FUSED_CULL (default 1): culling inside the preprocess, uncompacted
+  slots, culled keys dropped by the depth sort's first pass, against k_cull +
+  the compaction scan + k_preprocess (tests/helpers.grab_debug maps the
+  uncompacted slots to the compacted ones by rank);
+* GSR_SPLIT_ALONE (a frame alone, default 0): the depth keys first
+  (k_depth_fc), the depth sort on a side stream beside the preprocess, joined
+  before the binning, which then gathers the rects (no sort payload).
 
-Images, tile lists and tile ranges must be bit-identical, on a frame rendered alone (gsr_render) and on a group of
+Images, records, depth order, tile lists and tile ranges must be bit-identical, on a frame rendered alone (gsr_render) and on a group of
 views (gsr_render_finish_views), for frame sizes whose tile ids take one
 radix pass (<= 2048 tiles) and two, plus the full-size C2 frame."""
 import numpy as np
@@ -22,7 +29,7 @@ from helpers import batched_frames, gpu_frame
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [{}, {"GSR_BIN_FUSED": "0"}, {"GSR_TAIL_MERGE": "0", "GSR_TAIL_MERGE_ALONE": "1"},
-            {"GSR_FUSED_CULL": "0"}]
+            {"GSR_FUSED_CULL": "0"}, {"GSR_SPLIT_ALONE": "1"}]
 
 
 def _settings(**kw):
@@ -31,7 +38,7 @@ def _settings(**kw):
 
 
 def _frames(monkeypatch, env, g, scene, cams):
-    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE", "GSR_FUSED_CULL"):
+    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE", "GSR_FUSED_CULL", "GSR_SPLIT_ALONE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
