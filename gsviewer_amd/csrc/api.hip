@@ -125,7 +125,6 @@ struct PendingFrame {
     uint32_t *pa = nullptr, *pb = nullptr;  // packed tile rects carried by the depth sort (result in pa)
     bool packed = false;                    // the depth sort carries them (frames of <= 256 x 256 tiles)
     bool sort_ready = false;  // gsr_render_begin_views done, gsr_render_begin_sort not yet
-    bool split = false;       // the depth sort runs on the context's side stream (join before the binning)
 };
 }  // namespace gsr
 
@@ -167,11 +166,6 @@ struct gsr_context {
     bool first_major_alone = false;               // the same for a frame finished alone (gsr_render_finish)
     bool bin_fused = true;                        // the tile sort's pass 0 fused into the binning (k_bin_scatter)
     bool fused_cull = true;                       // culling inside the preprocess (launch_preprocess_fc)
-    bool split_alone = false;                     // gsr_render: depth keys first, sort beside the preprocess
-    unsigned split_per_cu = 3;                    // the preprocess grid beside the sort (blocks per CU)
-    bool alone_now = false;                       // inside gsr_render
-    hipStream_t side = nullptr;                   // split frames: the depth sort's stream
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int depth_passes_alone = kDepthPassesAlone;   // depth sort passes of gsr_render's frames
     int depth_passes_now = 0;                     // this frame's (0: kDepthPasses)
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
@@ -351,7 +345,7 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
     if ((rc = c->rect4_b.ensure(n, "rect4"))) return rc;
     if ((rc = c->bin_tmp.ensure(bin_tmp_elems(n), "bin_tmp"))) return rc;
     if ((rc = c->radix_tmp.ensure(radix_tmp_elems(n), "radix_tmp"))) return rc;
-    if ((rc = c->done_ctr.ensure(2 * kDoneCtrWords, "done_ctr"))) return rc;  // preprocess; k_depth_fc
+    if ((rc = c->done_ctr.ensure(kDoneCtrWords, "done_ctr"))) return rc;
     if (c->has_arena && c->arena.measure) return GSR_OK;  // gsr_workspace_size: sizes only, no HIP call
     if (!c->host_counters) {
         if (hipHostMalloc(&c->host_counters, 4 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
@@ -375,7 +369,7 @@ int ensure_scene_buffers(gsr_context* c, size_t n) {
 // context's next frame begins.
 int arm_done_ctr(gsr_context* c, hipStream_t s) {
     if (c->done_armed) return GSR_OK;
-    GSR_HIP_CHECK(hipMemsetAsync(c->done_ctr.p, 0, 2 * kDoneCtrWords * sizeof(unsigned long long), s));
+    GSR_HIP_CHECK(hipMemsetAsync(c->done_ctr.p, 0, kDoneCtrWords * sizeof(unsigned long long), s));
     c->done_armed = true;
     return GSR_OK;
 }
@@ -448,7 +442,7 @@ int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const 
                hipStream_t s) {
     f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
     f.pa = c->rect4_a.p, f.pb = c->rect4_b.p;
-    f.packed = !f.split && rects_packable(f.u);  // (split: the rects are written beside the sort)
+    f.packed = rects_packable(f.u);
     if (f.n == 0) return GSR_OK;
     return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32,
                             c->depth_passes_now ? c->depth_passes_now : kDepthPasses, key_range,
@@ -687,11 +681,6 @@ int gsr_context_create(gsr_context** out) {
     if (const char* e = std::getenv("GSR_FIRST_MAJOR")) (*out)->first_major = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_BIN_FUSED")) (*out)->bin_fused = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_FUSED_CULL")) (*out)->fused_cull = std::strtol(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("GSR_SPLIT_ALONE")) (*out)->split_alone = std::strtol(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("GSR_SPLIT_PER_CU")) {
-        const long v = std::strtol(e, nullptr, 10);
-        (*out)->split_per_cu = (unsigned)std::min(8l, std::max(1l, v));
-    }
     if (const char* e = std::getenv("GSR_FIRST_MAJOR_ALONE"))
         (*out)->first_major_alone = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_VIEWS_INTERLEAVE")) (*out)->views_interleave = std::strtol(e, nullptr, 10) != 0;
@@ -714,9 +703,6 @@ int gsr_context_destroy(gsr_context* c) {
         for (auto& e : row)
             if (e) (void)hipEventDestroy(e);
     c->stamps.release();
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-    if (c->side) (void)hipStreamDestroy(c->side);
     delete c;
     return GSR_OK;
 }
@@ -837,35 +823,7 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
 
     if ((rc = prof_record(c, slot, EV_START, s))) return rc;
     if (n == 0) GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * zl.total, s));
-    PendingFrame& f = c->pend;
-    f.split = n > 0 && c->fused_cull && c->split_alone && c->alone_now;
-    if (f.split) {
-        // A frame alone in two branches: k_depth_fc writes the keys, V and the
-        // key range; the depth sort then runs on the side stream while the
-        // preprocess computes the records on this one; the finish joins them
-        // before the binning (which gathers the rects: no payload).
-        if (!c->side) {
-            GSR_HIP_CHECK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-            GSR_HIP_CHECK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-            GSR_HIP_CHECK(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
-        }
-        const uint32_t seq = ++c->seq;
-        if ((rc = launch_depth_fc(sc->d, u, c->keys_a.p, counters, c->zero.p + zl.key_range,
-                                  c->done_ctr.p + kDoneCtrWords, seq, s)))
-            return rc;
-        if ((rc = prof_record(c, slot, EV_CULL, s))) return rc;
-        GSR_HIP_CHECK(hipEventRecord(c->ev_fork, s));
-        GSR_HIP_CHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-        f.n = n;
-        f.u = u;
-        if ((rc = depth_sort(c, f, counters + 0, c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, c->side)))
-            return rc;
-        GSR_HIP_CHECK(hipEventRecord(c->ev_join, c->side));
-        if ((rc = launch_preprocess_fc(sc->d, u, c->recs.p, nullptr, c->trect.p, counters, nullptr,
-                                       c->zero.p + zl.ranges, (uint32_t)(zl.total - zl.ranges), c->done_ctr.p,
-                                       c->host_counters_dev, seq, radii, s, c->split_per_cu)))
-            return rc;
-    } else if (n > 0 && c->fused_cull) {
+    if (n > 0 && c->fused_cull) {
         // one launch: cull, preprocess, V / D / key range, and the zero block's clearing
         if ((rc = prof_record(c, slot, EV_CULL, s))) return rc;
         if ((rc = launch_preprocess_fc(sc->d, u, c->recs.p, c->keys_a.p, c->trect.p, counters, c->zero.p + zl.key_range,
@@ -893,11 +851,10 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
     if ((rc = prof_record(c, slot, EV_AFTER_SYNC1, s))) return rc;
 
     // depth sort over the upper bound N; the device count V bounds the work
+    PendingFrame& f = c->pend;
     f.n = n;
     f.u = u;
-    if (!f.split &&
-        (rc = depth_sort(c, f, counters + 0, c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s)))
-        return rc;
+    if ((rc = depth_sort(c, f, counters + 0, c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s))) return rc;
     if ((rc = prof_record(c, slot, EV_DSORT, s))) return rc;
     f.active = true;
     f.u = u;
@@ -964,7 +921,6 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
                                c->zero.p + zl.ranges, c->done_ctr.p, c->host_counters_dev,
                                radii ? radii[v] : nullptr, (uint32_t)(zl.total - zl.ranges), c->seq};
         PendingFrame& f = c->pend;
-        f.split = false;
         f.u = u[v];
         f.t_min = st->t_min;
         std::memcpy(f.bg, st->bg, sizeof(f.bg));
@@ -1084,7 +1040,6 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     const auto h1 = std::chrono::steady_clock::now();
     if (n > 0 && (rc = wait_counts(c, s))) return rc;
     const auto h2 = std::chrono::steady_clock::now();
-    if (f.split) GSR_HIP_CHECK(hipStreamWaitEvent(s, c->ev_join, 0));  // the depth sort of the side stream
     const uint32_t n_vis = n > 0 ? __atomic_load_n(&c->host_counters[0], __ATOMIC_ACQUIRE) : 0u;
     const uint32_t n_dup = n > 0 ? __atomic_load_n(&c->host_counters[1], __ATOMIC_ACQUIRE) : 0u;
     if (c->prof_on) prof_accumulate(c, slot ^ 1, false);
@@ -1331,10 +1286,8 @@ int gsr_render(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam, const
                int32_t* radii, void* stream) {
     if (!c) return set_error(GSR_ERR_INVALID, "null argument");
     c->depth_passes_now = c->depth_passes_alone;  // nothing else in flight: the widest digits
-    c->alone_now = true;
     int rc = gsr_render_begin(c, sc, cam, st, out, radii, stream);
     c->depth_passes_now = 0;
-    c->alone_now = false;
     if (rc) return rc;
     return gsr_render_finish(c, stream);
 }

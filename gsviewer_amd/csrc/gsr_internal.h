@@ -384,13 +384,7 @@ constexpr size_t kDoneCtrWords = 1 + 3 * 64;
 int launch_preprocess_fc(const SceneData& sd, const FrameUniforms& u, SplatRec* recs, uint32_t* depth_keys,
                          uint2* trect, uint32_t* counters, uint32_t* key_range, uint32_t* zero_words, uint32_t n_zero,
                          unsigned long long* done_ctr, uint32_t* host_counters, uint32_t seq, int32_t* radii,
-                         hipStream_t s, unsigned per_cu = 4);
-// A frame alone split in two (GSR_SPLIT_PRE): the depth keys of every slot, V
-// and the key range (counters[0], key_range; done_ctr: its own kDoneCtrWords
-// words), for a depth sort that then runs beside launch_preprocess_fc with
-// depth_keys = key_range = nullptr.
-int launch_depth_fc(const SceneData& sd, const FrameUniforms& u, uint32_t* depth_keys, uint32_t* counters,
-                    uint32_t* key_range, unsigned long long* done_ctr, uint32_t seq, hipStream_t s);
+                         hipStream_t s);
 struct ViewPreFcArgs {
     const FrameUniforms* u;
     SplatRec* recs;
@@ -405,8 +399,7 @@ struct ViewPreFcArgs {
     uint32_t n_zero;
     uint32_t seq;
 };
-int launch_preprocess_fc_views(const SceneData& sd, const ViewPreFcArgs* views, int k, hipStream_t s,
-                               unsigned per_cu = 4);
+int launch_preprocess_fc_views(const SceneData& sd, const ViewPreFcArgs* views, int k, hipStream_t s);
 
 // composite.hip
 size_t bin_tmp_elems(size_t n_vis);

@@ -556,7 +556,7 @@ __device__ __forceinline__ uint32_t preprocess_compute(const GaussLoad<DEG>& g, 
     dst[1] = make_float4(rec.qa, rec.qb, rec.qc, __uint_as_float(rec.yspan));
     dst[2] = make_float4(rec.r, rec.g, rec.b, rec.mid);
     key = float_order_key(-pr.pv[2]);
-    if (depth_keys) depth_keys[slot] = key;  // (null: the keys come from k_depth_fc)
+    depth_keys[slot] = key;
     if (radii) {
         const float rr = ceilf(fmaxf(qs[0], qs[1]));
         radii[i] = (rr >= 0.f && rr < 2147483520.f) ? (int32_t)rr : 0;
@@ -757,21 +757,15 @@ __device__ __forceinline__ void load_attrs(GaussLoad<DEG>& g, const float4 po, c
 
 __device__ __forceinline__ void culled_slot(uint32_t slot, uint32_t* __restrict__ depth_keys,
                                             uint2* __restrict__ trect) {
-    if (depth_keys) depth_keys[slot] = 0xffffffffu;
+    depth_keys[slot] = 0xffffffffu;
     trect[slot] = make_uint2(0xffffu, 0u);
 }
 
 // One frame's block results: counts and the key range of its visible
 // Gaussians.  Thread 0 only; returns true in the block that completed the grid.
 __device__ __forceinline__ bool block_done(unsigned long long* __restrict__ done_ctr, uint32_t seq, uint32_t tiles,
-                                           uint32_t nvis, uint32_t kmax, uint32_t nkmin, uint32_t& n_dup,
-                                           bool keys = true) {
-    if (nvis && !keys) {  // visible count only (the key range is k_depth_fc's)
-        const unsigned long long r = __hip_atomic_fetch_add(
-            done_ctr + kKeyShards0 + 2 * kKeyShards + (int)(blockIdx.x % kKeyShards), (unsigned long long)nvis,
-            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("" ::"v"(r) : "memory");
-    } else if (nvis) {
+                                           uint32_t nvis, uint32_t kmax, uint32_t nkmin, uint32_t& n_dup) {
+    if (nvis) {
         const int sh = kKeyShards0 + (int)(blockIdx.x % kKeyShards);
         const unsigned long long tag = (unsigned long long)seq << 32;
         const unsigned long long r0 =
@@ -795,8 +789,6 @@ __device__ __forceinline__ bool block_done(unsigned long long* __restrict__ done
 // The completing block's publication, by one whole wave: the frame's key
 // range from the shards, V and D to the device counters and (V, D, seq) to
 // host-mapped memory; the counters are re-armed for the next frame.
-// key_range null: no key range, no V to the device counters (k_depth_fc's);
-// host_counters null: no D and no host publication (k_depth_fc).
 __device__ __forceinline__ void publish_frame(unsigned long long* __restrict__ done_ctr, uint32_t seq, uint32_t n_dup,
                                               uint32_t* __restrict__ key_range, uint32_t* __restrict__ counters,
                                               uint32_t* __restrict__ host_counters) {
@@ -813,17 +805,13 @@ __device__ __forceinline__ void publish_frame(unsigned long long* __restrict__ d
     __hip_atomic_store(done_ctr + kKeyShards0 + 2 * kKeyShards + lane, 0ull, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     if (lane == 0) {
-        if (key_range) {
-            key_range[0] = nkmin;  // {0, 0} when nothing is visible, like the scan's
-            key_range[1] = kmax;
-            counters[0] = n_vis;
-        }
-        if (host_counters) {
-            counters[1] = n_dup;
-            __hip_atomic_store(host_counters + 0, n_vis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(host_counters + 1, n_dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(host_counters + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+        key_range[0] = nkmin;  // {0, 0} when nothing is visible, like the scan's
+        key_range[1] = kmax;
+        counters[0] = n_vis;
+        counters[1] = n_dup;
+        __hip_atomic_store(host_counters + 0, n_vis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_counters + 1, n_dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(host_counters + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(done_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -919,9 +907,7 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_fc_views(co
         for (int w = 0; w < kThreads / 64; ++w)
             t += s_red[v][0][w], nv += s_red[v][1][w], kx = max(kx, s_red[v][2][w]), kn = max(kn, s_red[v][3][w]);
         uint32_t n_dup;
-        s_last[v] = block_done(vs.v[v].done_ctr, vs.v[v].seq, t, nv, kx, kn, n_dup, vs.v[v].key_range != nullptr)
-                        ? 1u
-                        : 0u;
+        s_last[v] = block_done(vs.v[v].done_ctr, vs.v[v].seq, t, nv, kx, kn, n_dup) ? 1u : 0u;
         s_dup[v] = n_dup;
     }
     __syncthreads();
@@ -929,47 +915,6 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_fc_views(co
         if (s_last[v])
             publish_frame(vs.v[v].done_ctr, vs.v[v].seq, s_dup[v], vs.v[v].key_range, vs.v[v].counters,
                           vs.v[v].host_counters);
-}
-
-// A frame alone split in two (GSR_SPLIT_PRE): this kernel writes the depth
-// keys of every slot (0xffffffff culled), V and the key range, and the depth
-// sort starts on a second stream right after it while the preprocess proper
-// (k_preprocess_fc_views with no depth_keys / key_range) computes the records
-// on the frame's stream.  The visibility test is the preprocess's (project()).
-__global__ __launch_bounds__(kThreads) void k_depth_fc(const float4* __restrict__ pos_op, int64_t n, FrameUniforms u,
-                                                       uint32_t* __restrict__ depth_keys,
-                                                       uint32_t* __restrict__ counters,
-                                                       uint32_t* __restrict__ key_range,
-                                                       unsigned long long* __restrict__ done_ctr, uint32_t seq) {
-    __shared__ uint32_t s_red[3][kThreads / 64];
-    __shared__ uint32_t s_last;
-    uint32_t nvis = 0, kmax = 0, nkmin = 0;
-    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
-        const float4 p = pos_op[i];
-        const Projected pr = project(p.x, p.y, p.z, u);
-        const uint32_t key = float_order_key(-pr.pv[2]);
-        depth_keys[n - 1 - i] = pr.vis ? key : 0xffffffffu;
-        if (pr.vis) {
-            nvis += 1;
-            kmax = max(kmax, key);
-            nkmin = max(nkmin, ~key);
-        }
-    }
-    const int wave = threadIdx.x >> 6;
-    {
-        const uint32_t a = wave_reduce_sum(nvis), b = wave_reduce_max(kmax), c = wave_reduce_max(nkmin);
-        if (__lane_id() == 0) s_red[0][wave] = a, s_red[1][wave] = b, s_red[2][wave] = c;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t v = 0, kx = 0, kn = 0;
-#pragma unroll
-        for (int w = 0; w < kThreads / 64; ++w) v += s_red[0][w], kx = max(kx, s_red[1][w]), kn = max(kn, s_red[2][w]);
-        uint32_t n_dup;
-        s_last = block_done(done_ctr, seq, 0u, v, kx, kn, n_dup) ? 1u : 0u;
-    }
-    __syncthreads();
-    if (s_last && wave == 0) publish_frame(done_ctr, seq, 0u, key_range, counters, nullptr);
 }
 
 __global__ __launch_bounds__(kThreads) void k_depth_keys_all(const float4* __restrict__ pos_op, int64_t n, float v8,
@@ -982,21 +927,15 @@ __global__ __launch_bounds__(kThreads) void k_depth_keys_all(const float4* __res
 
 }  // namespace
 
-static unsigned device_cus() {
-    static const unsigned cus = [] {
-        int dev = 0, c = 256;
+static unsigned preprocess_grid(int64_t n) {
+    static const unsigned max_grid = [] {
+        int dev = 0, cus = 256;
         if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
-            c = 256;
-        return (unsigned)c;
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return 4u * (unsigned)cus;  // ~4 resident blocks per CU (92 VGPRs: 5 waves/SIMD fit)
     }();
-    return cus;
-}
-
-// per_cu: resident blocks per CU the grid is sized for (4: one wave per SIMD
-// each, the occupancy of the DEG-3 kernel at 119 VGPRs)
-static unsigned preprocess_grid(int64_t n, unsigned per_cu = 4) {
-    return std::max(1u, std::min((unsigned)((n + kThreads - 1) / kThreads), per_cu * device_cus()));
+    return std::max(1u, std::min((unsigned)((n + kThreads - 1) / kThreads), max_grid));
 }
 
 static int effective_deg(const FrameUniforms& u) {
@@ -1081,22 +1020,13 @@ static_assert(kDoneCtrWords >= (size_t)(kKeyShards0 + 3 * kKeyShards), "completi
 int launch_preprocess_fc(const SceneData& sd, const FrameUniforms& u, SplatRec* recs, uint32_t* depth_keys,
                          uint2* trect, uint32_t* counters, uint32_t* key_range, uint32_t* zero_words, uint32_t n_zero,
                          unsigned long long* done_ctr, uint32_t* host_counters, uint32_t seq, int32_t* radii,
-                         hipStream_t s, unsigned per_cu) {
+                         hipStream_t s) {
     const ViewPreFcArgs a{&u, recs, depth_keys, trect, counters, key_range, zero_words, done_ctr, host_counters, radii,
                           n_zero, seq};
-    return launch_preprocess_fc_views(sd, &a, 1, s, per_cu);
+    return launch_preprocess_fc_views(sd, &a, 1, s);
 }
 
-int launch_depth_fc(const SceneData& sd, const FrameUniforms& u, uint32_t* depth_keys, uint32_t* counters,
-                    uint32_t* key_range, unsigned long long* done_ctr, uint32_t seq, hipStream_t s) {
-    if ((uint64_t)sd.n > 0xffffffffull) return set_error(GSR_ERR_OVERFLOW, "preprocess: too many Gaussians");
-    k_depth_fc<<<preprocess_grid(sd.n), kThreads, 0, s>>>(sd.pos_op, sd.n, u, depth_keys, counters, key_range,
-                                                          done_ctr, seq);
-    GSR_LAUNCH_CHECK("depth_fc");
-    return GSR_OK;
-}
-
-int launch_preprocess_fc_views(const SceneData& sd, const ViewPreFcArgs* views, int k, hipStream_t s, unsigned per_cu) {
+int launch_preprocess_fc_views(const SceneData& sd, const ViewPreFcArgs* views, int k, hipStream_t s) {
     if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "preprocess_views: view count out of range");
     if ((uint64_t)sd.n > 0xffffffffull) return set_error(GSR_ERR_OVERFLOW, "preprocess: too many Gaussians");
     ViewsPreFc vp{};
@@ -1108,7 +1038,7 @@ int launch_preprocess_fc_views(const SceneData& sd, const ViewPreFcArgs* views, 
         vp.v[v] = ViewPreFc{*a.u,         a.recs,      a.depth_keys, a.trect,         a.counters, a.key_range,
                             a.zero_words, a.done_ctr,  a.host_counters, a.radii,      a.n_zero,   a.seq};
     }
-    const unsigned grid = preprocess_grid(sd.n, per_cu);
+    const unsigned grid = preprocess_grid(sd.n);
 #define GSR_PREV(D)                                                                                             \
     (k == 1 ? k_preprocess_fc_views<D, true> : k_preprocess_fc_views<D, false>)<<<grid, kThreads, 0, s>>>(        \
         sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, vp)

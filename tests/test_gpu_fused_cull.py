@@ -75,15 +75,11 @@ def test_group_views_of_mixed_visibility(gpu, monkeypatch):
     scene.close()
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-def test_context_alternating_key_ranges(gpu, monkeypatch, split):
+def test_context_alternating_key_ranges(gpu):
     """One context renders frames whose visible depth ranges differ (wide,
     narrow, none, wide again, ...): each frame bit-identical to a fresh
     context's render of it.  A stale key-range shard of an earlier frame that
-    counted would widen or, worse, narrow the range the depth sort keeps.
-    split = 1: frames alone in two branches (GSR_SPLIT_ALONE), whose depth
-    keys and key range come from k_depth_fc's own completion words."""
-    monkeypatch.setenv("GSR_SPLIT_ALONE", split)
+    counted would widen or, worse, narrow the range the depth sort keeps."""
     import torch
 
     from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into

@@ -11,10 +11,7 @@
 * GSR_FUSED_CULL (default 1): culling inside the preprocess, uncompacted
   slots, culled keys dropped by the depth sort's first pass, against k_cull +
   the compaction scan + k_preprocess (tests/helpers.grab_debug maps the
-  uncompacted slots to the compacted ones by rank);
-* GSR_SPLIT_ALONE (a frame alone, default 0): the depth keys first
-  (k_depth_fc), the depth sort on a side stream beside the preprocess, joined
-  before the binning, which then gathers the rects (no sort payload).
+  uncompacted slots to the compacted ones by rank).
 
 Images, records, depth order, tile lists and tile ranges must be bit-identical, on a frame rendered alone (gsr_render) and on a group of
 views (gsr_render_finish_views), for frame sizes whose tile ids take one
@@ -29,7 +26,7 @@ from helpers import batched_frames, gpu_frame
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [{}, {"GSR_BIN_FUSED": "0"}, {"GSR_TAIL_MERGE": "0", "GSR_TAIL_MERGE_ALONE": "1"},
-            {"GSR_FUSED_CULL": "0"}, {"GSR_SPLIT_ALONE": "1"}]
+            {"GSR_FUSED_CULL": "0"}]
 
 
 def _settings(**kw):
@@ -38,7 +35,7 @@ def _settings(**kw):
 
 
 def _frames(monkeypatch, env, g, scene, cams):
-    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE", "GSR_FUSED_CULL", "GSR_SPLIT_ALONE"):
+    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE", "GSR_FUSED_CULL"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
