@@ -152,3 +152,19 @@ def test_binning_mixes_staged_and_direct_blocks(gpu, monkeypatch, limit):
     got = batched_frames(scene, cams, _settings(), group=2, debug_views=(0,))
     scene.close()
     check_frame_order(got[0], vs, U)
+
+
+def test_frame_wider_than_packed_rects(gpu):
+    """A frame of more than 256 tiles across: the depth sort carries no packed
+    rect payload and the binning gathers the rects by record slot.  Only a
+    band of the scene is visible, so (fused cull, uncompacted slots) the
+    gathered slots reach past V: tile lists exactly the oracle's."""
+    g = garden_standin(100_000, seed=4, sh_degree=0)
+    cam = Camera(96, 4128).yaw(20)  # 258 x 6 tiles
+    U = uniforms_for(cam)
+    vs = O.vertex_stage(g.flat(), g.sh_dim, U)
+    nv = int(vs["visible"].sum())
+    assert 0 < nv < len(g) // 2, nv
+    res = gpu_frame(g, cam, _settings(), with_debug=True)
+    assert res["stats"]["tiles_x"] > 256
+    check_frame_order(res, vs, U)
