@@ -461,6 +461,17 @@ int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const 
 // ahead of the frame that never finishes) fails the call with GSR_ERR_HIP and
 // marks the context failed instead of spinning forever; a failed context
 // refuses further frames (destroy it).
+// The frame's tile instances must fit 32 bits (the last preprocess block
+// publishes the count's high word beside it): a scene whose splats cover that
+// many tiles fails the frame instead of overrunning the instance buffers.
+int check_instances(gsr_context* c) {
+    const uint32_t hi = __atomic_load_n(&c->host_counters[3], __ATOMIC_ACQUIRE);
+    if (hi == 0) return GSR_OK;
+    return set_error(GSR_ERR_OVERFLOW, "render: the frame has " +
+                                           std::to_string(((uint64_t)hi << 32) | c->host_counters[1]) +
+                                           " tile instances (at most 2^32 - 1)");
+}
+
 int wait_counts(gsr_context* c, hipStream_t s) {
     const uint32_t want = c->seq;
     const auto t0 = std::chrono::steady_clock::now();
@@ -1042,6 +1053,7 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     const auto h2 = std::chrono::steady_clock::now();
     const uint32_t n_vis = n > 0 ? __atomic_load_n(&c->host_counters[0], __ATOMIC_ACQUIRE) : 0u;
     const uint32_t n_dup = n > 0 ? __atomic_load_n(&c->host_counters[1], __ATOMIC_ACQUIRE) : 0u;
+    if (n > 0 && (rc = check_instances(c))) return rc;
     if (c->prof_on) prof_accumulate(c, slot ^ 1, false);
     if (n_vis > 0) c->last_depth_order = f.va;
 
@@ -1172,6 +1184,7 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         PendingFrame& f = c->pend;
         const uint32_t n_vis = f.n > 0 ? __atomic_load_n(&c->host_counters[0], __ATOMIC_ACQUIRE) : 0u;
         const uint32_t n_dup = f.n > 0 ? __atomic_load_n(&c->host_counters[1], __ATOMIC_ACQUIRE) : 0u;
+        if (f.n > 0 && (rc = check_instances(c))) return rc;
         n_vis_max = std::max(n_vis_max, n_vis);
         n_dup_max = std::max(n_dup_max, n_dup);
         if (n_vis > 0) c->last_depth_order = f.va;

@@ -618,11 +618,13 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess(const float
         const uint32_t b = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
         const unsigned long long old = atomicAdd(done_ctr, (1ull << 40) | (unsigned long long)b);
         if ((old >> 40) == (unsigned long long)(gridDim.x - 1)) {
-            const uint32_t n_dup = (uint32_t)(old & ((1ull << 40) - 1)) + b;
+            const unsigned long long d64 = (old & ((1ull << 40) - 1)) + b;
+            const uint32_t n_dup = (uint32_t)d64;
             const uint32_t n_vis = n_vis_dev[0];
             counters[1] = n_dup;
             __hip_atomic_store(host_counters + 0, n_vis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_counters + 1, n_dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_counters + 3, (uint32_t)(d64 >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_counters + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(done_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -698,11 +700,14 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_views(const
         const uint32_t b = s_cnt[threadIdx.x][0] + s_cnt[threadIdx.x][1] + s_cnt[threadIdx.x][2] + s_cnt[threadIdx.x][3];
         const unsigned long long old = atomicAdd(V.done_ctr, (1ull << 40) | (unsigned long long)b);
         if ((old >> 40) == (unsigned long long)(gridDim.x - 1)) {
-            const uint32_t n_dup = (uint32_t)(old & ((1ull << 40) - 1)) + b;
+            const unsigned long long d64 = (old & ((1ull << 40) - 1)) + b;
+            const uint32_t n_dup = (uint32_t)d64;
             const uint32_t n_vis = V.n_vis_dev[0];
             V.counters[1] = n_dup;
             __hip_atomic_store(V.host_counters + 0, n_vis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(V.host_counters + 1, n_dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(V.host_counters + 3, (uint32_t)(d64 >> 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(V.host_counters + 2, V.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(V.done_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -764,7 +769,7 @@ __device__ __forceinline__ void culled_slot(uint32_t slot, uint32_t* __restrict_
 // One frame's block results: counts and the key range of its visible
 // Gaussians.  Thread 0 only; returns true in the block that completed the grid.
 __device__ __forceinline__ bool block_done(unsigned long long* __restrict__ done_ctr, uint32_t seq, uint32_t tiles,
-                                           uint32_t nvis, uint32_t kmax, uint32_t nkmin, uint32_t& n_dup) {
+                                           uint32_t nvis, uint32_t kmax, uint32_t nkmin, unsigned long long& n_dup) {
     if (nvis) {
         const int sh = kKeyShards0 + (int)(blockIdx.x % kKeyShards);
         const unsigned long long tag = (unsigned long long)seq << 32;
@@ -782,14 +787,15 @@ __device__ __forceinline__ bool block_done(unsigned long long* __restrict__ done
         asm volatile("" ::"v"(r0), "v"(r1), "v"(r2) : "memory");
     }
     const unsigned long long old = atomicAdd(done_ctr, (1ull << 40) | (unsigned long long)tiles);
-    n_dup = (uint32_t)(old & ((1ull << 40) - 1)) + tiles;
+    n_dup = (old & ((1ull << 40) - 1)) + tiles;
     return (old >> 40) == (unsigned long long)(gridDim.x - 1);
 }
 
 // The completing block's publication, by one whole wave: the frame's key
 // range from the shards, V and D to the device counters and (V, D, seq) to
 // host-mapped memory; the counters are re-armed for the next frame.
-__device__ __forceinline__ void publish_frame(unsigned long long* __restrict__ done_ctr, uint32_t seq, uint32_t n_dup,
+__device__ __forceinline__ void publish_frame(unsigned long long* __restrict__ done_ctr, uint32_t seq,
+                                              unsigned long long n_dup64,
                                               uint32_t* __restrict__ key_range, uint32_t* __restrict__ counters,
                                               uint32_t* __restrict__ host_counters) {
     const int lane = __lane_id();
@@ -807,10 +813,14 @@ __device__ __forceinline__ void publish_frame(unsigned long long* __restrict__ d
     if (lane == 0) {
         key_range[0] = nkmin;  // {0, 0} when nothing is visible, like the scan's
         key_range[1] = kmax;
+        const uint32_t n_dup = (uint32_t)n_dup64;
         counters[0] = n_vis;
         counters[1] = n_dup;
         __hip_atomic_store(host_counters + 0, n_vis, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_counters + 1, n_dup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // instances beyond 32 bits: the host refuses the frame (GSR_ERR_OVERFLOW)
+        __hip_atomic_store(host_counters + 3, (uint32_t)(n_dup64 >> 32), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(host_counters + 2, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(done_ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -852,7 +862,8 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_fc_views(co
                                                                               int64_t n, ViewsPreFc vs) {
     static_assert(kMaxViews * 4 * (kThreads / 64) <= kThreads, "one thread per LDS word");
     __shared__ uint32_t s_red[kMaxViews][4][kThreads / 64];
-    __shared__ uint32_t s_last[kMaxViews], s_dup[kMaxViews];
+    __shared__ uint32_t s_last[kMaxViews];
+    __shared__ unsigned long long s_dup[kMaxViews];
     const int wave = threadIdx.x >> 6;
     const int lane = __lane_id();
     for (int v = 0; v < vs.k; ++v) clear_words(vs.v[v].zero_words, vs.v[v].n_zero);
@@ -906,7 +917,7 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_fc_views(co
 #pragma unroll
         for (int w = 0; w < kThreads / 64; ++w)
             t += s_red[v][0][w], nv += s_red[v][1][w], kx = max(kx, s_red[v][2][w]), kn = max(kn, s_red[v][3][w]);
-        uint32_t n_dup;
+        unsigned long long n_dup;
         s_last[v] = block_done(vs.v[v].done_ctr, vs.v[v].seq, t, nv, kx, kn, n_dup) ? 1u : 0u;
         s_dup[v] = n_dup;
     }

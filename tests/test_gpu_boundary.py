@@ -539,3 +539,36 @@ def test_finish_views_nomem_ends_every_view(gpu):
     for c in ctxs:
         c.close()
     scene.close()
+
+
+def test_instance_count_beyond_32_bits_fails_the_frame(gpu):
+    """600K splats that each cover every tile of a 1080p frame make 4.9e9 tile
+    instances: the frame fails with GSR_ERR_OVERFLOW (the count's high word is
+    published beside it) instead of overrunning the instance buffers, and the
+    context renders its next frame normally."""
+    from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into
+    g = random_scene(600_000, sh_degree=0, seed=31, extent=0.5)
+    g.scale[:] = 30.0
+    g.opacity[:] = 0.99
+    huge = HipScene.from_gaussian_data(g)
+    cam = Camera(1080, 1920)
+    st = RenderSettings(t_min=1e-4, out_layout=1)
+    ctx = HipContext()
+    out = torch.empty((1080, 1920, 3), dtype=torch.float32, device="cuda")
+    with pytest.raises(RuntimeError, match="tile instances"):
+        render_into(ctx, huge, camera_from(cam), st, out)
+    torch.cuda.synchronize()
+    huge.close()
+    small = garden_standin(20_000, seed=32, sh_degree=1)
+    scene = HipScene.from_gaussian_data(small)
+    cam2 = Camera(180, 320).yaw(30)
+    o1 = torch.empty((180, 320, 3), dtype=torch.float32, device="cuda")
+    o2 = torch.empty_like(o1)
+    render_into(ctx, scene, camera_from(cam2), st, o1)
+    fresh = HipContext()
+    render_into(fresh, scene, camera_from(cam2), st, o2)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(o1.cpu().numpy(), o2.cpu().numpy())
+    for c in (ctx, fresh):
+        c.close()
+    scene.close()
