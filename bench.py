@@ -192,6 +192,8 @@ def cpu_baseline(g, cam, seconds):
 
 
 # stage name -> kernel symbol in rocprofv3 summaries
+JSON_OUT = sys.stdout  # main() points it at the real stdout before routing fd 1 to stderr
+
 KERNEL_SYMBOL = {"composite": "k_composite<0>", "preprocess": "k_preprocess_fc_views<3, true>", "merge": "k_merge"}
 PMC_PROFILE = os.path.join(ROOT, "profiles", "LATEST")
 
@@ -367,7 +369,7 @@ def dry_run(args):
                           "views_batched": {"views_per_gpu": max(1, args.inflight), "elapsed_max_s": elapsed},
                           "c4_one_view_per_gpu": None if world == 1 else
                           {"views": [r["c4_view"] for r in ranks], "elapsed_max_s": c4_elapsed},
-                          "ranks": ranks}), flush=True)
+                          "ranks": ranks}), file=JSON_OUT, flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -415,6 +417,13 @@ def main():
         ap.error("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    # Libraries below (gloo, RCCL, HIP) may write to file descriptor 1; the
+    # driver reads ONE JSON line from stdout.  Route fd 1 to stderr and keep
+    # a private handle on the real stdout for that line.
+    global JSON_OUT
+    JSON_OUT = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     if args.dry_run:
         return dry_run(args)
 
@@ -740,7 +749,7 @@ def main():
         "per_rank": per_rank,
         "scene_gen_s": t_gen,
     }
-    print(json.dumps(res), flush=True)
+    print(json.dumps(res), file=JSON_OUT, flush=True)
     if world > 1:
         dist.destroy_process_group()
 

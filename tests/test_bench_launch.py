@@ -22,8 +22,10 @@ def _run(*args, env_extra=None, timeout=240):
 
 
 def _json_line(out):
-    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, out
+    # stdout is exactly the one JSON line: library output on fd 1 (gloo's
+    # connection messages, RCCL) goes to stderr (bench.py routes fd 1 there)
+    lines = out.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), out
     return json.loads(lines[0])
 
 
