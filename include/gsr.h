@@ -40,7 +40,9 @@ typedef enum gsr_status {
     GSR_ERR_INVALID = -1,   /* bad argument (null pointer, size, layout) */
     GSR_ERR_HIP = -2,       /* HIP runtime error (launch / alloc / copy)  */
     GSR_ERR_NOMEM = -3,     /* device allocation failed                   */
-    GSR_ERR_OVERFLOW = -4   /* a capacity would exceed 2^31 entries       */
+    GSR_ERR_OVERFLOW = -4   /* a capacity would exceed 2^31 entries, or a frame's
+                               tile instances 2^32 - 1 (the frame fails; the context
+                               renders its next one)                     */
 } gsr_status;
 
 typedef struct gsr_scene gsr_scene;      /* static Gaussian set, SoA in HBM   */
