@@ -65,3 +65,22 @@ def test_stage_variants_identical(gpu, monkeypatch, h, w, n):
         for v in range(1, len(cams)):
             np.testing.assert_array_equal(ref[1][v]["image"], group[v]["image"], err_msg=f"{env} view {v}")
     scene.close()
+
+
+def test_group_frames_repeatable(gpu):
+    """The same group rendered again gives bit-identical images.  A group's
+    tiles of several chunks are folded in-kernel by the chunk that finishes
+    last (the tail merge), reading the other chunks' partials across XCDs;
+    a stale read there shows as a few pixels (single-splat footprints) that
+    differ from one render to the next, at the bench's 1080p / 1M size."""
+    from gsviewer_amd.rasterizer import HipScene
+    h, w = 1080, 1920
+    g = garden_standin(1_000_000, seed=1, sh_degree=3)
+    scene = HipScene.from_gaussian_data(g)
+    cams = [Camera(h, w).yaw(45.0 * v) for v in range(3)]
+    ref = [f["image"] for f in batched_frames(scene, cams, _settings(), group=3)]
+    for it in range(6):
+        got = batched_frames(scene, cams, _settings(), group=3)
+        for v in range(3):
+            np.testing.assert_array_equal(got[v]["image"], ref[v], err_msg=f"repeat {it} view {v}")
+    scene.close()
