@@ -1276,7 +1276,7 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
             const uint32_t last =
                 min(nchunks - 1u, 0xffffffffu - (uint32_t)__builtin_amdgcn_readlane((int)satv, k));
             float r = 0.f, g = 0.f, b = 0.f, T = 1.f;
-            for (uint32_t c0 = 0; c0 <= last; c0 += 8) {
+            for (uint32_t c0 = 0; c0 <= last; c0 += 4) {
                 // other chunks' partials, stored `sc1` (write-through) by their
                 // waves, are read with 16-B `sc1` loads (MI355X_MICROARCH.md,
                 // inter-workgroup visibility, hand-off table row 1: sc1 stores,
@@ -1285,45 +1285,30 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                 // images differ from run to run in a few pixels.  Slots this wave
                 // does not need (past `last`, or its own chunk, in registers) load
                 // its own partial instead, then are replaced.
-                const float4* src[8];
+                const float4* src[4];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
+                for (int j = 0; j < 4; ++j) {
                     const uint32_t c = c0 + j;
                     const uint32_t cs = (c > last || c == kk) ? slot : c == 0 ? (uint32_t)tile : cbase + c - 1;
                     src[j] = partial + (size_t)cs * 256 + k * 64 + lane;
                 }
-                f32x4 u0, u1, u2, u3, u4, u5, u6, u7;
+                f32x4 u0, u1, u2, u3;
                 asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u0) : "v"(src[0]) : "memory");
                 asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u1) : "v"(src[1]) : "memory");
                 asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u2) : "v"(src[2]) : "memory");
                 asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u3) : "v"(src[3]) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u4) : "v"(src[4]) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u5) : "v"(src[5]) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u6) : "v"(src[6]) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u7) : "v"(src[7]) : "memory");
                 // the loads' results are read only after this wait (they are its operands)
-                asm volatile("s_waitcnt vmcnt(0)"
-                             : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3), "+v"(u4), "+v"(u5), "+v"(u6), "+v"(u7)
-                             :
-                             : "memory");
-                const f32x4 u[8] = {u0, u1, u2, u3, u4, u5, u6, u7};
-                float4 v[8];
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : : "memory");
+                const f32x4 u[4] = {u0, u1, u2, u3};
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
+                for (int j = 0; j < 4; ++j) {
                     const uint32_t c = c0 + j;
-                    if (c > last)
-                        v[j] = make_float4(0.f, 0.f, 0.f, 1.f);
-                    else if (c == kk)
-                        v[j] = make_float4(rg[k].x, rg[k].y, bt[k].x, bt[k].y);
-                    else
-                        v[j] = make_float4(u[j][0], u[j][1], u[j][2], u[j][3]);
-                }
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    r += T * v[j].x;
-                    g += T * v[j].y;
-                    b += T * v[j].z;
-                    T *= v[j].w;
+                    if (c > last) continue;
+                    const f32x4 v = c == kk ? f32x4{rg[k].x, rg[k].y, bt[k].x, bt[k].y} : u[j];
+                    r += T * v[0];
+                    g += T * v[1];
+                    b += T * v[2];
+                    T *= v[3];
                 }
             }
             rg[k] = f32x2{r, g};

@@ -3,7 +3,13 @@ alone (C2 view 0, t_min 1e-4), per tile and per 16x4 slice, the number of
 list records composited front to back before every pixel of the slice has
 T < t_min (the compositor's early termination), from the frame's own records
 and tile lists (gsr_debug_copy), evaluated with the compositor's interval
-form in torch (float32; statistics, not parity).
+form in torch (float32; statistics, not parity).  Beside it, the depth a
+conservative bound reaches: per record and slice, the alpha at the slice's
+four corner pixels (alpha = opacity * 2^pw with pw concave, so its minimum over
+the slice is at a corner) counts when the record's rectangle and keep interval
+cover the whole slice; the slice is known saturated once the product of
+(1 - 0.99 min-alpha) falls below t_min / 2, and with 192-record chunks every
+chunk after that one could skip the slice ("bound_*" keys).
 usage (GPU box): python tools/saturation_depth.py [out.json]"""
 import json
 import os
@@ -42,6 +48,7 @@ def main():
     col = lane % 16
     row = lane // 16
     depth_tile, slice_depths, slice_work, lens = [], [], [], []
+    bound_depths, bound_chunk_work, chunk, all_touch = [], [], 192, []
     for t in range(len(ranges)):
         b, e = ranges[t]
         L = int(e - b)
@@ -76,8 +83,31 @@ def main():
             full = sat.all(dim=1)
             idx = int(torch.nonzero(full)[0]) + 1 if bool(full.any()) else L
             touch = cov.any(dim=1)
+            # conservative bound from the slice's corner pixels
+            live_rows = px_row[::16][(px_row[::16] < H)]
+            cx0, cx1 = tx * 16, min(tx * 16 + 15, W - 1)
+            rr0, rr1 = int(live_rows.min()), int(live_rows.max())
+            full = (x0 <= cx0) & (x1 >= cx1) & (r0 <= rr0) & (r1 >= rr1)
+            amin = torch.full_like(s, 1.0)
+            okc = full.clone()
+            for ccx in (cx0, cx1):
+                for ccr in (rr0, rr1):
+                    ddx = (ccx + 0.5) - cx
+                    ddy = (H - 1 - ccr + 0.5) - cy
+                    pwc = qa * ddx * ddx + qb * ddx * ddy + qc * ddy * ddy - mid
+                    okc &= pwc.abs() <= -mid * 0.999
+                    amin = torch.minimum(amin, (s * torch.exp2(pwc)).clamp(0, 1))
+            ab = torch.where(okc, 0.99 * amin * (1 - 1e-5), torch.zeros_like(amin))
+            Tb = torch.cumprod((1 - ab).double(), dim=0)
+            hit = torch.nonzero(Tb < T_MIN / 2)
+            bidx = int(hit[0]) + 1 if len(hit) else L
+            bound_depths.append(bidx)
+            # chunks up to and including the one holding record bidx - 1 composite the slice
+            last_chunk = (bidx - 1) // chunk
+            bound_chunk_work.append(int(touch[:min(L, (last_chunk + 1) * chunk)].sum()))
             slice_depths.append(idx)
             slice_work.append(int(touch[:idx].sum()))
+            all_touch.append(int(touch.sum()))
             worst = max(worst, idx)
         depth_tile.append(worst)
     lens = np.array(lens)
@@ -93,6 +123,11 @@ def main():
         "fraction_of_instances": float(dt.sum() / lens.sum()),
         "slice_walk_records": int(np.sum(slice_work)),
         "slice_walk_fraction": float(np.sum(slice_work) / lens.sum()),
+        "all_slice_evaluations": int(sum(int(x) for x in all_touch)),
+        "bound_depth_sum": int(np.sum(bound_depths)),
+        "bound_vs_exact_depth": float(np.sum(bound_depths) / max(1, np.sum(slice_depths))),
+        "bound_chunk_slice_evaluations": int(np.sum(bound_chunk_work)),
+        "bound_chunk_fraction_of_evaluations": float(np.sum(bound_chunk_work) / max(1, sum(all_touch))),
         "deep_tiles_depth_hist": np.histogram(dt[deep], bins=[0, 192, 384, 768, 1536, 3072, 6144, 12288, 1 << 20])[0]
         .tolist(),
     }
