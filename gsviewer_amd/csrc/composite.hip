@@ -1243,14 +1243,15 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
             for (int k = 0; k < 4; ++k) p[k * 64 + lane] = make_float4(rg[k].x, rg[k].y, bt[k].x, bt[k].y);
             return;
         }
-        // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the
-        // partials are stored `sc1` (16-B vector stores that write through
-        // past the XCD's L2, so no release fence: an agent release writes back
-        // the whole L2's dirty lines, and thousands of them serialised the
-        // launch), the wave waits for them, then one agent-scope add to the
-        // tile's counter (zeroed by k_cull every frame).  The wave whose add
-        // returns nchunks - 1 is the last: after an agent-scope acquire it
-        // reads every other chunk's partial and folds the tile in chunk order.
+        // Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, hand-off
+        // table row 1): the partials are stored `sc1` (16-B vector stores that
+        // write through past the XCD's L2, so no release fence: an agent
+        // release writes back the whole L2's dirty lines, and thousands of them
+        // serialised the launch), the wave waits for them, then one
+        // agent-scope add to the tile's counter (zeroed with the frame's other
+        // zero words by the cull / preprocess).  The wave whose add returns
+        // nchunks - 1 is the last: it reads every other chunk's partial with
+        // `sc1` loads and folds the tile in chunk order.
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const f32x4 v = f32x4{rg[k].x, rg[k].y, bt[k].x, bt[k].y};
