@@ -840,6 +840,16 @@ __device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The current value of a word other workgroups update by agent-scope atomics,
+// read by an atomic (max with 0 changes nothing), which is performed at the
+// coherence point.  An agent-scope load is served by this XCD's L2, which may
+// still hold the line from an earlier load in the same launch (the other
+// chunks' saturation polls), so a fold deciding which chunks count must not
+// use one.
+__device__ __forceinline__ uint32_t ld_atomic(uint32_t* p) {
+    return __hip_atomic_fetch_max(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // readfirstlane of a float's bits (the builtin takes int: a float argument
 // would be value-converted)
 __device__ __forceinline__ float uniform_f(float v) {
@@ -1270,7 +1280,7 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         // the slices' first saturating chunks, final now (every chunk's atomics
         // completed before its counter add), read coherently (ld_atomic)
         uint32_t satv = 0;
-        if (lane < 4) satv = ld_relaxed(sat + (size_t)tile * 4 + lane);
+        if (lane < 4) satv = ld_atomic(sat + (size_t)tile * 4 + lane);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             // chunks past the first one to saturate the slice add < t_min: k_merge's bound
