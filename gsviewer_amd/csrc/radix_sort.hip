@@ -32,8 +32,8 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 // Items per thread (64-item rounds per wave) is a template parameter R: a
 // tile holds 256*R items.  Bigger tiles mean longer digit runs in the
-// scatter's writes and a smaller digit matrix; the host picks R = 8 for wide
-// digits (depth keys, up to 11 bits) and R = 16 for narrow ones (tile ids).
+// scatter's writes and a smaller digit matrix, but fewer blocks to fill the
+// chip; every sort uses R = 8 (GSR_*_R build knobs for A/B).
 // items per thread for wide digits (> 8 bits: the depth sort); build knob for A/B
 #ifndef GSR_WIDE_R
 #define GSR_WIDE_R 8
@@ -44,9 +44,12 @@ constexpr int kRWide = GSR_WIDE_R;
 #define GSR_DEPTH_R 8
 #endif
 constexpr int kRDepth = GSR_DEPTH_R;
-// items per thread for host-known <= 8-bit digits (the tile sort); build knob for A/B
+// items per thread for host-known <= 8-bit digits (the tile sort); build knob for A/B.
+// 8 since the binning took over the tile sort's first pass: its one remaining
+// pass (1.76M instances at C2) ran 1.8 us faster in 2048-item tiles than in
+// 4096 (profiles/r3_s32)
 #ifndef GSR_TILE_R
-#define GSR_TILE_R 16
+#define GSR_TILE_R 8
 #endif
 constexpr int kRTile = GSR_TILE_R;
 constexpr int kRMin = kRWide < kRDepth ? (kRWide < kRTile ? kRWide : kRTile) : (kRDepth < kRTile ? kRDepth : kRTile);
@@ -511,8 +514,9 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
     if (n > 0xffffffffull - 4 * kMinTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
     if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
         return set_error(GSR_ERR_INVALID, "radix sort: digit width out of range");
-    // measured on MI355X: 2048-item tiles for wide digits and for device-chosen
-    // widths (the depth sort), 4096 for host-known <= 8-bit digits (the tile sort)
+    // measured on MI355X: 2048-item tiles for wide digits, for device-chosen
+    // widths (the depth sort) and, since round 3's fused binning, for host-known
+    // <= 8-bit digits (the tile sort's remaining pass)
     if ((bits + passes - 1) / passes <= 8) {
         if (key_range)
             return sort_passes<kRDepth, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
