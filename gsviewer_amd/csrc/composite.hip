@@ -1596,27 +1596,34 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_views(MergeViews vs, Co
 // ---------------------------------------------------------------- unorm8 blend
 // GSR_BLEND_UNORM8: what the reference viewer's RGBA8 framebuffer holds.  GL
 // blends every fragment in draw order (back to front) with SRC_ALPHA /
-// ONE_MINUS_SRC_ALPHA and stores the result as unorm8 (renderer_ogl.py:178-180,
-// main.py:197-198), i.e. rounds after EVERY blend.  That is not associative, so
-// there are no chunks, no early termination and no merge: one wave per tile
-// walks the tile's list backwards (its lists are front to back), 4 pixels per
-// lane as in composite_chunk.  Records are in plain form (u.plain_rec: plain
-// opacity and colour, mid = 0).  The per-fragment arithmetic is the fragment
-// stage's (gau_frag.glsl:30-53) and the blend is evaluated unfused and
-// correctly rounded in the oracle's order (oracle/gl_oracle.c: n = c a + d (1 - a),
-// then q8(n) = floor(clamp(n) 255 + 0.5) / 255); the falloff is the record's
-// log2-scaled quadratic, so alpha can differ from the oracle's expf(power) by
-// an ulp, which moves a blend result across an 8-bit rounding boundary rarely.
+// ONE_MINUS_SRC_ALPHA into unorm8 storage (renderer_ogl.py:178-180,
+// main.py:197-198).  That is not associative, so there are no chunks, no early
+// termination and no merge: one wave per tile walks the tile's list backwards
+// (its lists are front to back), 4 pixels per lane as in composite_chunk.
+// Records are in plain form (u.plain_rec: plain opacity and colour, mid = 0).
+// The per-fragment arithmetic is the fragment stage's (gau_frag.glsl:30-53);
+// the blend is the RGBA8 target's fixed-point arithmetic as Mesa llvmpipe runs
+// it on the reference's own shaders (tests/golden/llvmpipe_golden.npz,
+// oracle/gl_oracle.py blend8): colour and alpha to unorm8 by
+// rint(fl32(v * 255/256) * 256), then dst = min(255, mul8(c, a) +
+// mul8(dst, 255 - a)) with the exactly rounded mul8(x, y) = x y / 255.  The
+// falloff is the record's log2-scaled quadratic, so alpha can differ from the
+// oracle's expf(power) by an ulp, which moves it across an 8-bit rounding
+// boundary rarely.
 __device__ __forceinline__ float clamp01f(float v) { return fminf(fmaxf(v, 0.f), 1.f); }
 
-__device__ __forceinline__ float q8(float v) {
-#pragma clang fp contract(off)  // plain operators: the __f*_rn intrinsics' bodies may still be fused
-    return floorf(clamp01f(v) * 255.0f + 0.5f) / 255.0f;
+__device__ __forceinline__ uint32_t to_unorm8(float v) {
+#pragma clang fp contract(off)
+    return (uint32_t)rintf((clamp01f(v) * (255.0f / 256.0f)) * 256.0f);
 }
 
-__device__ __forceinline__ float blend8(float c, float a, float d) {
-#pragma clang fp contract(off)
-    return q8(c * a + d * (1.0f - a));
+__device__ __forceinline__ uint32_t mul8(uint32_t x, uint32_t y) {
+    const uint32_t t = x * y;
+    return (t + (t >> 8) + 128u) >> 8;
+}
+
+__device__ __forceinline__ uint32_t blend8(uint32_t c, uint32_t a, uint32_t d) {
+    return min(255u, mul8(c, a) + mul8(d, 255u - a));
 }
 
 template <int FRAG>
@@ -1633,12 +1640,12 @@ __device__ __forceinline__ void composite_tile_unorm8(const int tile, const uint
     float pyw[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) pyw[k] = (float)(a.height - 1 - (row_base + 4 * k + lrow)) + 0.5f;
-    float pr[4], pg[4], pb[4];  // the framebuffer (values k / 255), cleared to the background
+    uint32_t pr[4], pg[4], pb[4];  // the framebuffer (unorm8), cleared to the background
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        pr[k] = q8(a.bg[0]);
-        pg[k] = q8(a.bg[1]);
-        pb[k] = q8(a.bg[2]);
+        pr[k] = to_unorm8(a.bg[0]);
+        pg[k] = to_unorm8(a.bg[1]);
+        pb[k] = to_unorm8(a.bg[2]);
     }
     // batches of up to 64 records, last (backmost) first
     for (uint32_t top = range.y; top > range.x; top -= min((uint32_t)kBatch, top - range.x)) {
@@ -1689,14 +1696,11 @@ __device__ __forceinline__ void composite_tile_unorm8(const int tile, const uint
                         cbl = q2.z * e;
                     }
                 }
-                cr = clamp01f(cr);
-                cg = clamp01f(cg);
-                cbl = clamp01f(cbl);
-                al = clamp01f(al);
                 if (keep) {
-                    pr[k] = blend8(cr, al, pr[k]);
-                    pg[k] = blend8(cg, al, pg[k]);
-                    pb[k] = blend8(cbl, al, pb[k]);
+                    const uint32_t a8 = to_unorm8(al);
+                    pr[k] = blend8(to_unorm8(cr), a8, pr[k]);
+                    pg[k] = blend8(to_unorm8(cg), a8, pg[k]);
+                    pb[k] = blend8(to_unorm8(cbl), a8, pb[k]);
                 }
             }
         }
@@ -1708,14 +1712,15 @@ __device__ __forceinline__ void composite_tile_unorm8(const int tile, const uint
         const int row = row_base + 4 * k + lrow;
         if (row >= a.height) continue;
         const size_t pidx = (size_t)row * a.width + x;
+        const float vr = (float)pr[k] / 255.0f, vg = (float)pg[k] / 255.0f, vb = (float)pb[k] / 255.0f;
         if (a.out_layout == 0) {
-            out[pidx] = pr[k];
-            out[plane + pidx] = pg[k];
-            out[2 * plane + pidx] = pb[k];
+            out[pidx] = vr;
+            out[plane + pidx] = vg;
+            out[2 * plane + pidx] = vb;
         } else {
-            out[3 * pidx] = pr[k];
-            out[3 * pidx + 1] = pg[k];
-            out[3 * pidx + 2] = pb[k];
+            out[3 * pidx] = vr;
+            out[3 * pidx + 1] = vg;
+            out[3 * pidx + 2] = vb;
         }
     }
 }

@@ -87,7 +87,13 @@ __device__ __forceinline__ Projected project(float x, float y, float z, const Fr
     return o;
 }
 
-// Exact integer span [p0,p1] of pixel indices p with lo <= p+0.5 < hi.
+// GL coverage of the quad's edges lo, hi (window coordinates): the vertices
+// are snapped to 8 sub-pixel bits in the frame whose pixel centres are
+// integers, L = rint((lo - 0.5) * 256), and pixel p is covered iff
+// L <= 256 p < H (the top-left rule on an axis-aligned rectangle).  That is
+// Mesa llvmpipe's rasteriser (FIXED_ORDER 8), which runs the reference's
+// shaders in tests/golden/make_gl_golden.py; oracle/gl_oracle.py pixel_span.
+// rintf rounds half to even, like the oracle's np.rint; L / 256 is exact.
 __device__ __forceinline__ void pixel_span(float lo, float hi, int limit, int& p0, int& p1) {
     if (!(lo == lo) || !(hi == hi)) {
         p0 = limit;
@@ -96,12 +102,9 @@ __device__ __forceinline__ void pixel_span(float lo, float hi, int limit, int& p
     }
     lo = fminf(fmaxf(lo, -1048576.f), 1048576.f);
     hi = fminf(fmaxf(hi, -1048576.f), 1048576.f);
-    int a = (int)ceilf(lo - 0.5f);
-    if ((float)(a - 1) + 0.5f >= lo) --a;
-    if ((float)a + 0.5f < lo) ++a;
-    int b = (int)ceilf(hi - 0.5f) - 1;
-    if ((float)(b + 1) + 0.5f < hi) ++b;
-    if ((float)b + 0.5f >= hi) --b;
+    const float L = rintf((lo - 0.5f) * 256.0f), H = rintf((hi - 0.5f) * 256.0f);
+    const int a = (int)ceilf(L * 0.00390625f);
+    const int b = (int)ceilf(H * 0.00390625f) - 1;
     p0 = min(max(a, -1), limit);
     p1 = min(max(b, -1), limit);
 }

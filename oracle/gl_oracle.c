@@ -8,9 +8,10 @@
  * ("kind": "port").  It follows, step by step:
  *   depth sort            render/renderer_ogl.py:16-26 (ascending view z; parallel radix)
  *   vertex stage          shaders/gau_vert.glsl:75-331
- *   rasterisation         GL quad coverage at pixel centres (oracle/gl_oracle.py header)
+ *   rasterisation         GL quad coverage at pixel centres, 8 sub-pixel bits (oracle/gl_oracle.py header)
  *   fragment stage        shaders/gau_frag.glsl:14-53
- *   blending              SRC_ALPHA, ONE_MINUS_SRC_ALPHA in draw order (renderer_ogl.py:178-180)
+ *   blending              SRC_ALPHA, ONE_MINUS_SRC_ALPHA in draw order (renderer_ogl.py:178-180);
+ *                         gl8: the RGBA8 target's unorm8 arithmetic as Mesa llvmpipe does it
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may load it.
  */
 #include <math.h>
@@ -43,14 +44,18 @@ static const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
                                0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
                                -0.5900435899266435f};
 
+/* GL coverage with 8 sub-pixel bits (oracle/gl_oracle.py pixel_span/snap8):
+ * snap(v) = rint((v - 0.5) * 256) in float32, pixel p covered iff
+ * snap(lo) <= 256 p < snap(hi). */
+static double snap8(float v) {
+    if (v < -1048576.0f) v = -1048576.0f;
+    if (v > 1048576.0f) v = 1048576.0f;
+    return (double)rintf((v - 0.5f) * 256.0f);
+}
+
 static void span(float lo, float hi, int limit, int* p0, int* p1) {
     if (!(lo == lo) || !(hi == hi)) { *p0 = limit; *p1 = -1; return; }
-    double l = lo, h = hi;
-    if (l < -1048576.0) l = -1048576.0;
-    if (l > 1048576.0) l = 1048576.0;
-    if (h < -1048576.0) h = -1048576.0;
-    if (h > 1048576.0) h = 1048576.0;
-    double a = ceil(l - 0.5), b = ceil(h - 0.5) - 1.0;
+    double a = ceil(snap8(lo) / 256.0), b = ceil(snap8(hi) / 256.0) - 1.0;
     if (a < -1) a = -1;
     if (a > limit) a = limit;
     if (b < -1) b = -1;
@@ -304,7 +309,12 @@ static int64_t sort_visible(const vtx_out* vo, int64_t n, int32_t* order) {
 }
 
 static inline float clamp01(float v) { return v < 0.f ? 0.f : (v > 1.f ? 1.f : v); }
-static inline float q8(float v) { return floorf(clamp01(v) * 255.0f + 0.5f) / 255.0f; }
+/* RGBA8 target arithmetic as Mesa llvmpipe performs it (oracle/gl_oracle.py
+ * to_unorm8 / mul8 / blend8). */
+static inline int to_unorm8(float v) { return (int)rintf((clamp01(v) * (255.0f / 256.0f)) * 256.0f); }
+static inline int mul8(int x, int y) { const int t = x * y; return (t + (t >> 8) + 128) >> 8; }
+static inline int blend8(int s, int a, int d) { const int n = mul8(s, a) + mul8(d, 255 - a); return n < 255 ? n : 255; }
+static inline int from_img8(float v) { return (int)(v * 255.0f + 0.5f); }
 
 /* ------------------------------------------------------------------ entry */
 /* Renders into img (H*W*3, row 0 = top).  Returns the number of visible
@@ -325,7 +335,9 @@ int64_t oracle_render(const float* flat, int64_t n, int32_t sh_dim, const oracle
     const int64_t m = sort_visible(vo, n, order);
     if (m < 0) { free(vo); free(order); return -1; }
     const int mode = u->render_mod;
-    const float bg[3] = {gl8 ? q8(u->bg[0]) : u->bg[0], gl8 ? q8(u->bg[1]) : u->bg[1], gl8 ? q8(u->bg[2]) : u->bg[2]};
+    const float bg[3] = {gl8 ? (float)to_unorm8(u->bg[0]) / 255.0f : u->bg[0],
+                         gl8 ? (float)to_unorm8(u->bg[1]) / 255.0f : u->bg[1],
+                         gl8 ? (float)to_unorm8(u->bg[2]) / 255.0f : u->bg[2]};
 #pragma omp parallel
     {
         int nt = 1, t = 0;
@@ -362,11 +374,16 @@ int64_t oracle_render(const float* flat, int64_t n, int32_t sh_dim, const oracle
                     }
                     cr = clamp01(cr); cg = clamp01(cg); cb = clamp01(cb); a = clamp01(a);
                     float* p = img + 3 * ((size_t)r * W + x);
-                    float n0 = cr * a + p[0] * (1.0f - a);
-                    float n1 = cg * a + p[1] * (1.0f - a);
-                    float n2 = cb * a + p[2] * (1.0f - a);
-                    if (gl8) { n0 = q8(n0); n1 = q8(n1); n2 = q8(n2); }
-                    p[0] = n0; p[1] = n1; p[2] = n2;
+                    if (gl8) {  /* the framebuffer holds k / 255 */
+                        const int a8 = to_unorm8(a);
+                        p[0] = (float)blend8(to_unorm8(cr), a8, from_img8(p[0])) / 255.0f;
+                        p[1] = (float)blend8(to_unorm8(cg), a8, from_img8(p[1])) / 255.0f;
+                        p[2] = (float)blend8(to_unorm8(cb), a8, from_img8(p[2])) / 255.0f;
+                    } else {
+                        p[0] = cr * a + p[0] * (1.0f - a);
+                        p[1] = cg * a + p[1] * (1.0f - a);
+                        p[2] = cb * a + p[2] * (1.0f - a);
+                    }
                 }
             }
         }

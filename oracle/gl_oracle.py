@@ -17,23 +17,34 @@ What it restates (all citations into the read-only reference snapshot):
   cleared to (0,0,0,1) (``main.py:197-198``);
 * depth sort -- ``render/renderer_ogl.py:16-26`` (ascending view z).
 
-Parity pinning: the reference has no tests and no golden images, and its GLSL
-cannot execute here (no GL driver; MI355X has no graphics pipeline).  The parts
+Parity pinning: the reference has no tests and no golden images.  Its GLSL is
+run on Mesa's llvmpipe in the build container (``oracle/gl_ref/llvmpipe_gl.c``,
+``tests/golden/make_gl_golden.py``): the framebuffers it produces pin both
+blend modes of this restatement (``tests/test_oracle_gl_golden.py``).  The parts
 of the path that are plain NumPy in the reference (``GaussianData.flat``,
 ``_sort_gaussian_cpu``, ``scale_data``, ``naive_gaussian``,
 ``convert_euler_angles_to_rotation_matrix``) are pinned by golden vectors made
 by importing the reference (``tests/golden/make_golden.py``).  The shader
-arithmetic itself is restated line by line and is "parity unpinned" against a
-real GL driver -- see DESIGN.md section "Oracle".
+arithmetic is restated line by line and checked against the llvmpipe frames
+-- see DESIGN.md section "(c) Oracle and parity".
 
 Implementation-defined GL details are fixed here (and mirrored exactly by the
 HIP kernels) as follows:
 
 * float32 everywhere, left-to-right evaluation, no fused multiply-add;
 * a pixel (window column i, window row j, origin bottom-left) is covered by a
-  splat's quad iff ``lo_x <= i+0.5 < hi_x`` and ``lo_y <= j+0.5 < hi_y`` where
-  lo/hi are the quad's window-space corners (the GL top-left fill rule for an
-  axis-aligned rectangle, without sub-pixel vertex snapping);
+  splat's quad iff ``L_x <= 256 i < H_x`` and ``L_y <= 256 j < H_y`` where
+  ``L = rint((lo - 0.5) * 256)``, ``H = rint((hi - 0.5) * 256)`` (float32
+  subtraction, round half to even) and lo/hi are the quad's window-space
+  corners: vertices snapped to 8 sub-pixel bits, then the top-left fill rule
+  of an axis-aligned rectangle.  This is llvmpipe's rasteriser (Mesa's
+  FIXED_ORDER 8, pixel centres at +0.5); 8 sub-pixel bits is also what
+  desktop GPUs use;
+* ``gl8`` blending is the RGBA8 framebuffer's fixed-point arithmetic as Mesa
+  llvmpipe performs it: the fragment colour and alpha are converted to unorm8
+  (``rint(fl32(v * 255/256) * 256)``), then
+  ``dst = min(255, mul8(src, a) + mul8(dst, 255 - a))`` with the exactly
+  rounded ``mul8(x, y) = (t + (t >> 8) + 128) >> 8``, ``t = x y``;
 * ``coordxy`` at a pixel centre is the affine interpolation of the
   per-vertex values ``position*quadwh_scr`` (all four vertices have w = 1);
 * primitives with ``|ndc.z| > 1`` are clipped away entirely (all four
@@ -346,16 +357,24 @@ def sort_back_to_front(view_z, visible=None):
 # ----------------------------------------------------------------------------
 # coverage
 # ----------------------------------------------------------------------------
+def snap8(v):
+    """Window coordinate -> fixed point with 8 sub-pixel bits in the frame whose
+    pixel centres are integers (llvmpipe ``subpixel_snap(v - 0.5)``): float32
+    subtraction, exact scaling, round half to even.  float64 result (exact)."""
+    v = np.clip(np.asarray(v, F), F(-1048576.0), F(1048576.0))
+    return np.rint((v - F(0.5)) * F(256.0)).astype(np.float64)
+
+
 def pixel_span(lo, hi, limit):
-    """Integer pixel index range [p0, p1] with lo <= p+0.5 < hi, clamped to
-    [-1, limit].  Computed exactly (float64 arithmetic on float32 inputs)."""
-    lo = np.clip(np.asarray(lo, np.float64), -1048576.0, 1048576.0)
-    hi = np.clip(np.asarray(hi, np.float64), -1048576.0, 1048576.0)
+    """Integer pixel index range [p0, p1] covered by the quad edges lo, hi:
+    ``snap8(lo) <= 256 p < snap8(hi)``, clamped to [-1, limit]."""
+    lo = np.asarray(lo, F)
+    hi = np.asarray(hi, F)
     with np.errstate(invalid="ignore"):
-        p0 = np.ceil(lo - 0.5)
-        p1 = np.ceil(hi - 0.5) - 1.0
-    p0 = np.nan_to_num(p0, nan=limit)
-    p1 = np.nan_to_num(p1, nan=-1)
+        p0 = np.ceil(snap8(lo) / 256.0)
+        p1 = np.ceil(snap8(hi) / 256.0) - 1.0
+    p0 = np.where(np.isnan(lo) | np.isnan(hi), limit, p0)
+    p1 = np.where(np.isnan(lo) | np.isnan(hi), -1, p1)
     return np.clip(p0, -1, limit).astype(np.int64), np.clip(p1, -1, limit).astype(np.int64)
 
 
@@ -417,17 +436,39 @@ def fragment(vs, g, dx, dy, mode):
     return rgb, a.astype(F), keep
 
 
+def to_unorm8(v):
+    """float -> unorm8 as llvmpipe converts a fragment output for an RGBA8
+    target (lp_build_clamped_float_to_unsigned_norm: x * 255/256 in float32,
+    then the 1/256 grid, round half to even)."""
+    t = (np.clip(np.asarray(v, F), F(0.0), F(1.0)) * F(255.0 / 256.0)).astype(F)
+    return np.rint(t.astype(np.float64) * 256.0).astype(np.int32)
+
+
+def mul8(x, y):
+    """Exactly rounded x*y/255 of two unorm8 values (Blinn's form, as
+    llvmpipe's lp_build_mul_norm)."""
+    t = x * y
+    return (t + (t >> 8) + 128) >> 8
+
+
+def blend8(src8, a8, dst8):
+    """SRC_ALPHA, ONE_MINUS_SRC_ALPHA on an RGBA8 target, integer form."""
+    return np.minimum(255, mul8(src8, a8) + mul8(dst8, 255 - a8))
+
+
 def composite(vs, U, mode="float", order=None):
     """Instanced-draw + blend restatement.  ``mode='float'`` blends in float32
-    (SURVEY Appendix A.5 mode (a)); ``mode='gl8'`` rounds to 8 bits after every
-    blend (mode (b), GL RGBA8 default framebuffer).  Returns the RGB image
-    [H, W, 3] float32 with row 0 = TOP (as ``Save Image`` writes it,
-    gs_elements_control.py:192-196, and as the CUDA boundary returns it)."""
+    (SURVEY Appendix A.5 mode (a)); ``mode='gl8'`` is the RGBA8 framebuffer
+    (mode (b)), every blend in unorm8 fixed point (``blend8``).  Returns the RGB
+    image [H, W, 3] float32 with row 0 = TOP (as ``Save Image`` writes it,
+    gs_elements_control.py:192-196, and as the CUDA boundary returns it); in
+    gl8 mode the values are k / 255."""
     W, H = U["width"], U["height"]
     rm = U["render_mod"]
-    img = np.broadcast_to(U["bg"].astype(F), (H, W, 3)).copy()
     if mode == "gl8":
-        img = np.floor(np.clip(img, 0, 1) * F(255.0) + F(0.5)) / F(255.0)
+        img = np.broadcast_to(to_unorm8(U["bg"]), (H, W, 3)).astype(np.int32).copy()
+    else:
+        img = np.broadcast_to(U["bg"].astype(F), (H, W, 3)).copy()
     if order is None:
         order = sort_back_to_front(vs["view_z"], vs["visible"])
     x0, x1, r0, r1 = splat_rects(vs, U)
@@ -445,10 +486,13 @@ def composite(vs, U, mode="float", order=None):
         rgb = np.clip(rgb, F(0.0), F(1.0)).astype(F)   # unorm colour target
         a = np.clip(a, F(0.0), F(1.0)).astype(F)
         dst = img[r0[g]:r1[g] + 1, x0[g]:x1[g] + 1]
-        new = rgb * a[..., None] + dst * (F(1.0) - a)[..., None]
         if mode == "gl8":
-            new = np.floor(np.clip(new, 0, 1) * F(255.0) + F(0.5)) / F(255.0)
-        img[r0[g]:r1[g] + 1, x0[g]:x1[g] + 1] = np.where(keep[..., None], new, dst).astype(F)
+            new = blend8(to_unorm8(rgb), to_unorm8(a)[..., None], dst)
+        else:
+            new = (rgb * a[..., None] + dst * (F(1.0) - a)[..., None]).astype(F)
+        img[r0[g]:r1[g] + 1, x0[g]:x1[g] + 1] = np.where(keep[..., None], new, dst)
+    if mode == "gl8":
+        return (img.astype(F) / F(255.0)).astype(F)
     return img.astype(F)
 
 
