@@ -466,6 +466,10 @@ def test_first_frame_on_side_stream_after_sizing(gpu, how):
             ws.fill_(0xFF)  # a stale all-ones counter would never publish (V, D, seq)
             ctx.attach_workspace(ws, n, w, h)
         s = torch.cuda.Stream()
+        if ws is not None:
+            # the all-ones fill is really there when the frame starts: the stale-counter case is exercised
+            # every time, not only when the fill happens to land first (the sizing call itself syncs nothing)
+            s.wait_stream(torch.cuda.current_stream())
         cam = Camera(h, w).yaw(yaw)
         out = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
         st = RenderSettings(out_layout=1, t_min=0.0)

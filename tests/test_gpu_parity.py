@@ -226,16 +226,23 @@ def test_aabb_and_obb_cull(gpu):
 
 
 def test_gl8_framebuffer_closeness(gpu):
-    """Against the 8-bit-per-blend GL emulation."""
+    """The float output against the RGBA8 framebuffer.
+    The framebuffer's fixed-point blend (llvmpipe's, pinned by
+    tests/golden/llvmpipe_golden.npz) rounds each of its two products to 8 bits,
+    so it drifts from the float blend by a few steps over a deep pixel: on this
+    scene the oracle's own float and gl8 frames are 99.99 % within 3/255, at
+    most 4.07/255 apart, 57.9 dB.  Bounds: 99.9 % within 3/255, none over
+    6/255, PSNR >= 50 dB."""
     g = random_scene(2500, sh_degree=3, seed=12)
     cam = Camera(120, 160)
     res = gpu_frame(g, cam, _settings())
     U = uniforms_for(cam)
     ref8 = O.composite(O.vertex_stage(g.flat(), 48, U), U, mode="gl8")
     d = np.abs(res["image"] - ref8)
-    assert (d <= 2.0 / 255).mean() >= 0.999, d.max()
+    assert (d <= 3.0 / 255 + 1e-6).mean() >= 0.999, d.max()
+    assert d.max() <= 6.0 / 255, d.max()
     mse = float((d ** 2).mean())
-    assert 10 * np.log10(1.0 / max(mse, 1e-20)) >= 45.0
+    assert 10 * np.log10(1.0 / max(mse, 1e-20)) >= 50.0
 
 
 def test_empty_and_culled_scenes(gpu):

@@ -1,14 +1,15 @@
 """GSR_BLEND_UNORM8: the reference viewer's RGBA8 framebuffer as a GPU output
-mode, against the oracle's 8-bit-per-blend emulation (oracle/gl_oracle.c
-mode "gl8": GL SRC_ALPHA / ONE_MINUS_SRC_ALPHA in draw order, every blend
-result rounded to unorm8; renderer_ogl.py:178-180, main.py:197-198).
+mode, against the oracle's RGBA8 blend (oracle/gl_oracle.c mode "gl8": GL
+SRC_ALPHA / ONE_MINUS_SRC_ALPHA in draw order in unorm8 fixed point as Mesa
+llvmpipe performs it, pinned by tests/golden/llvmpipe_golden.npz;
+renderer_ogl.py:178-180, main.py:197-198).
 
-Both sides evaluate the same blend expression unfused and correctly rounded;
-the per-fragment alpha comes from the record's log2-scaled quadratic on the
-GPU and from expf(power) in the oracle, which can differ by an ulp and then,
-rarely, move one blend result across an 8-bit rounding boundary.  So the
-check is exact equality (values k/255) on at least 99.9 % of the channels,
-at most 1e-4 of the channels off by more than one step, none by more than 4."""
+Both sides run the same integer blend on the same 8-bit colour and alpha; the
+per-fragment alpha comes from the record's log2-scaled quadratic on the GPU
+and from expf(power) in the oracle, which can differ by an ulp and then,
+rarely, move its 8-bit value by one step.  So the check is exact equality
+(values k/255) on at least 99.9 % of the channels, at most 1e-4 of the
+channels off by more than one step, none by more than 4."""
 import numpy as np
 import pytest
 import torch
