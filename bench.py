@@ -352,7 +352,7 @@ def dry_run(args):
     n = args.n or 1000
     k_coef = (deg + 1) ** 2
     g = make_scene(args.config, n, deg)[0] if rank == 0 else None
-    tensors, bcast = broadcast_scene(g, n, k_coef, "cpu")
+    packed, bcast = broadcast_scene(g, n, k_coef, "cpu")
     views = [rank + world * j for j in range(max(1, args.inflight))]
     cam0 = view_of(views[0], H, W)
     elapsed = timed_region(lambda: None, args.steps, "cpu")
@@ -361,7 +361,7 @@ def dry_run(args):
     me = dict(rank=rank, world=dist.get_world_size() if world > 1 else 1, views=views, c4_view=c4_view,
               view0_row2=[float(x) for x in cam0.get_view_matrix()[2]],
               c4_view_row2=[float(x) for x in view_of(c4_view, H, W).get_view_matrix()[2]],
-              scene_sum=float(sum(float(t.double().sum()) for t in tensors)), elapsed=elapsed)
+              scene_sum=float(packed.double().sum()), elapsed=elapsed)
     ranks = gather_objects(me, world)
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "backend": "gloo" if world > 1 else None,
@@ -410,6 +410,9 @@ def main():
                          "points_center; obb = euler(30, 15, 0) deg, +-1.5")
     ap.add_argument("--scene-order", default="given", choices=["given", "morton"],
                     help="experiment: render the scene with its Gaussians permuted into 3D Morton order")
+    ap.add_argument("--priorities", default="none", choices=["none", "first", "ladder"],
+                    help="experiment: HIP stream priorities of the group streams (first: group 0 high; "
+                         "ladder: group i gets the i-th highest priority the device offers)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank launch over gloo (no GPU, no rendering)")
     args = ap.parse_args()
@@ -479,9 +482,9 @@ def main():
         g = g[morton_order(g.xyz)]
         data_desc += ", Gaussians in 3D Morton order"
     t_gen = time.perf_counter() - t_gen
-    tensors, bcast = broadcast_scene(g, n, k_coef, dev)  # one RCCL broadcast at load (world > 1)
-    scene = HipScene(*tensors)
-    del tensors
+    packed, bcast = broadcast_scene(g, n, k_coef, dev)  # one RCCL broadcast of the packed scene at load (world > 1)
+    scene = HipScene.from_flat(packed, 3 * k_coef)
+    del packed
     cam = view_of(rank, H, W)
     camc = camera_from(cam)
     st = RenderSettings(t_min=args.t_min, out_layout=0)
@@ -501,7 +504,17 @@ def main():
     ctxs = [HipContext() for _ in range(K)]
     for c in ctxs:  # workspace sized up front: no device allocation inside any frame
         c.reserve(n, W, H)
-    streams = [torch.cuda.Stream(device=dev) for _ in range(K)]
+    prio = [0] * K
+    if args.priorities != "none":
+        lo_p, hi_p = torch.cuda.Stream.priority_range()  # (least, greatest): greatest is the most negative
+        step_ = share if share > 1 else 1
+        for i in range(0, K, step_):
+            gi = i // step_
+            if args.priorities == "first":
+                prio[i] = hi_p if gi == 0 else lo_p
+            else:
+                prio[i] = max(hi_p, lo_p - (len(range(0, K, step_)) - 1 - gi))
+    streams = [torch.cuda.Stream(device=dev, priority=prio[i]) for i in range(K)]
     outs = [torch.empty((3, H, W), dtype=torch.float32, device=dev) for _ in range(K)]
     cams = [cam] + [view_of(rank + world * j, H, W) for j in range(1, K)]
     camcs = [camera_from(c) for c in cams]

@@ -23,41 +23,51 @@ from .camera import Camera, view_for_rank
 SCENE_FIELDS = ("xyz", "rot", "scale", "opacity", "sh")
 
 
-def scene_shapes(n: int, k_coef: int) -> Tuple[Tuple[int, int], ...]:
-    """Shapes of the five scene tensors for n Gaussians with k_coef SH coefficients per channel."""
-    return ((n, 3), (n, 4), (n, 3), (n, 1), (n, 3 * k_coef))
+def record_floats(k_coef: int) -> int:
+    """Floats per Gaussian of the packed scene record, ``GaussianData.flat()``
+    (util_gau.py:40-42): xyz, rot, scale, opacity, sh = 11 + 3 k_coef."""
+    return 11 + 3 * k_coef
 
 
-def broadcast_scene(g, n: int, k_coef: int, device, src: int = 0) -> Tuple[List[torch.Tensor], Optional[dict]]:
-    """Replicate the scene on every rank.
+def broadcast_scene(g, n: int, k_coef: int, device, src: int = 0) -> Tuple[torch.Tensor, Optional[dict]]:
+    """Replicate the scene on every rank as ONE packed buffer.
 
-    Rank `src` passes its GaussianData `g`; the other ranks pass None and
-    allocate receive buffers of the agreed shapes.  Returns the five float32
-    tensors on `device`, plus the broadcast's size/time (None when single-process).
+    Rank `src` passes its GaussianData `g` and packs it into the record
+    layout the reference uploads as its SSBO (``flat()``, [n, 11 + 3 k_coef]
+    float32); the other ranks pass None and allocate a receive buffer of that
+    shape.  One ``broadcast`` of the whole buffer (RCCL over xGMI on the GPU
+    pool) replicates it; ``HipScene.from_flat`` then repacks it on each device.
+    Returns the buffer on `device` and the broadcast's size/time (None when
+    single-process).
     """
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
+    shape = (n, record_floats(k_coef))
     if rank == src:
         if g is None:
             raise ValueError("broadcast_scene: the source rank must pass the scene")
-        tensors = [torch.from_numpy(np.ascontiguousarray(getattr(g, f), dtype=np.float32)).to(device)
-                   for f in SCENE_FIELDS]
-        for t, shp in zip(tensors, scene_shapes(n, k_coef)):
-            if tuple(t.shape) != shp:
-                raise ValueError(f"broadcast_scene: tensor shape {tuple(t.shape)} != expected {shp}")
+        flat = np.ascontiguousarray(g.flat(), dtype=np.float32)
+        if flat.shape != shape:
+            raise ValueError(f"broadcast_scene: packed scene {flat.shape} != expected {shape}")
+        buf = torch.from_numpy(flat).to(device)
     else:
-        tensors = [torch.empty(shp, dtype=torch.float32, device=device) for shp in scene_shapes(n, k_coef)]
+        buf = torch.empty(shape, dtype=torch.float32, device=device)
     if world == 1:
-        return tensors, None
+        return buf, None
     _sync(device)
     dist.barrier()
     t0 = time.perf_counter()
-    for t in tensors:
-        dist.broadcast(t, src=src)
+    dist.broadcast(buf, src=src)
     _sync(device)
     dt = time.perf_counter() - t0
-    nbytes = sum(t.numel() * t.element_size() for t in tensors)
-    return tensors, dict(bytes=nbytes, seconds=dt, GBps=nbytes / max(dt, 1e-12) / 1e9)
+    nbytes = buf.numel() * buf.element_size()
+    return buf, dict(bytes=nbytes, seconds=dt, GBps=nbytes / max(dt, 1e-12) / 1e9, collectives=1)
+
+
+def unpack_scene(buf: torch.Tensor, k_coef: int):
+    """The five field views (xyz, rot, scale, opacity, sh) of a packed buffer."""
+    cuts = np.cumsum([0, 3, 4, 3, 1, 3 * k_coef])
+    return [buf[:, cuts[i]:cuts[i + 1]] for i in range(5)]
 
 
 def view_of(rank: int, height: int, width: int) -> Camera:

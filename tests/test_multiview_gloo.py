@@ -15,7 +15,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from gsviewer_amd.gaussian_data import random_scene
-from gsviewer_amd.multiview import SCENE_FIELDS, broadcast_scene, gather_objects, timed_region, view_of
+from gsviewer_amd.multiview import broadcast_scene, gather_objects, timed_region, unpack_scene, view_of
 from oracle import gl_oracle as O
 
 WORLD = 2
@@ -36,10 +36,9 @@ def _digest(tensors):
     return h.hexdigest()
 
 
-def _oracle_image(tensors, k_coef, cam):
-    """CPU oracle render of the scene held in the five tensors, for one camera."""
-    xyz, rot, scale, opac, sh = [t.numpy() for t in tensors]
-    flat = np.concatenate([xyz, rot, scale, opac, sh], 1).astype(np.float32)
+def _oracle_image(flat, k_coef, cam):
+    """CPU oracle render of the packed scene buffer, for one camera."""
+    flat = np.ascontiguousarray(flat, np.float32)
     U = O.default_uniforms(cam.get_view_matrix(), cam.get_project_matrix(),
                            np.asarray(cam.get_htanfovxy_focal(), np.float32), cam.position, cam.w, cam.h)
     return O.render(flat, 3 * k_coef, U)[0]
@@ -50,11 +49,25 @@ def _worker(rank, port, out_dir):
     try:
         k_coef = (DEG + 1) ** 2
         g = random_scene(N, sh_degree=DEG, seed=5) if rank == 0 else None
-        tensors, info = broadcast_scene(g, N, k_coef, "cpu")
-        digests = gather_objects(_digest(tensors), WORLD)
+        calls = []
+        real_broadcast = dist.broadcast
+
+        def counting_broadcast(*a, **kw):  # every collective the scene load issues
+            calls.append(tuple(a[0].shape))
+            return real_broadcast(*a, **kw)
+
+        dist.broadcast = counting_broadcast
+        try:
+            packed, info = broadcast_scene(g, N, k_coef, "cpu")
+        finally:
+            dist.broadcast = real_broadcast
+        fields = unpack_scene(packed, k_coef)
+        digests = gather_objects(_digest([packed]), WORLD)
+        collectives = gather_objects(calls, WORLD)
 
         cam = view_of(rank, H, W)
-        img = _oracle_image(tensors, k_coef, cam)
+        img = _oracle_image(packed.numpy(), k_coef, cam)
+        assert [tuple(f.shape) for f in fields] == [(N, 3), (N, 4), (N, 3), (N, 1), (N, 3 * k_coef)]
         images = gather_objects(img, WORLD)
 
         # rank 1 is slower: both ranks must report the same (max) elapsed time
@@ -63,12 +76,14 @@ def _worker(rank, port, out_dir):
         times = gather_objects(elapsed, WORLD)
 
         if rank == 0:
-            src = [torch.from_numpy(np.ascontiguousarray(getattr(g, f), dtype=np.float32)) for f in SCENE_FIELDS]
+            src = torch.from_numpy(np.ascontiguousarray(g.flat(), dtype=np.float32))
             np.savez(os.path.join(out_dir, "result.npz"),
-                     src_digest=_digest(src), digests=np.array(digests), bytes=info["bytes"],
+                     src_digest=_digest([src]), digests=np.array(digests), bytes=info["bytes"],
+                     collectives=np.array([len(c) for c in collectives]), info_collectives=info["collectives"],
+                     collective_shapes=np.array([list(c[0]) for c in collectives]),
                      img0=images[0], img1=images[1], times=np.array(times),
-                     ref0=_oracle_image(src, k_coef, view_of(0, H, W)),
-                     ref1=_oracle_image(src, k_coef, view_of(1, H, W)))
+                     ref0=_oracle_image(g.flat(), k_coef, view_of(0, H, W)),
+                     ref1=_oracle_image(g.flat(), k_coef, view_of(1, H, W)))
     finally:
         dist.destroy_process_group()
 
@@ -81,10 +96,17 @@ def result(tmp_path_factory):
 
 
 def test_broadcast_replicates_scene(result):
-    # every rank holds a bit-identical copy of rank 0's scene after ONE broadcast
+    # every rank holds a bit-identical copy of rank 0's packed scene (GaussianData.flat()) after ONE broadcast
     assert len(set(result["digests"].tolist())) == 1
     assert result["digests"][0] == result["src_digest"]
     assert int(result["bytes"]) == N * 4 * (3 + 4 + 3 + 1 + 3 * (DEG + 1) ** 2)
+
+
+def test_scene_load_is_one_collective(result):
+    # one broadcast of the packed scene buffer, on every rank, and nothing else
+    assert result["collectives"].tolist() == [1] * WORLD
+    assert int(result["info_collectives"]) == 1
+    assert result["collective_shapes"].tolist() == [[N, 11 + 3 * (DEG + 1) ** 2]] * WORLD
 
 
 def test_views_are_independent_per_rank(result):
