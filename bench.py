@@ -402,6 +402,9 @@ def main():
     ap.add_argument("--no-batched-finish", action="store_true",
                     help="with --share > 1: finish each view's frame alone instead of one launch per stage "
                          "for the group")
+    ap.add_argument("--lookahead", type=int, default=None,
+                    help="with --share > 1: at most this many groups begun and not yet finished (default: all "
+                         "groups; a group is finished when it is begun again or drained)")
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage HIP events")
     ap.add_argument("--render-mod", type=int, default=6,
                     help="render_mod uniform (experiments; 6 = SH:0~3, the reference default)")
@@ -410,9 +413,6 @@ def main():
                          "points_center; obb = euler(30, 15, 0) deg, +-1.5")
     ap.add_argument("--scene-order", default="given", choices=["given", "morton"],
                     help="experiment: render the scene with its Gaussians permuted into 3D Morton order")
-    ap.add_argument("--priorities", default="none", choices=["none", "first", "ladder"],
-                    help="experiment: HIP stream priorities of the group streams (first: group 0 high; "
-                         "ladder: group i gets the i-th highest priority the device offers)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the multi-rank launch over gloo (no GPU, no rendering)")
     args = ap.parse_args()
@@ -504,17 +504,7 @@ def main():
     ctxs = [HipContext() for _ in range(K)]
     for c in ctxs:  # workspace sized up front: no device allocation inside any frame
         c.reserve(n, W, H)
-    prio = [0] * K
-    if args.priorities != "none":
-        lo_p, hi_p = torch.cuda.Stream.priority_range()  # (least, greatest): greatest is the most negative
-        step_ = share if share > 1 else 1
-        for i in range(0, K, step_):
-            gi = i // step_
-            if args.priorities == "first":
-                prio[i] = hi_p if gi == 0 else lo_p
-            else:
-                prio[i] = max(hi_p, lo_p - (len(range(0, K, step_)) - 1 - gi))
-    streams = [torch.cuda.Stream(device=dev, priority=prio[i]) for i in range(K)]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(K)]
     outs = [torch.empty((3, H, W), dtype=torch.float32, device=dev) for _ in range(K)]
     cams = [cam] + [view_of(rank + world * j, H, W) for j in range(1, K)]
     camcs = [camera_from(c) for c in cams]
@@ -526,7 +516,7 @@ def main():
         groups = [(ctxs[g:g + share], camcs[g:g + share], outs[g:g + share], streams[g])
                   for g in range(0, K, share)]
         pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=not args.no_batched_sorts,
-                                 batched_finish=not args.no_batched_finish)
+                                 batched_finish=not args.no_batched_finish, lookahead=args.lookahead)
 
     def serial_frame():
         render_into(ctx, scene, camc, st, outs[0])

@@ -253,7 +253,65 @@ struct BinScatterLds {
     uint32_t dbase[1 << kCB];                // window-local digit offsets
     uint32_t gbase[1 << kCB];                // global position of the digit's next instance
     uint32_t scan[2][kThreads / 64];
+    uint32_t own_o[kThreads + 1];            // balanced fill: each thread's first instance, then the total
+    uint32_t wmax[kThreads / 64];
 };
+
+// A block whose splats cover more than this many tiles each is enumerated
+// balanced (instance_at): every thread takes every kThreads-th instance of
+// the block.  Otherwise each thread walks its own splats' rectangles, which
+// costs as many serial steps as its largest splat has tiles: a block of
+// large near-camera splats (they are adjacent in depth order) would run
+// almost single-lane.
+constexpr uint32_t kSerialTiles = 64;
+
+// Instance idx (generation order: depth-sorted splats, each one's tiles
+// row-major) of block blk -> (tile key, record slot), given own_o: the
+// exclusive offsets of the block's threads' instances (thread t owns splats
+// blk * kBinBlock + 4t .. 4t + 3), own_o[kThreads] = the block's total.
+template <bool kPacked>
+__device__ __forceinline__ void instance_at(uint32_t idx, const uint32_t* own_o, uint32_t blk,
+                                            const uint32_t* __restrict__ sorted_ids,
+                                            const uint2* __restrict__ trect_sorted,
+                                            const uint32_t* __restrict__ rect4_sorted, int tiles_x, uint32_t& key,
+                                            uint32_t& val) {
+    uint32_t lo = 0, hi = kThreads;  // own_o[lo] <= idx < own_o[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (own_o[mid] <= idx) lo = mid;
+        else hi = mid;
+    }
+    uint32_t local = idx - own_o[lo];
+    const uint32_t base = blk * kBinBlock + lo * kBinItems;
+    key = 0xffffffffu;
+    val = 0u;
+    // (thread lo's instances all come from its splats below n_vis, which come first)
+    for (int k = 0; k < kBinItems; ++k) {
+        const uint32_t r = base + k;
+        const uint2 tr = kPacked ? unpack_rect(rect4_sorted[r]) : trect_sorted[r];
+        const uint32_t n = rect_tiles(tr);
+        if (local < n) {
+            const uint32_t tx0 = tr.x & 0xffffu, tx1 = tr.x >> 16, ty0 = tr.y & 0xffffu;
+            const uint32_t w = tx1 - tx0 + 1u;
+            const uint32_t dy = local / w;
+            key = (ty0 + dy) * (uint32_t)tiles_x + tx0 + (local - dy * w);
+            val = sorted_ids[r];
+            return;
+        }
+        local -= n;
+    }
+}
+
+// Block-wide unsigned max (every thread gets it); scratch: kThreads / 64 words.
+__device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t* scratch) {
+    v = wave_reduce_max(v);
+    if (__lane_id() == 0) scratch[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < kThreads / 64; ++k) m = max(m, scratch[k]);
+    return m;
+}
 
 // (sorted rect of depth-sorted splat r)
 template <bool kPacked>
@@ -269,25 +327,56 @@ __device__ __forceinline__ uint2 sorted_rect(const uint32_t* __restrict__ sorted
     }
 }
 
+// Per-block digit counts.  The rects are read in the coalesced strided layout
+// (and written in depth order for the non-packed form); a block with a splat
+// over kSerialTiles tiles counts its instances balanced instead (instance_at,
+// the consecutive layout bin_scatter uses).  own: kThreads + 1 + 2 kThreads / 64
+// words of LDS.
 template <bool kPacked, int kCB>
 __device__ __forceinline__ void bin_hist(const uint32_t* __restrict__ sorted_ids, const uint2* __restrict__ trect,
                                          const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis, int tiles_x,
                                          const PassArgs& pa, uint32_t* __restrict__ hist, uint32_t nbb,
-                                         uint2* __restrict__ trect_sorted, uint32_t blk, uint32_t* h) {
+                                         uint2* __restrict__ trect_sorted, uint32_t blk, uint32_t* h,
+                                         uint32_t* own) {
     const Digit dg = digit_params(pa);
     const uint32_t radix = dg.mask + 1u;
     for (uint32_t d = threadIdx.x; d < radix; d += kThreads) h[d] = 0u;
-    __syncthreads();
     const uint32_t base = blk * kBinBlock + threadIdx.x;
+    uint2 tr[kBinItems];
+    uint32_t nmax = 0;
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
         const uint32_t r = base + k * kThreads;
-        if (r >= n_vis) continue;
-        const uint2 tr = sorted_rect<kPacked>(sorted_ids, trect, rect4_sorted, n_vis, r, trect_sorted);
-        const uint32_t tx0 = tr.x & 0xffffu, tx1 = tr.x >> 16, ty0 = tr.y & 0xffffu, ty1 = tr.y >> 16;
-        if (tx0 > tx1) continue;
-        for (uint32_t ty = ty0; ty <= ty1; ++ty)
-            for (uint32_t tx = tx0; tx <= tx1; ++tx) atomicAdd(&h[dg.of(ty * (uint32_t)tiles_x + tx)], 1u);
+        tr[k] = r < n_vis ? sorted_rect<kPacked>(sorted_ids, trect, rect4_sorted, n_vis, r, trect_sorted)
+                          : make_uint2(0xffffu, 0u);
+        nmax = max(nmax, rect_tiles(tr[k]));
+    }
+    uint32_t* own_o = own;
+    if (block_max(nmax, own + kThreads + 1) <= kSerialTiles) {  // (its barrier also orders the zeroing of h)
+#pragma unroll
+        for (int k = 0; k < kBinItems; ++k) {
+            const uint32_t tx0 = tr[k].x & 0xffffu, tx1 = tr[k].x >> 16, ty0 = tr[k].y & 0xffffu, ty1 = tr[k].y >> 16;
+            if (tx0 > tx1) continue;
+            for (uint32_t ty = ty0; ty <= ty1; ++ty)
+                for (uint32_t tx = tx0; tx <= tx1; ++tx) atomicAdd(&h[dg.of(ty * (uint32_t)tiles_x + tx)], 1u);
+        }
+    } else {
+        // thread t's instances in the consecutive layout: splats blk * kBinBlock + 4t .. 4t + 3
+        const uint32_t cb = blk * kBinBlock + threadIdx.x * kBinItems;
+        uint32_t sc = 0;
+#pragma unroll
+        for (int k = 0; k < kBinItems; ++k)
+            if (cb + k < n_vis) sc += rect_tiles(kPacked ? unpack_rect(rect4_sorted[cb + k]) : trect_sorted[cb + k]);
+        uint32_t total;
+        const uint32_t o = block_exclusive<kThreads>(sc, own + kThreads + 1 + kThreads / 64, total);
+        own_o[threadIdx.x] = o;
+        if (threadIdx.x == kThreads - 1) own_o[kThreads] = total;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < total; i += kThreads) {
+            uint32_t key, val;
+            instance_at<kPacked>(i, own_o, blk, sorted_ids, trect_sorted, rect4_sorted, tiles_x, key, val);
+            atomicAdd(&h[dg.of(key)], 1u);
+        }
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < radix; d += kThreads) hist[(size_t)d * nbb + blk] = h[d];
@@ -300,8 +389,9 @@ __global__ __launch_bounds__(kThreads) void k_bin_hist(const uint32_t* __restric
                                                        int tiles_x, PassArgs pa, uint32_t* __restrict__ hist,
                                                        uint32_t nbb, uint2* __restrict__ trect_sorted) {
     __shared__ uint32_t h[1 << kCB];
+    __shared__ uint32_t own[kThreads + 1 + 2 * kThreads / 64];
     bin_hist<kPacked, kCB>(sorted_ids, trect, rect4_sorted, n_vis, tiles_x, pa, hist, nbb, trect_sorted, blockIdx.x,
-                           h);
+                           h, own);
 }
 
 template <bool kPacked, int kCB>
@@ -360,9 +450,23 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
     }
     uint32_t total;
     const uint32_t o = block_exclusive<kThreads>(s, L.scan[1], total);  // (its barrier publishes gbase)
+    uint32_t nmax = 0;
+#pragma unroll
+    for (int k = 0; k < kBinItems; ++k) nmax = max(nmax, rect_tiles(tr[k]));
+    const bool balanced = block_max(nmax, L.wmax) > kSerialTiles;
+    if (balanced) {
+        L.own_o[threadIdx.x] = o;
+        if (threadIdx.x == 0) L.own_o[kThreads] = total;
+        __syncthreads();
+    }
     for (uint32_t c0 = 0; c0 < total; c0 += (uint32_t)kBinStage) {
         // 1. this window's instances, in generation order
-        if (o < c0 + (uint32_t)kBinStage && o + s > c0) {
+        if (balanced) {
+            const uint32_t cnt = min((uint32_t)kBinStage, total - c0);
+            for (uint32_t j = threadIdx.x; j < cnt; j += kThreads)
+                instance_at<kPacked>(c0 + j, L.own_o, blk, sorted_ids, trect_sorted, rect4_sorted, tiles_x, L.k[j],
+                                     L.v[j]);
+        } else if (o < c0 + (uint32_t)kBinStage && o + s > c0) {
             uint32_t idx = o;
 #pragma unroll
             for (int k = 0; k < kBinItems; ++k) {
@@ -490,9 +594,10 @@ template <bool kPacked, int kCB>
 __global__ __launch_bounds__(kThreads) void k_bin_hist_views(BinSortViews vs, int tiles_x, PassArgs pa,
                                                              uint32_t nbb) {
     __shared__ uint32_t h[1 << kCB];
+    __shared__ uint32_t own[kThreads + 1 + 2 * kThreads / 64];
     const BinView& v = vs.v[blockIdx.y];
     bin_hist<kPacked, kCB>(v.sorted_ids, v.trect, v.rect4_sorted, v.n_vis, tiles_x, pa, vs.hist[blockIdx.y], nbb,
-                           v.trect_sorted, blockIdx.x, h);
+                           v.trect_sorted, blockIdx.x, h, own);
 }
 
 template <bool kPacked, int kCB>

@@ -169,13 +169,18 @@ class ViewBatchPipeline:
     batched_sorts / batched_finish=False use the per-view calls instead.  drain() finishes every pending frame.  Images
     are identical to rendering each view alone (tests/test_gpu_multiview.py)."""
 
-    def __init__(self, groups, scene, settings, batched_sorts=True, batched_finish=True):
+    def __init__(self, groups, scene, settings, batched_sorts=True, batched_finish=True, lookahead=None):
         assert len(groups) >= 1
         self.groups = groups
         self.scene, self.settings = scene, settings
         self.batched_sorts = batched_sorts  # the group's depth sorts in one launch per radix step
         self.batched_finish = batched_finish  # the group's second halves in one launch per stage
+        # at most `lookahead` groups begun and not finished: a step that begins a
+        # group finishes the oldest pending ones beyond that (None: all groups,
+        # i.e. a group is finished only when it is begun again or drained)
+        self.lookahead = len(groups) if lookahead is None else max(1, min(int(lookahead), len(groups)))
         self.pending = [False] * len(groups)
+        self.order = []  # pending groups, oldest first
         self.next = 0
 
     @property
@@ -191,6 +196,7 @@ class ViewBatchPipeline:
             for c in ctxs:
                 render_finish(c, stream)
         self.pending[gi] = False
+        self.order.remove(gi)
 
     def step(self):
         from .rasterizer import render_begin_sort, render_begin_sorts, render_begin_views
@@ -206,8 +212,10 @@ class ViewBatchPipeline:
             for c in ctxs:
                 render_begin_sort(c, stream)
         self.pending[gi] = True
+        self.order.append(gi)
+        while len(self.order) > self.lookahead:
+            self._finish(self.order[0])
 
     def drain(self):
-        for gi, p in enumerate(self.pending):
-            if p:
-                self._finish(gi)
+        while self.order:
+            self._finish(self.order[0])
