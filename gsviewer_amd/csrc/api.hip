@@ -165,6 +165,10 @@ struct gsr_context {
     bool first_major = true;                      // ... every tile's first chunk before any later one
     bool first_major_alone = false;               // the same for a frame finished alone (gsr_render_finish)
     bool bin_fused = true;                        // the tile sort's pass 0 fused into the binning (k_bin_scatter)
+    bool tail_merge_group = true;                 // a group's multi-chunk tiles folded in the compositing launch
+    bool tail_merge_alone = false;                // ... and a frame alone's (else k_merge)
+    uint32_t bin_stage_limit = 0xffffffffu;       // blocks of at most this many instances stage them (build cap)
+    uint32_t debug_handoff = 0;                   // tail-merge test knob (GSR_DEBUG_HANDOFF; 0 in production)
     bool fused_cull = true;                       // culling inside the preprocess (launch_preprocess_fc)
     int depth_passes_alone = kDepthPassesAlone;   // depth sort passes of gsr_render's frames
     int depth_passes_now = 0;                     // this frame's (0: kDepthPasses)
@@ -695,6 +699,13 @@ int gsr_context_create(gsr_context** out) {
     if (const char* e = std::getenv("GSR_FIRST_MAJOR_ALONE"))
         (*out)->first_major_alone = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_VIEWS_INTERLEAVE")) (*out)->views_interleave = std::strtol(e, nullptr, 10) != 0;
+    // stage forms and test knobs, read once here so that every launch of a frame sees the same value
+    if (const char* e = std::getenv("GSR_TAIL_MERGE")) (*out)->tail_merge_group = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("GSR_TAIL_MERGE_ALONE"))
+        (*out)->tail_merge_alone = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("GSR_BIN_STAGE_LIMIT"))
+        (*out)->bin_stage_limit = gsr::clamp_stage_limit(std::strtol(e, nullptr, 10));
+    if (const char* e = std::getenv("GSR_DEBUG_HANDOFF")) (*out)->debug_handoff = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("GSR_WAIT_TIMEOUT_MS")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1) (*out)->wait_timeout_ms = v;
@@ -1076,7 +1087,7 @@ int gsr_render_finish(gsr_context* c, void* stream) {
                                        c->tvals_a.p, s);
         else
             rc = launch_binning(f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, u.tiles_x, c->bin_tmp.p,
-                                c->trect_sorted.p, c->tkeys_a.p, c->tvals_a.p, s);
+                                c->trect_sorted.p, c->tkeys_a.p, c->tvals_a.p, c->bin_stage_limit, s);
         if (rc) return rc;
     }
     if ((rc = prof_record(c, slot, EV_COUNTS, s))) return rc;
@@ -1114,11 +1125,11 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
         if ((rc = launch_composite(c->chunk_desc.p, c->chunk_order.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
                                    sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.t_min, f.bg,
-                                   f.out_layout, f.out, c->partial.p, c->tmax.p, s)))
+                                   f.out_layout, f.out, c->partial.p, c->tmax.p, c->tail_merge_alone, s)))
             return rc;
         if ((rc = prof_record(c, slot, EV_COMPOSITE, s))) return rc;
         if ((rc = launch_merge(c->chunk_cnt.p, c->chunk_base.p, c->partial.p, sat, u, f.t_min, f.bg, f.out_layout,
-                               f.out, s)))
+                               f.out, c->tail_merge_alone, s)))
             return rc;
     }
     if ((rc = prof_record(c, slot, EV_COUNT, s))) return rc;
@@ -1232,7 +1243,7 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
     }
     if (n_vis_max > 0 && n_dup_max > 0) {
         rc = fused ? launch_binning_sorted_views(fv, hist, ttot, k, u0.tiles_x, tbits, tpasses, s)
-                   : launch_binning_views(fv, k, u0.tiles_x, s);
+                   : launch_binning_views(fv, k, u0.tiles_x, c0->bin_stage_limit, s);
         if (rc) return rc;
     }
     if (n_dup_max > 0 && tbits > 0 &&
@@ -1262,16 +1273,18 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         // never reallocates inside a profiled region
         uint64_t* stamps = nullptr;
         const size_t blocks = composite_views_blocks((uint32_t)max_chunks, k);
+        const size_t words = blocks * (1 + (size_t)composite_views_waves_per_block());  // block starts + wave ends
         if (c0->prof_group) {
-            if (!c0->stamps.p && (rc = c0->stamps.ensure(kSpanLaunches * blocks * 5, "stamps"))) return rc;
-            if (c0->stamp_used + blocks * 5 <= c0->stamps.cap) {
+            if (!c0->stamps.p && (rc = c0->stamps.ensure(kSpanLaunches * words, "stamps"))) return rc;
+            if (c0->stamp_used + words <= c0->stamps.cap) {
                 stamps = c0->stamps.p + c0->stamp_used;
                 c0->spans.emplace_back(c0->stamp_used, blocks);
-                c0->stamp_used += blocks * 5;
+                c0->stamp_used += words;
             }
         }
         if ((rc = launch_composite_views(fv, k, (uint32_t)max_chunks, c0->len_classes, c0->first_major, c0->views_interleave, u0,
-                                         frag_class_of(u0.render_mod), f0.t_min, f0.bg, f0.out_layout, s, stamps)))
+                                         frag_class_of(u0.render_mod), f0.t_min, f0.bg, f0.out_layout,
+                                         c0->tail_merge_group, c0->debug_handoff, s, stamps)))
             return rc;
         if (c0->prof_group) {
             GSR_HIP_CHECK(hipEventRecord(c0->evg[gslot][1], s));
@@ -1279,7 +1292,8 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
             c0->evg_views[gslot] = k;
             c0->evg_slot = gslot ^ 1;
         }
-        if ((rc = launch_merge_views(fv, k, u0, f0.t_min, f0.bg, f0.out_layout, s))) return rc;
+        if ((rc = launch_merge_views(fv, k, u0, f0.t_min, f0.bg, f0.out_layout, c0->tail_merge_group, s)))
+            return rc;
     }
     const auto h3 = std::chrono::steady_clock::now();
     using ms = std::chrono::duration<double, std::milli>;
@@ -1359,7 +1373,8 @@ int gsr_context_group_times(gsr_context* c, double* composite_ms, int64_t* launc
                 const uint64_t* b = st.data() + sp.first;
                 uint64_t lo = ~0ull, hi = 0;
                 for (size_t i = 0; i < sp.second; ++i) lo = std::min(lo, b[i]);
-                for (size_t i = 0; i < 4 * sp.second; ++i) hi = std::max(hi, b[sp.second + i]);
+                const size_t waves = (size_t)composite_views_waves_per_block() * sp.second;
+                for (size_t i = 0; i < waves; ++i) hi = std::max(hi, b[sp.second + i]);
                 sum += hi > lo ? hi - lo : 0;
             }
             *span_ms = (double)sum * 1e-5;  // 100 MHz constant clock

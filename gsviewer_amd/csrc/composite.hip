@@ -37,16 +37,10 @@ constexpr int kBinBlock = kThreads * kBinItems;  // 1024
 #endif
 constexpr int kBinStage = GSR_BIN_STAGE;
 
-// Blocks of at most this many instances take the staged write (default and
-// upper bound kBinStage; GSR_BIN_STAGE_LIMIT lowers it, read per launch, so a
-// test can make one frame mix staged and direct blocks).
-uint32_t bin_stage_limit() {
-    if (const char* e = std::getenv("GSR_BIN_STAGE_LIMIT")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v >= 0 && v < kBinStage) return (uint32_t)v;
-    }
-    return (uint32_t)kBinStage;
-}
+// Blocks of at most stage_limit instances take the staged write (default and
+// upper bound kBinStage; the context's GSR_BIN_STAGE_LIMIT, read at creation,
+// lowers it so a test can make one frame mix staged and direct blocks).
+uint32_t clamp_stage_limit(long v) { return (v >= 0 && v < kBinStage) ? (uint32_t)v : (uint32_t)kBinStage; }
 
 __device__ __forceinline__ uint32_t rect_tiles(uint2 tr) {
     const uint32_t tx0 = tr.x & 0xffffu, tx1 = tr.x >> 16, ty0 = tr.y & 0xffffu, ty1 = tr.y >> 16;
@@ -668,7 +662,7 @@ struct CompositeArgs {
     float bg[3];
     int out_layout;
     int tail_merge;  // a multi-chunk tile's last chunk to finish folds the tile (no merge launch)
-    uint32_t pos_begin, pos_end;  // k_composite: the dispatch positions [pos_begin, pos_end) of this launch
+    uint32_t debug_handoff;  // test knob (GSR_DEBUG_HANDOFF, 0 in production): see composite_chunk's tail merge
 };
 
 constexpr int kBatch = 64;  // records staged per wave per LDS batch
@@ -1120,6 +1114,27 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         live &= ~__builtin_amdgcn_readfirstlane(dead);
     }
 #endif
+    if (a.debug_handoff && nchunks > 1 && kk == 0) {
+        // Test knob (tests/test_gpu_handoff.py), chunk 0 of a multi-chunk tile,
+        // before any other chunk can have finished: bit 1 polls the tile's
+        // saturation words (agent-scope loads, as the later chunks' polls do),
+        // bit 2 plain-loads the other chunks' partial slots, so this XCD's L2
+        // holds those lines with their old contents when chunk 0 folds.
+        float junk = 0.f;
+        if (a.debug_handoff & 2u) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) junk += __uint_as_float(ld_relaxed(my_sat + k));
+        }
+        if (a.debug_handoff & 4u) {
+            const uint32_t cb = chunk_base[tile];
+            for (uint32_t c = 1; c < nchunks; ++c) {
+                const float4* q = partial + (size_t)(cb + c - 1) * 256;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) junk += q[k * 64 + lane].w;
+            }
+        }
+        asm volatile("" ::"v"(junk));
+    }
 #ifdef GSR_COMP_STATS
     uint32_t st_evals = 0, st_wasted = 0, st_records = 0;
 #endif
@@ -1374,6 +1389,13 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t old = 0;
+        if ((a.debug_handoff & 1u) && kk == 0 && lane == 0) {
+            // test knob: chunk 0 adds last (waits for the other chunks' adds; 0.2 s bound)
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (ld_atomic(sat + 4 * (size_t)a.num_tiles + tile) < nchunks - 1u &&
+                   __builtin_amdgcn_s_memrealtime() - t0 < 20000000ull)
+                __builtin_amdgcn_s_sleep(4);
+        }
         if (lane == 0)
             old = __hip_atomic_fetch_add(sat + 4 * (size_t)a.num_tiles + tile, 1u, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
@@ -1385,7 +1407,11 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         // the slices' first saturating chunks, final now (every chunk's atomics
         // completed before its counter add), read coherently (ld_atomic)
         uint32_t satv = 0;
+#ifdef GSR_TAIL_REVERT_SAT_ATOMIC  // verification build: the pre-8352f97 read (tests/test_gpu_handoff.py)
+        if (lane < 4) satv = ld_relaxed(sat + (size_t)tile * 4 + lane);
+#else
         if (lane < 4) satv = ld_atomic(sat + (size_t)tile * 4 + lane);
+#endif
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             // chunks past the first one to saturate the slice add < t_min: k_merge's bound
@@ -1409,12 +1435,19 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                     src[j] = partial + (size_t)cs * 256 + k * 64 + lane;
                 }
                 f32x4 u0, u1, u2, u3;
+#ifdef GSR_TAIL_REVERT_SC1_LOADS  // verification build: the pre-f4e3b53 plain loads (tests/test_gpu_handoff.py)
+                u0 = *reinterpret_cast<const f32x4*>(src[0]);
+                u1 = *reinterpret_cast<const f32x4*>(src[1]);
+                u2 = *reinterpret_cast<const f32x4*>(src[2]);
+                u3 = *reinterpret_cast<const f32x4*>(src[3]);
+#else
                 asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u0) : "v"(src[0]) : "memory");
                 asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u1) : "v"(src[1]) : "memory");
                 asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u2) : "v"(src[2]) : "memory");
                 asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(u3) : "v"(src[3]) : "memory");
                 // the loads' results are read only after this wait (they are its operands)
                 asm volatile("s_waitcnt vmcnt(0)" : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : : "memory");
+#endif
                 const f32x4 u[4] = {u0, u1, u2, u3};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -1482,8 +1515,8 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
                                                         const uint32_t* __restrict__ chunk_base) {
     __shared__ float4 lds[kCompWaves][kBatch * 3];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t pos = a.pos_begin + blockIdx.x * kCompWaves + wave;
-    if (pos >= min(a.pos_end, (uint32_t)a.num_tiles + n_chunks_dev[0])) return;  // device count of extra chunks
+    const uint32_t pos = blockIdx.x * kCompWaves + wave;
+    if (pos >= (uint32_t)a.num_tiles + n_chunks_dev[0]) return;  // device count of extra chunks
     const uint32_t slot = order[pos];
 #ifdef GSR_COMP_TRACE
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
@@ -1867,7 +1900,8 @@ size_t bin_tmp_elems(size_t n_vis) { return (n_vis + kBinBlock - 1) / kBinBlock 
 
 int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted, uint32_t n_vis,
                    int tiles_x, uint32_t* tmp, uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals,
-                   hipStream_t s) {
+                   uint32_t stage_limit, hipStream_t s) {
+    stage_limit = std::min(stage_limit, (uint32_t)kBinStage);
     if (n_vis == 0) return GSR_OK;
     const uint32_t nb = (n_vis + kBinBlock - 1) / kBinBlock;
     if (rect4_sorted)
@@ -1877,10 +1911,10 @@ int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_
     GSR_LAUNCH_CHECK("bin_reduce");
     if (rect4_sorted)
         k_bin_write<true><<<nb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tmp, tiles_x,
-                                                  tile_keys, tile_vals, bin_stage_limit());
+                                                  tile_keys, tile_vals, stage_limit);
     else
         k_bin_write<false><<<nb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tmp, tiles_x,
-                                                   tile_keys, tile_vals, bin_stage_limit());
+                                                   tile_keys, tile_vals, stage_limit);
     GSR_LAUNCH_CHECK("bin_write");
     return GSR_OK;
 }
@@ -1934,21 +1968,17 @@ int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
     return GSR_OK;
 }
 
-// Multi-chunk tiles folded by their last chunk inside the compositing launch.
-// A group's frames (3072-instance chunks: few multi-chunk tiles) do it by
-// default, which drops one launch per group (GSR_TAIL_MERGE=0: k_merge_views).
-// A frame alone (192-instance chunks: ~2500 multi-chunk tiles at C2) keeps
-// k_merge: a deep tile's last chunk folding ~40 partials alone put the fold on
-// the launch's tail, composite 120 -> 170 us (profiles/r3_s9); its four waves
-// per tile in k_merge take 15 (GSR_TAIL_MERGE_ALONE=1 to A/B).
-bool env_flag(const char* name, bool dflt) {
-    const char* e = std::getenv(name);
-    return e ? std::strtol(e, nullptr, 10) != 0 : dflt;
-}
-bool tail_merge_on(bool group) { return group ? env_flag("GSR_TAIL_MERGE", true) : env_flag("GSR_TAIL_MERGE_ALONE", false); }
-
+// Multi-chunk tiles folded by their last chunk inside the compositing launch
+// (tail_merge): a group's frames (3072-instance chunks: few multi-chunk tiles)
+// do it by default, which drops one launch per group (the context's
+// GSR_TAIL_MERGE=0: k_merge_views).  A frame alone (192-instance chunks: ~2500
+// multi-chunk tiles at C2) keeps k_merge: a deep tile's last chunk folding ~40
+// partials alone put the fold on the launch's tail, composite 120 -> 170 us
+// (profiles/r3_s9); its four waves per tile in k_merge take 15
+// (GSR_TAIL_MERGE_ALONE=1 to A/B).  The flags are read once, at context
+// creation, and the compositing and merge launches of a frame get the same one.
 static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float* bg, int out_layout,
-                               bool group = false) {
+                               bool tail_merge = false, uint32_t debug_handoff = 0) {
     CompositeArgs a;
     a.width = u.width;
     a.height = u.height;
@@ -1959,9 +1989,8 @@ static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float*
     a.bg[1] = bg[1];
     a.bg[2] = bg[2];
     a.out_layout = out_layout;
-    a.tail_merge = tail_merge_on(group) ? 1 : 0;
-    a.pos_begin = 0u;
-    a.pos_end = 0xffffffffu;
+    a.tail_merge = tail_merge ? 1 : 0;
+    a.debug_handoff = tail_merge ? debug_handoff : 0u;
     return a;
 }
 
@@ -1996,13 +2025,10 @@ int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n
                      const uint32_t* chunk_cnt,
                      const uint32_t* chunk_base, uint32_t* sat, const uint32_t* tile_vals, const SplatRec* recs,
                      const FrameUniforms& u, int frag_class, float t_min, const float* bg, int out_layout, float* out,
-                     float4* partial, float4* tmax, hipStream_t s, uint32_t pos_begin, uint32_t pos_end) {
-    CompositeArgs a = make_args(u, t_min, bg, out_layout);
-    a.pos_begin = pos_begin;
-    a.pos_end = pos_end;
-    const uint32_t last = std::min(max_chunks, pos_end);
-    if (last <= pos_begin) return GSR_OK;
-    const unsigned grid = (unsigned)((last - pos_begin + kCompWaves - 1) / kCompWaves);
+                     float4* partial, float4* tmax, bool tail_merge, hipStream_t s) {
+    const CompositeArgs a = make_args(u, t_min, bg, out_layout, tail_merge);
+    if (max_chunks == 0) return GSR_OK;
+    const unsigned grid = (unsigned)((max_chunks + kCompWaves - 1) / kCompWaves);
     switch (frag_class) {
         case kFragGauss:
             k_composite<kFragGauss><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial, sat,
@@ -2045,16 +2071,18 @@ int launch_composite_unorm8(const uint2* ranges, const uint32_t* tile_list, cons
 }
 
 int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const float4* partial, const uint32_t* sat,
-                 const FrameUniforms& u, float t_min, const float* bg, int out_layout, float* out, hipStream_t s) {
+                 const FrameUniforms& u, float t_min, const float* bg, int out_layout, float* out, bool tail_merge,
+                 hipStream_t s) {
+    if (tail_merge) return GSR_OK;  // the compositing launch folded its multi-chunk tiles
     const CompositeArgs a = make_args(u, t_min, bg, out_layout);
-    if (a.tail_merge) return GSR_OK;  // the compositing launch folded its multi-chunk tiles
     k_merge<<<(unsigned)a.num_tiles, kMergeThreads, 0, s>>>(chunk_cnt, chunk_base, partial, sat, a, out);
     GSR_LAUNCH_CHECK("merge");
     return GSR_OK;
 }
 
 // ------------------------------------------------------------ groups of views
-int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s) {
+int launch_binning_views(FinishView* views, int k, int tiles_x, uint32_t stage_limit, hipStream_t s) {
+    stage_limit = std::min(stage_limit, (uint32_t)kBinStage);
     BinViews bv{};
     uint32_t nb[kMaxViews];
     uint32_t nb_max = 0;
@@ -2075,9 +2103,9 @@ int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s) {
         k_bin_reduce_views<false><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv);
     GSR_LAUNCH_CHECK("bin_reduce_views");
     if (packed)
-        k_bin_write_views<true><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x, bin_stage_limit());
+        k_bin_write_views<true><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x, stage_limit);
     else
-        k_bin_write_views<false><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x, bin_stage_limit());
+        k_bin_write_views<false><<<dim3(nb_max, (unsigned)k), kThreads, 0, s>>>(bv, tiles_x, stage_limit);
     GSR_LAUNCH_CHECK("bin_write_views");
     return GSR_OK;
 }
@@ -2164,8 +2192,8 @@ int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk,
 
 int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32_t classes, bool first_major,
                            bool interleave, const FrameUniforms& u, int frag_class, float t_min, const float* bg,
-                           int out_layout, hipStream_t s, uint64_t* stamps) {
-    const CompositeArgs a = make_args(u, t_min, bg, out_layout, true);
+                           int out_layout, bool tail_merge, uint32_t debug_handoff, hipStream_t s, uint64_t* stamps) {
+    const CompositeArgs a = make_args(u, t_min, bg, out_layout, tail_merge, debug_handoff);
     CompViews cv{};
     for (int i = 0; i < k; ++i) {
         const FinishView& f = views[i];
@@ -2192,10 +2220,12 @@ size_t composite_views_blocks(uint32_t max_chunks, int k) {
     return (size_t)((max_chunks + kCompWaves - 1) / kCompWaves) * (size_t)k;
 }
 
+int composite_views_waves_per_block() { return kCompWaves; }
+
 int launch_merge_views(FinishView* views, int k, const FrameUniforms& u, float t_min, const float* bg,
-                       int out_layout, hipStream_t s) {
-    const CompositeArgs a = make_args(u, t_min, bg, out_layout, true);
-    if (a.tail_merge) return GSR_OK;  // the compositing launch folded its multi-chunk tiles
+                       int out_layout, bool tail_merge, hipStream_t s) {
+    if (tail_merge) return GSR_OK;  // the compositing launch folded its multi-chunk tiles
+    const CompositeArgs a = make_args(u, t_min, bg, out_layout);
     MergeViews mv{};
     for (int i = 0; i < k; ++i) {
         const FinishView& f = views[i];

@@ -406,9 +406,11 @@ size_t bin_tmp_elems(size_t n_vis);
 // trect_sorted: n_vis uint2 of scratch (the rects in depth order)
 // rect4_sorted (nullable): the packed rects in depth order (the depth sort's
 // payload); else the rects are gathered by id from trect
+// stage_limit: blocks with at most this many instances stage them in LDS (capped at the build's kBinStage)
+uint32_t clamp_stage_limit(long v);
 int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted, uint32_t n_vis,
                    int tiles_x, uint32_t* tmp, uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals,
-                   hipStream_t s);
+                   uint32_t stage_limit, hipStream_t s);
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
                        hipStream_t s);
 // The binning with the tile sort's first radix pass fused in (composite.hip,
@@ -435,15 +437,16 @@ int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n
                      const uint32_t* chunk_cnt, const uint32_t* chunk_base, uint32_t* sat,
                      const uint32_t* tile_vals, const SplatRec* recs, const FrameUniforms& u,
                      int frag_class, float t_min, const float* bg, int out_layout, float* out,
-                     float4* partial, float4* tmax, hipStream_t s, uint32_t pos_begin = 0,
-                     uint32_t pos_end = 0xffffffffu);
+                     float4* partial, float4* tmax, bool tail_merge, hipStream_t s);
 // GSR_BLEND_UNORM8: one wave per tile, back to front, 8-bit rounding after every blend
 int launch_composite_unorm8(const uint2* ranges, const uint32_t* tile_list, const SplatRec* recs,
                             const FrameUniforms& u, int frag_class, const float* bg, int out_layout, float* out,
                             hipStream_t s);
 // k_merge: folds the partials of multi-chunk tiles into `out` (after launch_composite)
+// (tail_merge: the compositing launch folded the tiles; nothing is launched)
 int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const float4* partial, const uint32_t* sat,
-                 const FrameUniforms& u, float t_min, const float* bg, int out_layout, float* out, hipStream_t s);
+                 const FrameUniforms& u, float t_min, const float* bg, int out_layout, float* out, bool tail_merge,
+                 hipStream_t s);
 
 // The second half of a group of views' frames (gsr_render_finish_views): each
 // stage is one launch for the whole group (view = blockIdx.y); grids cover the
@@ -473,7 +476,7 @@ struct FinishView {
     float4* partial;
 };
 // binning: bin_tmp of each view holds its per-block instance counts
-int launch_binning_views(FinishView* views, int k, int tiles_x, hipStream_t s);
+int launch_binning_views(FinishView* views, int k, int tiles_x, uint32_t stage_limit, hipStream_t s);
 // ... and with the tile sort's pass 0 fused in (hist[v], totals[v] per view)
 int launch_binning_sorted_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
                                 int tbits, int passes, hipStream_t s);
@@ -484,14 +487,18 @@ int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk,
 // interleave: dispatch class-major over the views (k * classes <= 64), else view after view
 // stamps (nullable, profiling): the launch writes, by plain stores, every
 // block's start clock ([blocks]) and then every wave's end clock
-// ([blocks * 4]) of the 100 MHz constant clock (s_memrealtime).
+// ([blocks * composite_views_waves_per_block()]) of the 100 MHz constant
+// clock (s_memrealtime).  debug_handoff: the tail merge's test knob (0).
 int launch_composite_views(FinishView* views, int k, uint32_t max_chunks, uint32_t classes, bool first_major,
                            bool interleave, const FrameUniforms& u, int frag_class, float t_min, const float* bg,
-                           int out_layout, hipStream_t s, uint64_t* stamps = nullptr);
-// Blocks of one launch_composite_views launch (stamps: 5 words per block).
+                           int out_layout, bool tail_merge, uint32_t debug_handoff, hipStream_t s,
+                           uint64_t* stamps = nullptr);
+// Blocks of one launch_composite_views launch, and its waves per block (the
+// build's GSR_COMP_THREADS / 64): a launch's stamps take blocks * (1 + waves) words.
 size_t composite_views_blocks(uint32_t max_chunks, int k);
+int composite_views_waves_per_block();
 int launch_merge_views(FinishView* views, int k, const FrameUniforms& u, float t_min, const float* bg,
-                       int out_layout, hipStream_t s);
+                       int out_layout, bool tail_merge, hipStream_t s);
 
 }  // namespace gsr
 

@@ -137,10 +137,13 @@ def test_binning_mixes_staged_and_direct_blocks(gpu, monkeypatch, limit):
     directly.  The garden stand-in averages ~1.8 instances per splat, so the
     limits 1700 / 1900 split one frame's 1024-splat blocks between the two
     paths (0: every block direct).  Single view (k_bin_write) and a group of
-    views (k_bin_write_views): the tile lists must be the oracle's exactly."""
+    views (k_bin_write_views): the tile lists must be the oracle's exactly.
+    That is the separate binning (GSR_BIN_FUSED=0); both knobs are read at
+    context creation."""
     from gsviewer_amd.rasterizer import HipScene
     from helpers import batched_frames
     monkeypatch.setenv("GSR_BIN_STAGE_LIMIT", limit)
+    monkeypatch.setenv("GSR_BIN_FUSED", "0")
     g = garden_standin(200_000, seed=1, sh_degree=0)
     cam = Camera(540, 960).yaw(45)
     U = uniforms_for(cam)

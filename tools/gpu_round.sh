@@ -10,7 +10,7 @@ MODE=${2:-full}
 O=gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-B="python bench.py --steps 50 --warmup 10 --no-cpu-baseline"
+B="python bench.py --steps 20 --warmup 5 --no-cpu-baseline"  # the driver's region (BENCH_rNN: --steps 20 --warmup 5)
 
 step() {  # step NAME SECONDS CMD...
     local name=$1 secs=$2

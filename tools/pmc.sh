@@ -13,7 +13,7 @@ shift 2
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p $O
-B="python bench.py --steps 50 --warmup 10 --no-cpu-baseline $*"
+B="python bench.py --steps 20 --warmup 5 --no-cpu-baseline $*"  # the driver's region
 case $PRESET in
     traffic) PASSES=("FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_WAVES") ;;
     stalls) PASSES=("SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS"
