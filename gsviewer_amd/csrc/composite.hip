@@ -40,8 +40,6 @@ constexpr int kBinStage = GSR_BIN_STAGE;
 // Blocks of at most stage_limit instances take the staged write (default and
 // upper bound kBinStage; the context's GSR_BIN_STAGE_LIMIT, read at creation,
 // lowers it so a test can make one frame mix staged and direct blocks).
-uint32_t clamp_stage_limit(long v) { return (v >= 0 && v < kBinStage) ? (uint32_t)v : (uint32_t)kBinStage; }
-
 __device__ __forceinline__ uint32_t rect_tiles(uint2 tr) {
     const uint32_t tx0 = tr.x & 0xffffu, tx1 = tr.x >> 16, ty0 = tr.y & 0xffffu, ty1 = tr.y >> 16;
     return (tx0 <= tx1) ? (tx1 - tx0 + 1) * (ty1 - ty0 + 1) : 0u;
@@ -1895,6 +1893,8 @@ extern "C" int64_t gsr_debug_comp_trace(void* host_dst, int64_t max_entries) {
     return n;
 }
 #endif
+
+uint32_t clamp_stage_limit(long v) { return (v >= 0 && v < kBinStage) ? (uint32_t)v : (uint32_t)kBinStage; }
 
 size_t bin_tmp_elems(size_t n_vis) { return (n_vis + kBinBlock - 1) / kBinBlock + 1; }
 
