@@ -405,6 +405,8 @@ def main():
     ap.add_argument("--lookahead", type=int, default=None,
                     help="with --share > 1: at most this many groups begun and not yet finished (default: all "
                          "groups; a group is finished when it is begun again or drained)")
+    ap.add_argument("--host-threads", action="store_true",
+                    help="with --share > 1: one host thread per group drives its stream (parallel enqueue)")
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage HIP events")
     ap.add_argument("--render-mod", type=int, default=6,
                     help="render_mod uniform (experiments; 6 = SH:0~3, the reference default)")
@@ -465,7 +467,8 @@ def main():
             raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
     from gsviewer_amd import _lib
-    from gsviewer_amd.multiview import ViewBatchPipeline, ViewPipeline, broadcast_scene, timed_region, view_of
+    from gsviewer_amd.multiview import (ThreadedViewBatchPipeline, ViewBatchPipeline, ViewPipeline, broadcast_scene,
+                                        timed_region, view_of)
     from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera_from, render_into
 
     _lib.load()
@@ -515,8 +518,12 @@ def main():
         # groups of `share` views (the last one may be smaller), one stream each
         groups = [(ctxs[g:g + share], camcs[g:g + share], outs[g:g + share], streams[g])
                   for g in range(0, K, share)]
-        pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=not args.no_batched_sorts,
-                                 batched_finish=not args.no_batched_finish, lookahead=args.lookahead)
+        if args.host_threads:
+            pipe = ThreadedViewBatchPipeline(groups, scene, st, batched_sorts=not args.no_batched_sorts,
+                                             batched_finish=not args.no_batched_finish)
+        else:
+            pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=not args.no_batched_sorts,
+                                     batched_finish=not args.no_batched_finish, lookahead=args.lookahead)
 
     def serial_frame():
         render_into(ctx, scene, camc, st, outs[0])

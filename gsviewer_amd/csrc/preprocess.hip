@@ -16,6 +16,8 @@
 // the exact reverse of the GL draw order (renderer_ogl.py:24, ascending z,
 // ties by ascending index), i.e. front-to-back.
 #pragma clang fp contract(off)
+#include <cstdlib>
+
 #include "gsr_internal.h"
 
 #include <algorithm>
@@ -947,7 +949,12 @@ static unsigned preprocess_grid(int64_t n) {
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
-        return 4u * (unsigned)cus;  // ~4 resident blocks per CU (92 VGPRs: 5 waves/SIMD fit)
+        unsigned per_cu = 4u;  // ~4 resident blocks per CU (92 VGPRs: 5 waves/SIMD fit)
+        if (const char* e = std::getenv("GSR_PRE_BLOCKS_PER_CU")) {  // experiment knob (read once per process)
+            const long v = std::strtol(e, nullptr, 10);
+            if (v >= 1 && v <= 32) per_cu = (unsigned)v;
+        }
+        return per_cu * (unsigned)cus;
     }();
     return std::max(1u, std::min((unsigned)((n + kThreads - 1) / kThreads), max_grid));
 }

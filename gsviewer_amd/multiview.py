@@ -11,6 +11,8 @@ use these helpers, so the tested code is the benchmarked code.
 """
 from __future__ import annotations
 
+import queue
+import threading
 import time
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -219,3 +221,92 @@ class ViewBatchPipeline:
     def drain(self):
         while self.order:
             self._finish(self.order[0])
+
+
+class _GroupWorker(threading.Thread):
+    """One host thread driving one group's stream (ThreadedViewBatchPipeline)."""
+
+    def __init__(self, device):
+        super().__init__(daemon=True)
+        self.q = queue.Queue()
+        self.error = None
+        self.device = device
+        self.start()
+
+    def run(self):
+        if self.device is not None:  # HIP's current device is per thread: the group stream's own
+            torch.cuda.set_device(self.device)
+        while True:
+            fn = self.q.get()
+            if fn is None:
+                self.q.task_done()
+                return
+            try:
+                if self.error is None:
+                    fn()
+            except BaseException as e:  # re-raised by the pipeline's wait()
+                self.error = e
+            finally:
+                self.q.task_done()
+
+
+class ThreadedViewBatchPipeline(ViewBatchPipeline):
+    """ViewBatchPipeline with one host thread per group: a group's finish
+    (which waits on the host for its frames' counts) and begin calls run on
+    its own thread, so the groups' launch sequences are enqueued in parallel
+    instead of one after the other (ctypes releases the GIL during each call;
+    the library's calls for different contexts and streams are independent).
+    step() hands the group's next step to its thread and returns; drain()
+    finishes every pending frame and waits for all threads.  Images are
+    identical to ViewBatchPipeline's (tests/test_gpu_multiview.py)."""
+
+    def __init__(self, groups, scene, settings, batched_sorts=True, batched_finish=True):
+        super().__init__(groups, scene, settings, batched_sorts, batched_finish)
+        self.workers = [_GroupWorker(getattr(g[3], "device", None)) for g in groups]
+
+    def _group_step(self, gi):
+        from .rasterizer import render_begin_sort, render_begin_sorts, render_begin_views
+        ctxs, cams, outs, stream = self.groups[gi]
+        if self.pending[gi]:
+            self._finish_group(gi)
+        render_begin_views(ctxs, self.scene, cams, self.settings, outs, stream=stream)
+        if self.batched_sorts:
+            render_begin_sorts(ctxs, stream)
+        else:
+            for c in ctxs:
+                render_begin_sort(c, stream)
+        self.pending[gi] = True
+
+    def _finish_group(self, gi):
+        from .rasterizer import render_finish, render_finish_views
+        ctxs, _, _, stream = self.groups[gi]
+        if self.batched_finish:
+            render_finish_views(ctxs, stream)
+        else:
+            for c in ctxs:
+                render_finish(c, stream)
+        self.pending[gi] = False
+
+    def step(self):
+        gi = self.next
+        self.next = (gi + 1) % len(self.groups)
+        self.workers[gi].q.put(lambda gi=gi: self._group_step(gi))
+
+    def wait(self):
+        for w in self.workers:
+            w.q.join()
+        for w in self.workers:
+            if w.error is not None:
+                e, w.error = w.error, None
+                raise e
+
+    def drain(self):
+        for gi, w in enumerate(self.workers):
+            w.q.put(lambda gi=gi: self._finish_group(gi) if self.pending[gi] else None)
+        self.wait()
+
+    def close(self):
+        for w in self.workers:
+            w.q.put(None)
+        for w in self.workers:
+            w.join()

@@ -106,14 +106,18 @@ def test_contexts_share_one_scene_concurrently(gpu):
     scene.close()
 
 
-@pytest.mark.parametrize("batched_sorts,batched_finish", [(True, True), (True, False), (False, False)])
-def test_shared_scene_pass_matches_serial_renders(gpu, batched_sorts, batched_finish):
+@pytest.mark.parametrize("batched_sorts,batched_finish,mode", [(True, True, "serial"), (True, False, "serial"),
+                                                                (False, False, "serial"), (True, True, "lookahead1"),
+                                                                (True, True, "threads")])
+def test_shared_scene_pass_matches_serial_renders(gpu, batched_sorts, batched_finish, mode):
     """gsr_render_begin_views (one cull + preprocess pass over the scene for a
     group of views) through ViewBatchPipeline with two groups: images, radii
-    and counts identical to each view rendered alone."""
+    and counts identical to each view rendered alone; also with one group
+    finished a step after it began (lookahead 1) and with one host thread per
+    group (ThreadedViewBatchPipeline)."""
     import torch
 
-    from gsviewer_amd.multiview import ViewBatchPipeline
+    from gsviewer_amd.multiview import ThreadedViewBatchPipeline, ViewBatchPipeline
     from gsviewer_amd.rasterizer import HipContext, render_into
     K, G = 3, 2
     scene, st, cams, ctxs, streams, outs = _setup(K * G)
@@ -127,11 +131,18 @@ def test_shared_scene_pass_matches_serial_renders(gpu, batched_sorts, batched_fi
         want_stats.append(ref_ctx.stats())
     groups = [(ctxs[g * K:(g + 1) * K], cams[g * K:(g + 1) * K], outs[g * K:(g + 1) * K], streams[g])
               for g in range(G)]
-    pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=batched_sorts, batched_finish=batched_finish)
+    if mode == "threads":
+        pipe = ThreadedViewBatchPipeline(groups, scene, st, batched_sorts=batched_sorts,
+                                         batched_finish=batched_finish)
+    else:
+        pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=batched_sorts, batched_finish=batched_finish,
+                                 lookahead=1 if mode == "lookahead1" else None)
     for _ in range(3 * G + 1):  # every group several times, one group a step ahead
         pipe.step()
     pipe.drain()
     torch.cuda.synchronize()
+    if mode == "threads":
+        pipe.close()
     for k in range(K * G):
         np.testing.assert_array_equal(outs[k].cpu().numpy(), want[k].cpu().numpy(), err_msg=f"view {k}")
         got = ctxs[k].stats()
