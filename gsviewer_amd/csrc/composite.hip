@@ -1002,7 +1002,7 @@ __device__ __forceinline__ void prior_bound(const float4* tmax, uint32_t tile, u
 #ifdef GSR_COMP_STATS
 // Tooling build only (tools/comp_stats.py): {slice evaluations, evaluations
 // of an already saturated slice, records visited, records in the chunks}.
-__device__ unsigned long long g_comp_stats[4];
+__device__ unsigned long long g_comp_stats[5];
 #endif
 
 // One wave per chunk, 4 pixels per lane (four 16x4 slices of the 16x16 tile).
@@ -1134,7 +1134,7 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         asm volatile("" ::"v"(junk));
     }
 #ifdef GSR_COMP_STATS
-    uint32_t st_evals = 0, st_wasted = 0, st_records = 0;
+    uint32_t st_evals = 0, st_wasted = 0, st_records = 0, st_empty = 0;
 #endif
     for (uint32_t b = begin; b < end && live; b += kBatch) {
         __builtin_amdgcn_wave_barrier();
@@ -1304,6 +1304,9 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                 // alpha == 0 leaves (C, T) bit-identical: a discarded fragment.
                 // C += c w, T += kT w with w = alpha T (kFragGauss: alpha =
                 // 0.99 a1, the colour already carries its 0.99)
+#ifdef GSR_COMP_STATS
+                if (!__any(alpha > 0.f)) st_empty += 1;  // no lane keeps a fragment of this slice
+#endif
                 const float w = alpha * bt[k].y;
                 const f32x2 ww = f32x2{w, w};
                 rg[k] = __builtin_elementwise_fma(crg, ww, rg[k]);
@@ -1360,6 +1363,7 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         atomicAdd(&g_comp_stats[1], (unsigned long long)st_wasted);
         atomicAdd(&g_comp_stats[2], (unsigned long long)st_records);
         atomicAdd(&g_comp_stats[3], (unsigned long long)(end - begin));
+        atomicAdd(&g_comp_stats[4], (unsigned long long)st_empty);
     }
 #endif
     if (nchunks > 1) {
@@ -1876,11 +1880,12 @@ __global__ __launch_bounds__(256) void k_composite_unorm8(const uint2* __restric
 }  // namespace
 
 #ifdef GSR_COMP_STATS
-extern "C" int gsr_debug_comp_stats(unsigned long long* host4) {
+// host5: slice evaluations, those on saturated slices, records, instances, slices where no lane keeps a fragment
+extern "C" int gsr_debug_comp_stats(unsigned long long* host5) {
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(host4, HIP_SYMBOL(gsr::g_comp_stats), 32, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    static const unsigned long long zeros[4] = {0, 0, 0, 0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_comp_stats), zeros, 32, 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+    if (hipMemcpyFromSymbol(host5, HIP_SYMBOL(gsr::g_comp_stats), 40, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    static const unsigned long long zeros[5] = {0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_comp_stats), zeros, 40, 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -22,7 +22,7 @@ def main():
     scene = HipScene.from_gaussian_data(g)
     ctx = HipContext()
     out = torch.empty((3, 1080, 1920), dtype=torch.float32, device="cuda")
-    buf = (ctypes.c_ulonglong * 4)()
+    buf = (ctypes.c_ulonglong * 5)()
     # --views: the group path (gsr_render_finish_views: GSR_CHUNK_VIEWS, first-major order), one group of
     # the bench's first 5 views (stats summed over them)
     views = "--views" in sys.argv
@@ -49,9 +49,10 @@ def main():
         frame(st)
         torch.cuda.synchronize()
         lib.gsr_debug_comp_stats(buf)
-        ev, wasted, recs, inst = list(buf)
+        ev, wasted, recs, inst, empty = list(buf)
         print(f"t_min={t_min}: instances {inst} records visited {recs} ({recs / inst:.3f}), slice evals {ev} "
-              f"({ev / max(recs, 1):.2f} per record), on saturated slices {wasted} ({wasted / max(ev, 1):.3f})")
+              f"({ev / max(recs, 1):.2f} per record), on saturated slices {wasted} ({wasted / max(ev, 1):.3f}), "
+              f"with no kept fragment {empty} ({empty / max(ev, 1):.3f})", flush=True)
 
 
 if __name__ == "__main__":
