@@ -282,7 +282,9 @@ def frame_valu_issue(args, share, ms_per_frame):
     valu, trans, disp = {}, {}, {}
     for r in rows:
         k = r[0]
-        if "_views" not in k:
+        # the group kernels only: the fused preprocess of a frame alone is the same template
+        # instantiated <DEG, true> (it runs in the latency regions, not in the frame in flight)
+        if "_views" not in k or k.endswith(", true>"):
             continue
         if r[1] == "SQ_INSTS_VALU":
             valu[k], disp[k] = float(r[4]), int(r[2])
