@@ -1283,9 +1283,10 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                     // pw' = pw - mid; keep <=> |pw'| <= -mid; alpha / 0.99 = clamp(s * 2^pw')
                     const float dy = pyw[k] - q0.y;
                     const float pw = (c2 * dy + p1) * dy + p0;
+                    const float u = fmaf(-kKeepScale, fabsf(pw), km);  // >= 0 exactly where the fragment is kept
                     const float e = __builtin_amdgcn_exp2f(pw);
                     const float a1 = __builtin_amdgcn_fmed3f(__uint_as_float(covk & __float_as_uint(q0.z)) * e, 0.f, 1.f);
-                    alpha = __builtin_amdgcn_fmed3f(fmaf(-kKeepScale, fabsf(pw), km), 0.f, a1);
+                    alpha = __builtin_amdgcn_fmed3f(u, 0.f, a1);
                 } else if (FRAG == kFragBillboard) {
                     alpha = __uint_as_float(covk & 0x3f800000u);  // 1.0 or 0.0
                 } else {
