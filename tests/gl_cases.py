@@ -16,7 +16,7 @@ import hashlib
 import numpy as np
 
 from gsviewer_amd.camera import Camera, euler_to_quaternion, euler_to_rotation_matrix
-from gsviewer_amd.gaussian_data import naive_gaussian, random_scene
+from gsviewer_amd.gaussian_data import garden_standin, naive_gaussian, random_scene
 
 F = np.float32
 
@@ -27,6 +27,7 @@ SCENES = {
     "sh1": ("random", 3000, 1, 12, (0.005, 0.05)),
     "sh3": ("random", 3000, 3, 11, (0.005, 0.05)),
     "sh3_big": ("random", 1500, 3, 14, (0.03, 0.25)),
+    "garden": ("garden", 100_000, 3, 1, None),  # the bench's scene generator (C2's stand-in), 1/10 size
 }
 
 # name: (scene, (h, w), yaw_deg, target_dist, orthographic, uniform overrides)
@@ -57,13 +58,19 @@ CASES = {
     "sh3_ortho_depth": ("sh3", (150, 200), 20.0, 5.0, True, {"render_mod": -3}),
     "sh3_ortho_normal": ("sh3", (150, 200), 20.0, 5.0, True, {"render_mod": -2}),
     "big_close": ("sh3_big", (144, 176), 60.0, 2.5, False, {}),
+    "garden_100k": ("garden", (180, 320), 0.0, 5.0, False, {}),
 }
+
+# cases the CPU test checks with the C oracle (oracle/gl_oracle.c) instead of the NumPy one (too slow there)
+LARGE = {"garden_100k"}
 
 
 def scene(name):
     kind, n, deg, seed, sr = SCENES[name]
     if kind == "naive":
         return naive_gaussian()
+    if kind == "garden":
+        return garden_standin(n, seed=seed, sh_degree=deg)
     return random_scene(n, sh_degree=deg, seed=seed, scale_range=sr)
 
 

@@ -50,16 +50,31 @@ def oracle_frames(golden, name):
     return vs, U, order
 
 
+def _frames(golden, name):
+    """(float image, gl8 image) of the oracle for a case: the NumPy restatement
+    in the reference's own draw order, or for the large cases the C one
+    (oracle/gl_oracle.c, pinned against the NumPy one by tests/test_oracle_c.py)
+    in its own depth order."""
+    if name in GC.LARGE:
+        from oracle import c_oracle as C
+        g = GC.scene(GC.CASES[name][0])
+        assert str(golden[f"{name}/sha"]) == GC.flat_sha(g), "scene generator changed: regenerate the fixture"
+        _, U = GC.uniforms(name, g)
+        return (C.render(g.flat(), g.sh_dim, U, mode="float", threads=8),
+                C.render(g.flat(), g.sh_dim, U, mode="gl8", threads=8))
+    vs, U, order = oracle_frames(golden, name)
+    return O.composite(vs, U, "float", order=order), O.composite(vs, U, "gl8", order=order)
+
+
 @pytest.mark.parametrize("name", list(GC.CASES))
 def test_oracle_matches_llvmpipe(golden, name):
-    vs, U, order = oracle_frames(golden, name)
-    f = O.composite(vs, U, "float", order=order)
+    f, q8 = _frames(golden, name)
     ref = golden[f"{name}/float"]
     d = np.abs(f - ref).max(-1)
     assert (d <= TOL_FLOAT).mean() >= FRAC_FLOAT, (name, int((d > TOL_FLOAT).sum()))
     assert d.max() <= TOL_MAX, (name, float(d.max()))
 
-    q = np.rint(O.composite(vs, U, "gl8", order=order) * 255).astype(np.int32)
+    q = np.rint(q8 * 255).astype(np.int32)
     d8 = np.abs(q - golden[f"{name}/rgba8"].astype(np.int32)).max(-1)
     assert (d8 == 0).mean() >= FRAC_GL8, (name, int((d8 > 0).sum()))
     assert d8.max() <= 1, (name, int(d8.max()))
