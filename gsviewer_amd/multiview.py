@@ -179,8 +179,9 @@ class ViewBatchPipeline:
         self.batched_finish = batched_finish  # the group's second halves in one launch per stage
         # at most `lookahead` groups begun and not finished: a step that begins a
         # group finishes the oldest pending ones beyond that (None: all groups,
-        # i.e. a group is finished only when it is begun again or drained)
-        self.lookahead = len(groups) if lookahead is None else max(1, min(int(lookahead), len(groups)))
+        # i.e. a group is finished only when it is begun again or drained; 0: every
+        # group is finished in the step that begins it, the host waiting for its counts)
+        self.lookahead = len(groups) if lookahead is None else max(0, min(int(lookahead), len(groups)))
         self.pending = [False] * len(groups)
         self.order = []  # pending groups, oldest first
         self.next = 0

@@ -108,7 +108,7 @@ def test_contexts_share_one_scene_concurrently(gpu):
 
 @pytest.mark.parametrize("batched_sorts,batched_finish,mode", [(True, True, "serial"), (True, False, "serial"),
                                                                 (False, False, "serial"), (True, True, "lookahead1"),
-                                                                (True, True, "threads")])
+                                                                (True, True, "lookahead0"), (True, True, "threads")])
 def test_shared_scene_pass_matches_serial_renders(gpu, batched_sorts, batched_finish, mode):
     """gsr_render_begin_views (one cull + preprocess pass over the scene for a
     group of views) through ViewBatchPipeline with two groups: images, radii
@@ -136,7 +136,7 @@ def test_shared_scene_pass_matches_serial_renders(gpu, batched_sorts, batched_fi
                                          batched_finish=batched_finish)
     else:
         pipe = ViewBatchPipeline(groups, scene, st, batched_sorts=batched_sorts, batched_finish=batched_finish,
-                                 lookahead=1 if mode == "lookahead1" else None)
+                                 lookahead={"lookahead1": 1, "lookahead0": 0}.get(mode))
     for _ in range(3 * G + 1):  # every group several times, one group a step ahead
         pipe.step()
     pipe.drain()
