@@ -49,6 +49,10 @@ def _compile(src, debug, bdir=BUILD, defines=()):
     cmd += ["-O0", "-g"] if debug else ["-O3"]
     cmd += EXTRA_FLAGS.get(src, [])
     cmd += ["-D" + d for d in defines]
+    # experiment builds only (never the product): extra flags for one source, "file.hip:-flag,-flag"
+    extra = os.environ.get("GSR_BUILD_EXTRA", "")
+    if extra and defines and extra.split(":", 1)[0] == src:
+        cmd += extra.split(":", 1)[1].split(",")
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
