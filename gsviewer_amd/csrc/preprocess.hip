@@ -15,9 +15,7 @@
 // ascending depth sort resolves exact depth ties in DESCENDING index order:
 // the exact reverse of the GL draw order (renderer_ogl.py:24, ascending z,
 // ties by ascending index), i.e. front-to-back.
-#ifndef GSR_EXP_CONTRACT  // (experiment builds only: measure what contraction would buy)
 #pragma clang fp contract(off)
-#endif
 #include <cstdlib>
 
 #include "gsr_internal.h"
