@@ -400,6 +400,9 @@ def main():
                          "(tools/short_region_sweep2.sh: 0.204 ms/frame over 100 frames and 0.215 over the "
                          "driver's 20, against 0.209 / 0.230 for 16 as 4 x 4), and 20 frames are then exactly "
                          "one begin + finish of every group")
+    ap.add_argument("--group-sizes", default=None,
+                    help="with --share > 1: explicit group sizes in step order, e.g. 2,6,6,6 (each <= 8, summing "
+                         "to --inflight); default: groups of --share")
     ap.add_argument("--share", type=int, default=None,
                     help="views per shared scene pass (gsr_render_begin_views): the views in flight form "
                          "inflight/share groups, one stream each, whose cull + preprocess read the scene once "
@@ -524,8 +527,15 @@ def main():
         pipe = ViewPipeline(ctxs, streams, scene, camcs, st, outs)
     else:
         # groups of `share` views (the last one may be smaller), one stream each
-        groups = [(ctxs[g:g + share], camcs[g:g + share], outs[g:g + share], streams[g])
-                  for g in range(0, K, share)]
+        starts = list(range(0, K, share))
+        if args.group_sizes:
+            sizes_req = [int(x) for x in args.group_sizes.split(",")]
+            if sum(sizes_req) != K or not all(1 <= x <= 8 for x in sizes_req):
+                raise SystemExit(f"--group-sizes {args.group_sizes}: sizes in 1..8 summing to --inflight {K}")
+            starts = [sum(sizes_req[:i]) for i in range(len(sizes_req))]
+        bounds = starts + [K]
+        groups = [(ctxs[a:b], camcs[a:b], outs[a:b], streams[gi])
+                  for gi, (a, b) in enumerate(zip(bounds[:-1], bounds[1:]))]
         if args.host_threads:
             pipe = ThreadedViewBatchPipeline(groups, scene, st, batched_sorts=not args.no_batched_sorts,
                                              batched_finish=not args.no_batched_finish)
