@@ -1514,6 +1514,27 @@ __device__ uint4 g_comp_trace[2 * kTraceMax];
 #endif
 constexpr int kCompThreads = GSR_COMP_THREADS;
 constexpr int kCompWaves = kCompThreads / 64;
+
+// A frame alone's compositing (k_composite): blocks are dealt round-robin to
+// the 8 XCDs; each XCD gets R = 8 consecutive logical blocks (32 consecutive
+// chunks, mostly neighbouring tiles) per window of 64, and the dispatch order
+// changes only within a window.  Measured (profiles/r4_s23, r4_s24): 120.2 ->
+// 117.0 us per launch, HBM fetch -1 %; R = 16 or 32 the same.  A group's
+// launch (k_composite_views) keeps the plain order: remapped it ran no faster
+// in flight (its class-major, first-major order matters more there).
+#ifndef GSR_COMP_XCD_RUN
+#define GSR_COMP_XCD_RUN 8
+#endif
+__device__ __forceinline__ uint32_t comp_block() {
+    const uint32_t b = blockIdx.x;
+    if (GSR_COMP_XCD_RUN <= 1) return b;
+    constexpr uint32_t R = GSR_COMP_XCD_RUN, W = 8u * R;
+    const uint32_t w = b / W;
+    if ((w + 1) * W > gridDim.x) return b;  // the last partial window keeps the plain order
+    const uint32_t r = b - w * W;
+    return w * W + (r & 7u) * R + (r >> 3);
+}
+
 template <int FRAG>
 __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const uint4* __restrict__ desc,
                                                         const uint32_t* __restrict__ order,
@@ -1525,7 +1546,7 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
                                                         const uint32_t* __restrict__ chunk_base) {
     __shared__ float4 lds[kCompWaves][kBatch * 3];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t pos = blockIdx.x * kCompWaves + wave;
+    const uint32_t pos = comp_block() * kCompWaves + wave;
     if (pos >= (uint32_t)a.num_tiles + n_chunks_dev[0]) return;  // device count of extra chunks
     const uint32_t slot = order[pos];
 #ifdef GSR_COMP_TRACE
