@@ -943,20 +943,25 @@ __global__ __launch_bounds__(kThreads) void k_depth_keys_all(const float4* __res
 
 }  // namespace
 
-static unsigned preprocess_grid(int64_t n) {
-    static const unsigned max_grid = [] {
-        int dev = 0, cus = 256;
+// Grid-stride blocks: ~4 resident blocks per CU (92 VGPRs: 5 waves/SIMD fit)
+// for a group's views; 3 for a frame alone (fused kernel with k = 1), whose
+// preprocess measured 68.3 -> 66.1 us with 3 (2: 66.7, 16 = one thread per
+// Gaussian: 82.4; a group's kernel was no faster with 3 or 2, profiles/r4_s27).
+static unsigned preprocess_grid(int64_t n, bool alone = false) {
+    static const int cus = [] {
+        int dev = 0, c = 256;
         if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        unsigned per_cu = 4u;  // ~4 resident blocks per CU (92 VGPRs: 5 waves/SIMD fit)
-        if (const char* e = std::getenv("GSR_PRE_BLOCKS_PER_CU")) {  // experiment knob (read once per process)
-            const long v = std::strtol(e, nullptr, 10);
-            if (v >= 1 && v <= 32) per_cu = (unsigned)v;
-        }
-        return per_cu * (unsigned)cus;
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 256;
+        return c;
     }();
-    return std::max(1u, std::min((unsigned)((n + kThreads - 1) / kThreads), max_grid));
+    static const long knob = [] {  // experiment knob (read once per process): blocks per CU for both
+        const char* e = std::getenv("GSR_PRE_BLOCKS_PER_CU");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (v >= 1 && v <= 32) ? v : 0L;
+    }();
+    const unsigned per_cu = knob ? (unsigned)knob : (alone ? 3u : 4u);
+    return std::max(1u, std::min((unsigned)((n + kThreads - 1) / kThreads), per_cu * (unsigned)cus));
 }
 
 static int effective_deg(const FrameUniforms& u) {
@@ -1059,7 +1064,7 @@ int launch_preprocess_fc_views(const SceneData& sd, const ViewPreFcArgs* views, 
         vp.v[v] = ViewPreFc{*a.u,         a.recs,      a.depth_keys, a.trect,         a.counters, a.key_range,
                             a.zero_words, a.done_ctr,  a.host_counters, a.radii,      a.n_zero,   a.seq};
     }
-    const unsigned grid = preprocess_grid(sd.n);
+    const unsigned grid = preprocess_grid(sd.n, k == 1);
 #define GSR_PREV(D)                                                                                             \
     (k == 1 ? k_preprocess_fc_views<D, true> : k_preprocess_fc_views<D, false>)<<<grid, kThreads, 0, s>>>(        \
         sd.pos_op, sd.rot, sd.scale, sd.sh, sd.n, vp)
