@@ -123,6 +123,7 @@ SIGNATURES = {
     "gsr_render_begin_sort": (ctypes.c_int, [_P, _P]),
     "gsr_render_begin_sorts": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int32, _P]),
     "gsr_render_finish_views": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int32, _P]),
+    "gsr_render_wait_counts": (ctypes.c_int, [_P]),
     "gsr_context_stats": (ctypes.c_int, [_P, ctypes.POINTER(GsrFrameStats)]),
     "gsr_sort_depth": (ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_float * 16), _P, _P]),
     "gsr_debug_host_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),

@@ -1150,6 +1150,13 @@ int gsr_render_finish(gsr_context* c, void* stream) {
 // The second halves of a group of frames in one set of launches (view =
 // blockIdx.y in every kernel): binning, tile sort, ranges, chunks, composite
 // and merge are each one launch for the group instead of one per view.
+int gsr_render_wait_counts(gsr_context* ctx) {
+    if (!ctx) return set_error(GSR_ERR_INVALID, "null argument");
+    if (!ctx->pend.active) return set_error(GSR_ERR_INVALID, "render_wait_counts: no frame was begun");
+    if (ctx->failed) return set_error(GSR_ERR_HIP, "render: the context failed earlier (destroy it)");
+    return ctx->pend.n > 0 ? wait_counts(ctx, ctx->pend.stream) : GSR_OK;
+}
+
 int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
     if (!ctxs) return set_error(GSR_ERR_INVALID, "null argument");
     if (k < 1 || k > GSR_MAX_VIEWS) return set_error(GSR_ERR_INVALID, "render_finish_views: k out of range");

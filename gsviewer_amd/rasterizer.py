@@ -357,6 +357,13 @@ def render_begin_sorts(ctxs, stream=None):
     _lib.check(_lib.load().gsr_render_begin_sorts(arr, k, _stream_handle(stream)), "gsr_render_begin_sorts")
 
 
+def render_wait_counts(ctx: HipContext):
+    """gsr_render_wait_counts: host wait until the begun frame of `ctx` has
+    published its counts (its cull + preprocess completed); the frame stays
+    pending."""
+    _lib.check(_lib.load().gsr_render_wait_counts(ctx.handle), "gsr_render_wait_counts")
+
+
 def render_finish_views(ctxs, stream=None):
     """gsr_render_finish_views: completes the pending frames of `ctxs` (all
     begun on `stream`) with one launch per stage for the group; identical

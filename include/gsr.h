@@ -234,6 +234,14 @@ int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream);
  * bounds) ends all k frames, and each context can begin its next one. */
 int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream);
 
+/* Host wait, without finishing, until the begun frame of `ctx` has published its
+ * counts (its cull + preprocess has completed on the GPU).  The frame stays
+ * pending; finish it as usual.  (Staggering a pipeline's groups with it --
+ * each group's preprocess waited for before the next group begins -- measured
+ * slower: profiles/r4_s30.)  Same deadline and failure rules as the finish's
+ * own wait; GSR_ERR_INVALID when no frame is pending. */
+int gsr_render_wait_counts(gsr_context* ctx);
+
 int gsr_context_stats(const gsr_context* ctx, gsr_frame_stats* out);
 
 /* Back-to-front Gaussian order for a view matrix: the renderer_ogl

@@ -68,9 +68,14 @@ def test_begin_finish_protocol_errors(gpu):
 
     from gsviewer_amd.rasterizer import camera_from, render_begin, render_finish
     scene, st, cams, ctxs, streams, outs = _setup(2, n=2000)
+    from gsviewer_amd.rasterizer import render_wait_counts
     with pytest.raises(RuntimeError, match="no frame was begun"):
         render_finish(ctxs[0], streams[0])
+    with pytest.raises(RuntimeError, match="no frame was begun"):
+        render_wait_counts(ctxs[0])
     render_begin(ctxs[0], scene, cams[0], st, outs[0], stream=streams[0])
+    render_wait_counts(ctxs[0])  # the frame stays pending: waiting twice, then finishing, is fine
+    render_wait_counts(ctxs[0])
     with pytest.raises(RuntimeError, match="not finished"):
         render_begin(ctxs[0], scene, cams[0], st, outs[0], stream=streams[0])
     with pytest.raises(RuntimeError, match="stream"):
