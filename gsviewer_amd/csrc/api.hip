@@ -112,6 +112,7 @@ namespace gsr {
 // A frame between gsr_render_begin and gsr_render_finish.
 struct PendingFrame {
     bool active = false;
+    uint32_t coarse = 0;  // its depth sort's coarse bits (0: exact), for the run repair
     FrameUniforms u{};
     float t_min = 0.f;
     float bg[3] = {0.f, 0.f, 0.f};
@@ -133,6 +134,21 @@ constexpr size_t kSpanLaunches = 64;
 
 // depth sort passes of a frame rendered alone (gsr_render; see kDepthPasses)
 constexpr int kDepthPassesAlone = 3;
+// Coarse depth order (round 4): a frame's depth sort may order only the top
+// bits of its key range and keep equal coarse keys in slot order.  Only each
+// tile's list needs the exact (key, slot) order; k_tile_ranges restores it run
+// by run (RunFix).  A frame alone sorts 16 bits in 2 passes of 8 (against 3
+// exact passes of <= 9): depth sort 76 -> 51 us, but the repair's gathers of
+// the slots' keys add ~20 us to k_tile_ranges, so the frame gains ~4 us
+// (profiles/r4_s32).  A group's frames keep the exact sort (4 passes of <= 8
+// bits): in flight the sort's VALU work is the same in 3 or 4 passes (24 digit
+// bits of ballot ranking either way) and the repair only costs
+// (0.1356-0.1365 vs 0.1332-0.1353 ms per frame with 3 passes of 8).  With a
+// coarse sort the frame's global depth order (GSR_DEBUG_DEPTH_ORDER) is the
+// coarse one; gsr_sort_depth stays exact.
+constexpr uint32_t kDepthCoarseAlone = 16;
+constexpr uint32_t kDepthCoarseViews = 0;
+inline int coarse_passes(uint32_t coarse) { return coarse <= 22 ? 2 : 3; }
 
 struct gsr_context {
     gsr::DevBuf<uint64_t> vis_mask;
@@ -172,6 +188,10 @@ struct gsr_context {
     bool fused_cull = true;                       // culling inside the preprocess (launch_preprocess_fc)
     int depth_passes_alone = kDepthPassesAlone;   // depth sort passes of gsr_render's frames
     int depth_passes_now = 0;                     // this frame's (0: kDepthPasses)
+    // depth sort of a frame: the top bits of its key range, the exact order restored per tile list by
+    // k_tile_ranges (GSR_DEPTH_COARSE[_ALONE|_VIEWS]=0: every bit, depth_passes_*)
+    uint32_t depth_coarse_alone = kDepthCoarseAlone;
+    uint32_t depth_coarse_views = kDepthCoarseViews;
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
     uint32_t seq = 0;                       // frame sequence number the host waits for
     uint32_t* host_counters_dev = nullptr;  // its device address
@@ -447,7 +467,13 @@ int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const 
     f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
     f.pa = c->rect4_a.p, f.pb = c->rect4_b.p;
     f.packed = rects_packable(f.u);
+    f.coarse = 0;
     if (f.n == 0) return GSR_OK;
+    f.coarse = c->depth_passes_now ? c->depth_coarse_alone : c->depth_coarse_views;
+    if (f.coarse)  // the last pass writes no keys: keys_a keeps every slot's key for the repair
+        return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, (int)f.coarse,
+                                coarse_passes(f.coarse), key_range, c->radix_tmp.p, totals, s,
+                                f.packed ? c->trect.p : nullptr, &f.pa, &f.pb, 0, c->fused_cull, f.coarse, false);
     return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32,
                             c->depth_passes_now ? c->depth_passes_now : kDepthPasses, key_range,
                             c->radix_tmp.p, totals, s, f.packed ? c->trect.p : nullptr, &f.pa, &f.pb, 0,
@@ -695,6 +721,18 @@ int gsr_context_create(gsr_context** out) {
     }
     if (const char* e = std::getenv("GSR_FIRST_MAJOR")) (*out)->first_major = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_BIN_FUSED")) (*out)->bin_fused = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("GSR_DEPTH_COARSE")) {
+        const long v = std::strtol(e, nullptr, 10);  // 0: exact depth sort; 8..16: coarse bits (2 passes of <= 8)
+        if (v == 0 || (v >= 8 && v <= 24)) (*out)->depth_coarse_alone = (*out)->depth_coarse_views = (uint32_t)v;
+    }
+    if (const char* e = std::getenv("GSR_DEPTH_COARSE_ALONE")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v == 0 || (v >= 8 && v <= 24)) (*out)->depth_coarse_alone = (uint32_t)v;
+    }
+    if (const char* e = std::getenv("GSR_DEPTH_COARSE_VIEWS")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v == 0 || (v >= 8 && v <= 24)) (*out)->depth_coarse_views = (uint32_t)v;
+    }
     if (const char* e = std::getenv("GSR_FUSED_CULL")) (*out)->fused_cull = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_FIRST_MAJOR_ALONE"))
         (*out)->first_major_alone = std::strtol(e, nullptr, 10) != 0;
@@ -1028,10 +1066,16 @@ int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream) {
             return set_error(GSR_ERR_INVALID, "render_begin_sorts: views differ in frame size");
         views[v] = RadixViewArgs{&f.ka, &f.va, &f.kb, &f.vb, c->zero.p + zl.counters, c->zero.p + zl.key_range,
                                  c->radix_tmp.p, c->zero.p + zl.totals_depth, f.packed ? c->trect.p : nullptr,
-                                 &f.pa, &f.pb, c->fused_cull};
+                                 &f.pa, &f.pb, c->fused_cull, c->depth_coarse_views, c->depth_coarse_views == 0};
+        f.coarse = c->depth_coarse_views;
+        if (c->depth_coarse_views != ctxs[0]->depth_coarse_views)
+            return set_error(GSR_ERR_INVALID, "render_begin_sorts: contexts differ in the depth order (GSR_DEPTH_COARSE)");
     }
     int rc;
-    if (n > 0 && (rc = radix_sort_pairs_views(views, k, true, n, 32, kDepthPasses, s))) return rc;
+    const uint32_t coarse = ctxs[0]->depth_coarse_views;
+    if (n > 0 && (rc = radix_sort_pairs_views(views, k, true, n, coarse ? (int)coarse : 32,
+                                              coarse ? coarse_passes(coarse) : kDepthPasses, s)))
+        return rc;
     for (int v = 0; v < k; ++v) {
         PendingFrame& f = ctxs[v]->pend;
         f.sort_ready = false;
@@ -1102,7 +1146,11 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         c->last_tile_list = tva;
     }
     if ((rc = prof_record(c, slot, EV_TSORT, s))) return rc;
-    if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, ranges, s))) return rc;
+    if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, ranges,
+                                              RunFix{tva, c->keys_a.p, c->zero.p + zl.key_range, f.coarse,
+                                                     tkb, tvb},
+                                              s)))
+        return rc;
 
     if (f.blend == GSR_BLEND_UNORM8) {  // the RGBA8 framebuffer: whole lists, back to front, no chunks
         if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
@@ -1224,7 +1272,7 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         tka[v] = c->tkeys_a.p, tkb[v] = c->tkeys_b.p, tva[v] = c->tvals_a.p, tvb[v] = c->tvals_b.p;
         if (f.packed != c0->pend.packed)
             return set_error(GSR_ERR_INVALID, "render_finish_views: views differ in frame size or settings");
-        fv[v] = FinishView{f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, n_dup, c->bin_tmp.p, c->trect_sorted.p, tka[v], tva[v],
+        fv[v] = FinishView{f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, n_dup, c->bin_tmp.p, c->trect_sorted.p, tka[v], tva[v], RunFix{},
                            reinterpret_cast<uint2*>(c->zero.p + zl.ranges), c->chunk_cnt.p, c->chunk_base.p,
                            counters + 2, c->chunk_desc.p, c->chunk_order.p, c->tmax.p, c->zero.p + zl.sat,
                            c->recs.p, f.out, c->partial.p};
@@ -1259,6 +1307,8 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
     for (int v = 0; v < k; ++v) {
         fv[v].tile_keys = tka[v];
         fv[v].tile_vals = tva[v];
+        fv[v].fix = RunFix{tva[v], ctxs[v]->keys_a.p, ctxs[v]->zero.p + zl.key_range, ctxs[v]->pend.coarse, tkb[v],
+                           tvb[v]};
         if (fv[v].n_dup > 0) ctxs[v]->last_tile_list = tva[v];
     }
     if ((rc = launch_tile_ranges_views(fv, k, s))) return rc;

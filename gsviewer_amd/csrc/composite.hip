@@ -609,8 +609,168 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter_views(BinSortViews vs,
 // compositors for CU slots.)
 constexpr int kRangeItems = 16;
 
+// The repair of one run of a coarse depth order, [i, i + L): instances of one
+// tile with equal coarse keys, in slot order (the stable coarse sort's).  The
+// exact order is (full key, slot); a run without a descent of the full key is
+// already in it.  Otherwise its (key, slot) pairs are copied to scratch and
+// each one is written at its rank.  One thread owns the run (the thread
+// holding its first instance), so its reads all precede its writes; other
+// threads read the run's slots only for their (tile, coarse key), which the
+// permutation leaves unchanged.  O(L^2), but L is a handful at C2.
+__device__ __noinline__ void fix_run(const uint32_t* __restrict__ keys, uint32_t n, uint32_t* vals,
+                                     const uint32_t* __restrict__ slot_keys, uint32_t* __restrict__ scratch_keys,
+                                     uint32_t* __restrict__ scratch_vals, uint32_t i, uint32_t tile, uint32_t cv,
+                                     uint32_t kmin, uint32_t s0) {
+    uint32_t fprev = slot_keys[vals[i]];
+    uint32_t L = 1;
+    bool descent = false;
+    for (uint32_t q = i + 1; q < n; ++q) {
+        if (keys[q] != tile) break;
+        const uint32_t f = slot_keys[vals[q]];
+        if (((f - kmin) >> s0) != cv) break;
+        descent |= f < fprev;
+        fprev = f;
+        ++L;
+    }
+    if (!descent) return;
+    for (uint32_t r = 0; r < L; ++r) {
+        const uint32_t sl = vals[i + r];
+        scratch_vals[i + r] = sl;
+        scratch_keys[i + r] = slot_keys[sl];
+    }
+    for (uint32_t r = 0; r < L; ++r) {
+        const uint32_t kr = scratch_keys[i + r], vr = scratch_vals[i + r];
+        uint32_t rank = 0;
+        for (uint32_t q = 0; q < L; ++q) {
+            const uint32_t kq = scratch_keys[i + q], vq = scratch_vals[i + q];
+            rank += (kq < kr || (kq == kr && vq < vr)) ? 1u : 0u;
+        }
+        vals[i + rank] = vr;
+    }
+}
+
+// kmin and the coarse shift of the frame's depth sort (digit_params, PassArgs::coarse)
+__device__ __forceinline__ uint32_t coarse_shift(const uint32_t* key_range, uint32_t coarse, uint32_t& kmin) {
+    kmin = ~key_range[0];
+    const uint32_t kmax = key_range[1];
+    const uint32_t B = kmax > kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
+    if (kmax < kmin) kmin = 0u;
+    return B > coarse ? B - coarse : 0u;
+}
+
+// The thread's kRangeItems instances: every run of equal (tile, coarse key)
+// that starts among them is repaired, in registers over a window of the
+// thread's items and the kFixExtra after them (all loads issued at once: a
+// chain of dependent loads per run cost ~200 us at C2).  Runs are short (C2,
+// 16 coarse bits: 41 % of the instances in runs, the longest 8; 22 bits: 1 %,
+// 4), so an odd-even transposition sort restricted to pairs inside one run,
+// as many rounds as the longest run, puts each in (full key, slot) order.  A
+// run that reaches the window's end is left to fix_run (global memory).
+constexpr int kFixExtra = 8;
+constexpr int kFixWin = kRangeItems + kFixExtra;
+static_assert(kFixWin <= 32, "run masks are 32-bit");
+
+__device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ keys, uint32_t n, const RunFix& fx,
+                                                uint32_t base, const uint32_t (&k)[kRangeItems], uint32_t prev) {
+    uint32_t kw[kFixWin], vw[kFixWin], fw[kFixWin];
+#pragma unroll
+    for (int j = 0; j < kRangeItems; ++j) kw[j] = k[j];
+    if (base + kFixWin <= n) {
+        const uint4* pv = reinterpret_cast<const uint4*>(fx.vals + base);  // (base: a multiple of 16)
+        const uint4* pk = reinterpret_cast<const uint4*>(keys + base + kRangeItems);
+#pragma unroll
+        for (int q = 0; q < kFixWin / 4; ++q) {
+            const uint4 v = pv[q];
+            vw[4 * q] = v.x; vw[4 * q + 1] = v.y; vw[4 * q + 2] = v.z; vw[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int q = 0; q < kFixExtra / 4; ++q) {
+            const uint4 v = pk[q];
+            kw[kRangeItems + 4 * q] = v.x; kw[kRangeItems + 4 * q + 1] = v.y;
+            kw[kRangeItems + 4 * q + 2] = v.z; kw[kRangeItems + 4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kFixWin; ++j) {
+            const bool ok = base + j < n;
+            vw[j] = ok ? fx.vals[base + j] : 0u;
+            if (j >= kRangeItems) kw[j] = ok ? keys[base + j] : 0xffffffffu;
+        }
+    }
+    const uint32_t vprev = base > 0 ? fx.vals[base - 1] : 0u;
+    uint32_t kmin;  // (the window's loads are in flight meanwhile)
+    const uint32_t s0 = coarse_shift(fx.key_range, fx.coarse, kmin);
+    if (s0 == 0u) return;  // the coarse sort was exact
+#pragma unroll
+    for (int j = 0; j < kFixWin; ++j) fw[j] = base + j < n ? fx.slot_keys[vw[j]] : 0u;
+    const uint32_t fprev = base > 0 ? fx.slot_keys[vprev] : 0u;
+    // same bit j: items j and j + 1 are one run (both valid, same tile and coarse key)
+    uint32_t same = 0;
+#pragma unroll
+    for (int j = 0; j + 1 < kFixWin; ++j)
+        if (base + j + 1 < n && kw[j] == kw[j + 1] && ((fw[j] - kmin) >> s0) == ((fw[j + 1] - kmin) >> s0))
+            same |= 1u << j;
+    // own bit j: item j is in a run that starts among the thread's items
+    const bool cont0 = base > 0 && prev == kw[0] && ((fprev - kmin) >> s0) == ((fw[0] - kmin) >> s0);
+    uint32_t own = cont0 ? 0u : 1u;
+#pragma unroll
+    for (int j = 1; j < kFixWin; ++j) {
+        const bool in = ((same >> (j - 1)) & 1u) ? ((own >> (j - 1)) & 1u) != 0u : j < kRangeItems;
+        if (in) own |= 1u << j;
+    }
+    // a run that may go on past the window: fix_run from its start, out of the register sort
+    if ((own >> (kFixWin - 1)) & 1u) {
+        int st = kFixWin - 1;
+#pragma unroll
+        for (int j = kFixWin - 2; j >= 0; --j)
+            if (st == j + 1 && ((same >> j) & 1u)) st = j;
+        own &= (1u << st) - 1u;
+        uint32_t kst = 0, fst = 0;  // items st (selected: a dynamic index would put the arrays in scratch)
+#pragma unroll
+        for (int j = 0; j < kFixWin; ++j)
+            if (j == st) kst = kw[j], fst = fw[j];
+        fix_run(keys, n, fx.vals, fx.slot_keys, fx.scratch_keys, fx.scratch_vals, base + (uint32_t)st, kst,
+                (fst - kmin) >> s0, kmin, s0);
+    }
+    const uint32_t pairs = same & own;  // adjacent pairs inside one owned run
+    uint32_t descent = 0;
+#pragma unroll
+    for (int j = 0; j + 1 < kFixWin; ++j)
+        if (((pairs >> j) & 1u) && fw[j] > fw[j + 1]) descent = 1u;  // slots ascend in a run: only keys descend
+#ifdef GSR_EXP_FIX_NOSORT  // experiment build: the window's loads and tests only (timing; lists unrepaired)
+    asm volatile("" ::"v"(descent));
+    return;
+#endif
+    if (!descent) return;
+    // the longest owned run: rounds of the transposition sort
+    uint32_t len = 1, rounds = 1;
+#pragma unroll
+    for (int j = 0; j + 1 < kFixWin; ++j) {
+        len = ((pairs >> j) & 1u) ? len + 1u : 1u;
+        rounds = max(rounds, len);
+    }
+    uint32_t v0[kFixWin];
+#pragma unroll
+    for (int j = 0; j < kFixWin; ++j) v0[j] = vw[j];
+    for (uint32_t r = 0; r < rounds; ++r) {
+#pragma unroll
+        for (int j = 0; j + 1 < kFixWin; ++j) {
+            if ((j & 1) != (int)(r & 1u) || !((pairs >> j) & 1u)) continue;
+            const bool gt = fw[j] > fw[j + 1] || (fw[j] == fw[j + 1] && vw[j] > vw[j + 1]);
+            const uint32_t fa = fw[j], va = vw[j];
+            fw[j] = gt ? fw[j + 1] : fa;
+            vw[j] = gt ? vw[j + 1] : va;
+            fw[j + 1] = gt ? fa : fw[j + 1];
+            vw[j + 1] = gt ? va : vw[j + 1];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kFixWin; ++j)
+        if (((own >> j) & 1u) && vw[j] != v0[j]) fx.vals[base + j] = vw[j];
+}
+
 __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, uint32_t n, uint2* __restrict__ ranges,
-                                            uint32_t t) {
+                                            uint32_t t, const RunFix& fx) {
     const uint32_t base = t * kRangeItems;
     if (base >= n) return;
     uint32_t k[kRangeItems];
@@ -627,6 +787,8 @@ __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, u
     }
     const uint32_t prev = base > 0 ? keys[base - 1] : 0xffffffffu;
     const uint32_t next = base + kRangeItems < n ? keys[base + kRangeItems] : 0xffffffffu;
+    // the run repair first: its window loads are issued before the range stores
+    if (fx.coarse) fix_coarse_runs(keys, n, fx, base, k, prev);
 #pragma unroll
     for (int j = 0; j < kRangeItems; ++j) {
         const uint32_t i = base + j;
@@ -639,19 +801,20 @@ __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, u
 }
 
 __global__ __launch_bounds__(kThreads) void k_tile_ranges(const uint32_t* __restrict__ keys, uint32_t n,
-                                                          uint2* __restrict__ ranges) {
-    tile_ranges(keys, n, ranges, blockIdx.x * kThreads + threadIdx.x);
+                                                          uint2* __restrict__ ranges, RunFix fx) {
+    tile_ranges(keys, n, ranges, blockIdx.x * kThreads + threadIdx.x, fx);
 }
 
 struct RangeViews {
     const uint32_t* keys[kMaxViews];
     uint2* ranges[kMaxViews];
     uint32_t n[kMaxViews];
+    RunFix fix[kMaxViews];
 };
 
 __global__ __launch_bounds__(kThreads) void k_tile_ranges_views(RangeViews vs) {
     const int v = blockIdx.y;
-    tile_ranges(vs.keys[v], vs.n[v], vs.ranges[v], blockIdx.x * kThreads + threadIdx.x);
+    tile_ranges(vs.keys[v], vs.n[v], vs.ranges[v], blockIdx.x * kThreads + threadIdx.x, vs.fix[v]);
 }
 
 struct CompositeArgs {
@@ -1994,10 +2157,10 @@ int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const 
     return GSR_OK;
 }
 
-int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, hipStream_t s) {
+int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, const RunFix& fix, hipStream_t s) {
     if (n_dup == 0) return GSR_OK;
     const uint32_t per_block = kThreads * kRangeItems;
-    k_tile_ranges<<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges);
+    k_tile_ranges<<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, fix);
     GSR_LAUNCH_CHECK("tile_ranges");
     return GSR_OK;
 }
@@ -2194,6 +2357,7 @@ int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s) {
         rv.keys[i] = views[i].tile_keys;
         rv.ranges[i] = views[i].ranges;
         rv.n[i] = views[i].n_dup;
+        rv.fix[i] = views[i].fix;
         n_max = std::max(n_max, views[i].n_dup);
     }
     if (n_max == 0) return GSR_OK;

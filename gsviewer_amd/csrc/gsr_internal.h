@@ -197,6 +197,11 @@ struct PassArgs {
     // keys are read (not the device count) and keys outside {kmin, kmax}
     // (culled slots, key 0xffffffff) are dropped; later passes see only V
     uint32_t drop = 0;
+    // Coarse depth order (the frame's depth sort): only the top `coarse` bits
+    // of the B-bit key range are sorted (0: all B).  Equal coarse keys keep
+    // their input (slot) order; tile_ranges restores the exact order inside
+    // each tile's list (RunFix).
+    uint32_t coarse = 0;
 };
 
 struct Digit {
@@ -208,7 +213,7 @@ struct Digit {
 
 __device__ __forceinline__ Digit digit_params(const PassArgs& p) {
     Digit d;
-    uint32_t B;
+    uint32_t B, s0 = 0;
     if (p.key_range) {
         d.kmin = ~p.key_range[0];
         const uint32_t kmax = p.key_range[1];
@@ -216,13 +221,17 @@ __device__ __forceinline__ Digit digit_params(const PassArgs& p) {
         // an empty range ({0, 0}: nothing visible) keeps no key: every slot is then culled (0xffffffff)
         d.lim = kmax >= d.kmin ? kmax - d.kmin : 0xfffffffeu;
         if (kmax < d.kmin) d.kmin = 0u;
+        if (p.coarse && B > p.coarse) {
+            s0 = B - p.coarse;
+            B = p.coarse;
+        }
     } else {
         d.kmin = 0u;
         d.lim = 0xffffffffu;
         B = p.bits;
     }
     d.w = max(1u, (B + p.passes - 1u) / p.passes);
-    d.shift = p.pass * d.w;
+    d.shift = s0 + p.pass * d.w;
     d.mask = (1u << d.w) - 1u;
     return d;
 }
@@ -283,6 +292,8 @@ struct RadixViewArgs {
     uint32_t** pay_io = nullptr;
     uint32_t** pay_alt = nullptr;
     bool drop_first = false;  // see radix_sort_pairs
+    uint32_t coarse = 0;      // see PassArgs::coarse
+    bool keys_last = true;    // the last pass writes the sorted keys (else keys_io keeps its input)
 };
 int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
                            hipStream_t s, int first_pass = 0);
@@ -302,7 +313,7 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
                      int bits, int passes, const uint32_t* key_range, uint32_t* tmp,
                      uint32_t* totals, hipStream_t s, const uint2* rect_in = nullptr,
                      uint32_t** pay_io = nullptr, uint32_t** pay_alt = nullptr, int first_pass = 0,
-                     bool drop_first = false);
+                     bool drop_first = false, uint32_t coarse = 0, bool keys_last = true);
 // drop_first (needs key_range): the keys are the fused cull's n slots; the
 // first pass reads all n and drops the culled ones (PassArgs::drop), later
 // passes run over the device count n_dev = V.
@@ -411,7 +422,18 @@ uint32_t clamp_stage_limit(long v);
 int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted, uint32_t n_vis,
                    int tiles_x, uint32_t* tmp, uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals,
                    uint32_t stage_limit, hipStream_t s);
-int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
+// Repair of a coarse depth order inside the tile lists (k_tile_ranges): runs of
+// one tile's instances with equal coarse depth keys are put in (full key, slot)
+// order, in place.  coarse == 0 (an exact depth sort): nothing to repair.
+struct RunFix {
+    uint32_t* vals;             // the tile list (slots), repaired in place
+    const uint32_t* slot_keys;  // the full depth key of every slot
+    const uint32_t* key_range;  // the frame's {~kmin, kmax}
+    uint32_t coarse;
+    uint32_t* scratch_keys;     // n_dup words each, free at this point (the tile sort's alternates)
+    uint32_t* scratch_vals;
+};
+int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, const RunFix& fix,
                        hipStream_t s);
 // The binning with the tile sort's first radix pass fused in (composite.hip,
 // k_bin_hist / k_bin_scatter): the instances end in (tile_keys, tile_vals)
@@ -462,6 +484,7 @@ struct FinishView {
     uint2* trect_sorted;
     uint32_t* tile_keys;  // tile-sorted (keys, vals) after the tile sort
     uint32_t* tile_vals;
+    RunFix fix;           // coarse depth order repair (vals, scratch set after the tile sort)
     // chunks, composite, merge
     uint2* ranges;
     uint32_t* chunk_cnt;

@@ -19,6 +19,43 @@ TOL_MAX = 8e-3             # any pixel-channel: a fragment whose alpha sits on t
 TOL_TMIN = 1e-4            # extra error allowed by early termination at t_min = 1e-4
 
 
+def depth_coarse_bits(path="alone") -> int:
+    """A frame depth sort's coarse bits: api.hip kDepthCoarseAlone (gsr_render)
+    or kDepthCoarseViews (a group's frames); GSR_DEPTH_COARSE[_ALONE|_VIEWS]=0:
+    exact."""
+    import os
+    bits = 16 if path == "alone" else 0
+    for name in ("GSR_DEPTH_COARSE", "GSR_DEPTH_COARSE_" + path.upper()):
+        v = os.environ.get(name)
+        if v is not None and (int(v) == 0 or 8 <= int(v) <= 24):
+            bits = int(v)
+    return bits
+
+
+def frame_depth_order(vs, coarse=None):
+    """The order a frame's depth sort leaves (GSR_DEBUG_DEPTH_ORDER), as Gaussian
+    ids front to back.  Exact: the reverse of the GL draw order (ties: descending
+    id).  Coarse (the default, api.hip kDepthCoarse): only the top `coarse` bits
+    of the frame's key range (key = order-preserving bits of -z, minus the
+    smallest visible key) are ordered, equal coarse keys by descending id; the
+    tile lists are still exact (k_tile_ranges restores each run)."""
+    vis = vs["visible"]
+    f2b = O.sort_back_to_front(vs["view_z"], vis)[::-1]
+    coarse = depth_coarse_bits("alone") if coarse is None else coarse
+    if coarse == 0:
+        return f2b
+    gid = np.nonzero(vis)[0]
+    if gid.size == 0:
+        return f2b
+    b = (-vs["view_z"][gid].astype(np.float32)).view(np.uint32).astype(np.uint64)
+    key = np.where(b & 0x80000000, ~b & 0xFFFFFFFF, b | 0x80000000)
+    kmin, kmax = int(key.min()), int(key.max())
+    B = (kmax - kmin).bit_length()
+    s0 = max(0, B - coarse)
+    ck = (key - kmin) >> np.uint64(s0)
+    return gid[np.lexsort((-gid, ck))]
+
+
 def uniforms_for(cam: Camera, settings=None, **over):
     """Oracle uniform dict from a Camera + RenderSettings (same inputs the GPU gets)."""
     V = cam.get_view_matrix()
@@ -59,7 +96,7 @@ def gpu_frame(g, cam, settings, with_debug=False, radii=False):
     settings.out_layout = 1
     render_into(ctx, scene, camera_from(cam), settings, out, rad)
     torch.cuda.synchronize()
-    res = {"image": out.cpu().numpy(), "stats": ctx.stats()}
+    res = {"image": out.cpu().numpy(), "stats": ctx.stats(), "depth_coarse": depth_coarse_bits("alone")}
     if radii:
         res["radii"] = rad.cpu().numpy()
     if with_debug:
@@ -128,7 +165,8 @@ def batched_frames(scene, cams, settings, group=4, debug_views=()):
     torch.cuda.synchronize()
     res = []
     for v, (ctx, out) in enumerate(zip(ctxs, outs)):
-        r = {"image": out.permute(1, 2, 0).contiguous().cpu().numpy(), "stats": ctx.stats()}
+        r = {"image": out.permute(1, 2, 0).contiguous().cpu().numpy(), "stats": ctx.stats(),
+             "depth_coarse": depth_coarse_bits("views")}
         if v in debug_views:
             r.update(grab_debug(ctx, r["stats"]))
         res.append(r)

@@ -6,7 +6,8 @@ import pytest
 from gsviewer_amd.camera import Camera, euler_to_rotation_matrix
 from gsviewer_amd.gaussian_data import garden_standin, naive_gaussian, random_scene
 from oracle import gl_oracle as O
-from helpers import (TOL_TMIN, alpha_box_rects, compare_images, decode_records, kept_fragments, narrowed_rects,
+from helpers import (TOL_TMIN, alpha_box_rects, compare_images, decode_records, frame_depth_order, kept_fragments,
+                     narrowed_rects,
                      tile_lists_for, expected_interval_form, expected_quadratic, gpu_frame,
                      uniforms_for)
 
@@ -97,9 +98,9 @@ def test_depth_order_and_tile_lists_exact(gpu):
     U = uniforms_for(cam)
     vs = O.vertex_stage(g.flat(), 3, U)
     vis_desc = np.nonzero(vs["visible"])[0][::-1]
-    # global front-to-back order == reverse of the GL draw order
-    f2b = O.sort_back_to_front(vs["view_z"], vs["visible"])[::-1]
-    np.testing.assert_array_equal(vis_desc[res["depth_order"]], f2b)
+    # the frame's global order: the coarse depth order (helpers.frame_depth_order),
+    # or, with GSR_DEPTH_COARSE=0, the reverse of the GL draw order
+    np.testing.assert_array_equal(vis_desc[res["depth_order"]], frame_depth_order(vs, res["depth_coarse"]))
     # per-tile instance lists == GL order restricted to the tile, reversed, over
     # the quads narrowed by the alpha box
     rects = narrowed_rects(res, vs, U)

@@ -35,7 +35,7 @@ def _settings(**kw):
 
 
 def _frames(monkeypatch, env, g, scene, cams):
-    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE", "GSR_FUSED_CULL"):
+    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE", "GSR_FUSED_CULL", "GSR_DEPTH_COARSE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
