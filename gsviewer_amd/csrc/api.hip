@@ -191,6 +191,7 @@ struct gsr_context {
     // depth sort of a frame: the top bits of its key range, the exact order restored per tile list by
     // k_tile_ranges (GSR_DEPTH_COARSE[_ALONE|_VIEWS]=0: every bit, depth_passes_*)
     uint32_t depth_coarse_alone = kDepthCoarseAlone;
+    gsr::DevBuf<uint32_t> tpay_a, tpay_b;  // the instances' depth keys through the tile sort (coarse order repair)
     uint32_t depth_coarse_views = kDepthCoarseViews;
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
     uint32_t seq = 0;                       // frame sequence number the host waits for
@@ -243,6 +244,7 @@ void each_buf(gsr_context* c, F&& f) {
     f(c->vis_mask); f(c->wave_counts); f(c->block_ranges); f(c->scan_tmp); f(c->recs);
     f(c->keys_a); f(c->keys_b); f(c->vals_a); f(c->vals_b); f(c->trect); f(c->trect_sorted);
     f(c->rect4_a); f(c->rect4_b); f(c->bin_tmp); f(c->tkeys_a); f(c->tkeys_b); f(c->tvals_a); f(c->tvals_b);
+    f(c->tpay_a); f(c->tpay_b);
     f(c->radix_tmp); f(c->zero); f(c->chunk_cnt); f(c->chunk_base); f(c->chunk_desc); f(c->chunk_order);
     f(c->partial); f(c->tmax); f(c->done_ctr);
 }
@@ -470,10 +472,14 @@ int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const 
     f.coarse = 0;
     if (f.n == 0) return GSR_OK;
     f.coarse = c->depth_passes_now ? c->depth_coarse_alone : c->depth_coarse_views;
-    if (f.coarse)  // the last pass writes no keys: keys_a keeps every slot's key for the repair
+    // The repair reads each instance's depth key: with the fused binning the sorted keys (f.ka) travel with the
+    // instances (binning, tile sort payload); otherwise the last pass writes no keys, so keys_a keeps every slot's
+    // key to gather.
+    if (f.coarse)
         return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, (int)f.coarse,
                                 coarse_passes(f.coarse), key_range, c->radix_tmp.p, totals, s,
-                                f.packed ? c->trect.p : nullptr, &f.pa, &f.pb, 0, c->fused_cull, f.coarse, false);
+                                f.packed ? c->trect.p : nullptr, &f.pa, &f.pb, 0, c->fused_cull, f.coarse,
+                                c->bin_fused);
     return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32,
                             c->depth_passes_now ? c->depth_passes_now : kDepthPasses, key_range,
                             c->radix_tmp.p, totals, s, f.packed ? c->trect.p : nullptr, &f.pa, &f.pb, 0,
@@ -796,6 +802,10 @@ int gsr_context_reserve(gsr_context* c, int64_t n, int32_t width, int32_t height
     if ((rc = c->tkeys_b.ensure(d, "tile_keys"))) return rc;
     if ((rc = c->tvals_a.ensure(d, "tile_vals"))) return rc;
     if ((rc = c->tvals_b.ensure(d, "tile_vals"))) return rc;
+    if (c->depth_coarse_alone && c->bin_fused) {  // a frame alone's depth keys through the tile sort
+        if ((rc = c->tpay_a.ensure(d, "tile_pay"))) return rc;
+        if ((rc = c->tpay_b.ensure(d, "tile_pay"))) return rc;
+    }
     if ((rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(d), radix_tmp_elems(un), rhist}), "radix_tmp"))) return rc;
     const size_t mc = (size_t)num_tiles + d / std::min(c->chunk, c->chunk_views) + 1;
     if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
@@ -1116,6 +1126,8 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     const int tbits = bits_for((uint32_t)num_tiles);
     const int tpasses = radix_passes_for(tbits);
     const bool fused = c->bin_fused;
+    const bool carry = f.coarse && fused;  // the instances' depth keys ride along (coarse order repair)
+    uint32_t *tpa = c->tpay_a.p, *tpb = c->tpay_b.p;
     if (n_dup > 0) {
         if ((rc = c->tkeys_a.ensure(n_dup, "tile_keys"))) return rc;
         if ((rc = c->tkeys_b.ensure(n_dup, "tile_keys"))) return rc;
@@ -1125,10 +1137,13 @@ int gsr_render_finish(gsr_context* c, void* stream) {
                                                 bin_hist_elems(n_vis, tbits > 0 ? tbits : 1, tpasses > 0 ? tpasses : 1)}),
                                       "radix_tmp")))
             return rc;
+        if (carry && ((rc = c->tpay_a.ensure(n_dup, "tile_pay"))) == 0) rc = c->tpay_b.ensure(n_dup, "tile_pay");
+        if (rc) return rc;
+        tpa = c->tpay_a.p, tpb = c->tpay_b.p;
         if (fused)  // the tile sort's pass 0 in the binning: instances leave it ordered by digit 0
             rc = launch_binning_sorted(f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, u.tiles_x, tbits, tpasses,
                                        c->radix_tmp.p, c->zero.p + zl.totals_tile, c->trect_sorted.p, c->tkeys_a.p,
-                                       c->tvals_a.p, s);
+                                       c->tvals_a.p, s, carry ? f.ka : nullptr, carry ? c->tpay_a.p : nullptr);
         else
             rc = launch_binning(f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, u.tiles_x, c->bin_tmp.p,
                                 c->trect_sorted.p, c->tkeys_a.p, c->tvals_a.p, c->bin_stage_limit, s);
@@ -1139,8 +1154,9 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     if ((rc = prof_record(c, slot, EV_DUPW, s))) return rc;
     uint32_t *tka = c->tkeys_a.p, *tkb = c->tkeys_b.p, *tva = c->tvals_a.p, *tvb = c->tvals_b.p;
     if (n_dup > 0) {
-        if (tbits > 0 && (rc = sort_pairs(c, &tka, &tva, &tkb, &tvb, false, n_dup, nullptr, tbits, tpasses, nullptr,
-                                          c->zero.p + zl.totals_tile, s, fused ? 1 : 0)))
+        if (tbits > 0 && (rc = radix_sort_pairs(&tka, &tva, &tkb, &tvb, false, n_dup, nullptr, tbits, tpasses, nullptr,
+                                                c->radix_tmp.p, c->zero.p + zl.totals_tile, s, nullptr,
+                                                carry ? &tpa : nullptr, carry ? &tpb : nullptr, fused ? 1 : 0)))
             return rc;
         tile_list = tva;
         c->last_tile_list = tva;
@@ -1148,7 +1164,7 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     if ((rc = prof_record(c, slot, EV_TSORT, s))) return rc;
     if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, ranges,
                                               RunFix{tva, c->keys_a.p, c->zero.p + zl.key_range, f.coarse,
-                                                     tkb, tvb},
+                                                     tkb, tvb, carry ? tpa : nullptr},
                                               s)))
         return rc;
 

@@ -237,10 +237,11 @@ __global__ __launch_bounds__(kThreads) void k_bin_write_views(BinViews vs, int t
 // The instances leave the binning already sorted by digit 0: the tile sort's
 // pass-0 upsweep and scatter launches and one read + write of every instance
 // are gone.  The remaining passes run as before (radix_sort_pairs from pass 1).
-template <int kCB>
+template <int kCB, bool kKeys = false>
 struct BinScatterLds {
     uint32_t k[kBinStage], v[kBinStage];    // a window of the block's instances, generation order
     uint32_t k2[kBinStage], v2[kBinStage];  // ... restaged in digit order
+    uint32_t u[kKeys ? kBinStage : 1], u2[kKeys ? kBinStage : 1];  // their splats' depth keys (kKeys)
     uint16_t wcnt[kThreads / 64][1 << kCB];  // per-wave digit counts, then per-wave prefixes
     uint32_t dbase[1 << kCB];                // window-local digit offsets
     uint32_t gbase[1 << kCB];                // global position of the digit's next instance
@@ -266,7 +267,8 @@ __device__ __forceinline__ void instance_at(uint32_t idx, const uint32_t* own_o,
                                             const uint32_t* __restrict__ sorted_ids,
                                             const uint2* __restrict__ trect_sorted,
                                             const uint32_t* __restrict__ rect4_sorted, int tiles_x, uint32_t& key,
-                                            uint32_t& val) {
+                                            uint32_t& val, const uint32_t* __restrict__ sorted_keys = nullptr,
+                                            uint32_t* skey = nullptr) {
     uint32_t lo = 0, hi = kThreads;  // own_o[lo] <= idx < own_o[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -288,6 +290,7 @@ __device__ __forceinline__ void instance_at(uint32_t idx, const uint32_t* own_o,
             const uint32_t dy = local / w;
             key = (ty0 + dy) * (uint32_t)tiles_x + tx0 + (local - dy * w);
             val = sorted_ids[r];
+            if (sorted_keys) *skey = sorted_keys[r];
             return;
         }
         local -= n;
@@ -386,14 +389,18 @@ __global__ __launch_bounds__(kThreads) void k_bin_hist(const uint32_t* __restric
                            h, own);
 }
 
-template <bool kPacked, int kCB>
+// kKeys: each instance also carries its splat's depth key (sorted_keys, in
+// depth order) to inst_keys, for the coarse depth order's run repair.
+template <bool kPacked, int kCB, bool kKeys = false>
 __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_ids,
                                             const uint2* __restrict__ trect_sorted,
                                             const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis, int tiles_x,
                                             const PassArgs& pa, const uint32_t* __restrict__ hist_off,
                                             const uint32_t* __restrict__ totals, uint32_t nbb,
                                             uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ tile_vals,
-                                            uint32_t blk, BinScatterLds<kCB>& L) {
+                                            uint32_t blk, BinScatterLds<kCB, kKeys>& L,
+                                            const uint32_t* __restrict__ sorted_keys = nullptr,
+                                            uint32_t* __restrict__ inst_keys = nullptr) {
     constexpr int kCap = 1 << kCB;
     constexpr int kDpt = kCap / kThreads > 0 ? kCap / kThreads : 1;  // digits per thread
     constexpr int kWaveItems = kBinStage / (kThreads / 64);           // window items per wave
@@ -414,13 +421,14 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
     }
     // this thread's 4 consecutive depth-sorted splats
     const uint32_t base = blk * kBinBlock + threadIdx.x * kBinItems;
-    uint32_t id[kBinItems];
+    uint32_t id[kBinItems], sk[kBinItems];
     uint2 tr[kBinItems];
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
         const uint32_t r = base + k;
         id[k] = r < n_vis ? sorted_ids[r] : 0u;
+        if constexpr (kKeys) sk[k] = r < n_vis ? sorted_keys[r] : 0u;
         if constexpr (kPacked)
             tr[k] = r < n_vis ? unpack_rect(rect4_sorted[r]) : make_uint2(0xffffu, 0u);
         else
@@ -457,7 +465,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
             const uint32_t cnt = min((uint32_t)kBinStage, total - c0);
             for (uint32_t j = threadIdx.x; j < cnt; j += kThreads)
                 instance_at<kPacked>(c0 + j, L.own_o, blk, sorted_ids, trect_sorted, rect4_sorted, tiles_x, L.k[j],
-                                     L.v[j]);
+                                     L.v[j], kKeys ? sorted_keys : nullptr, kKeys ? &L.u[j] : nullptr);
         } else if (o < c0 + (uint32_t)kBinStage && o + s > c0) {
             uint32_t idx = o;
 #pragma unroll
@@ -470,6 +478,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
                         if (idx >= c0 && idx < c0 + (uint32_t)kBinStage) {
                             L.k[idx - c0] = ty * (uint32_t)tiles_x + tx;
                             L.v[idx - c0] = id[k];
+                            if constexpr (kKeys) L.u[idx - c0] = sk[k];
                         }
             }
         }
@@ -538,6 +547,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
                 const uint32_t p = L.dbase[d] + L.wcnt[w][d] + rank[r];
                 L.k2[p] = key[r];
                 L.v2[p] = L.v[j];
+                if constexpr (kKeys) L.u2[p] = L.u[j];
             }
         }
         __syncthreads();
@@ -548,6 +558,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
             const uint32_t g = L.gbase[d] + (j - L.dbase[d]);
             tile_keys[g] = kk;
             tile_vals[g] = L.v2[j];
+            if constexpr (kKeys) inst_keys[g] = L.u2[j];
         }
         __syncthreads();
 #pragma unroll
@@ -559,7 +570,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
     }
 }
 
-template <bool kPacked, int kCB>
+template <bool kPacked, int kCB, bool kKeys>
 __global__ __launch_bounds__(kThreads) void k_bin_scatter(const uint32_t* __restrict__ sorted_ids,
                                                           const uint2* __restrict__ trect_sorted,
                                                           const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
@@ -567,10 +578,12 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(const uint32_t* __rest
                                                           const uint32_t* __restrict__ hist_off,
                                                           const uint32_t* __restrict__ totals, uint32_t nbb,
                                                           uint32_t* __restrict__ tile_keys,
-                                                          uint32_t* __restrict__ tile_vals) {
-    __shared__ BinScatterLds<kCB> L;
-    bin_scatter<kPacked, kCB>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tiles_x, pa, hist_off, totals, nbb,
-                              tile_keys, tile_vals, blockIdx.x, L);
+                                                          uint32_t* __restrict__ tile_vals,
+                                                          const uint32_t* __restrict__ sorted_keys,
+                                                          uint32_t* __restrict__ inst_keys) {
+    __shared__ BinScatterLds<kCB, kKeys> L;
+    bin_scatter<kPacked, kCB, kKeys>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tiles_x, pa, hist_off, totals,
+                                     nbb, tile_keys, tile_vals, blockIdx.x, L, sorted_keys, inst_keys);
 }
 
 // Views of a group (blockIdx.y = view): hist / totals per view.
@@ -618,15 +631,17 @@ constexpr int kRangeItems = 16;
 // threads read the run's slots only for their (tile, coarse key), which the
 // permutation leaves unchanged.  O(L^2), but L is a handful at C2.
 __device__ __noinline__ void fix_run(const uint32_t* __restrict__ keys, uint32_t n, uint32_t* vals,
-                                     const uint32_t* __restrict__ slot_keys, uint32_t* __restrict__ scratch_keys,
-                                     uint32_t* __restrict__ scratch_vals, uint32_t i, uint32_t tile, uint32_t cv,
-                                     uint32_t kmin, uint32_t s0) {
-    uint32_t fprev = slot_keys[vals[i]];
+                                     const uint32_t* __restrict__ slot_keys, const uint32_t* __restrict__ inst_keys,
+                                     uint32_t* __restrict__ scratch_keys, uint32_t* __restrict__ scratch_vals,
+                                     uint32_t i, uint32_t tile, uint32_t cv, uint32_t kmin, uint32_t s0) {
+    // the depth key of list position q (inst_keys: carried by the binning and the tile sort; else gathered)
+    auto key_at = [&](uint32_t q) { return inst_keys ? inst_keys[q] : slot_keys[vals[q]]; };
+    uint32_t fprev = key_at(i);
     uint32_t L = 1;
     bool descent = false;
     for (uint32_t q = i + 1; q < n; ++q) {
         if (keys[q] != tile) break;
-        const uint32_t f = slot_keys[vals[q]];
+        const uint32_t f = key_at(q);
         if (((f - kmin) >> s0) != cv) break;
         descent |= f < fprev;
         fprev = f;
@@ -636,7 +651,7 @@ __device__ __noinline__ void fix_run(const uint32_t* __restrict__ keys, uint32_t
     for (uint32_t r = 0; r < L; ++r) {
         const uint32_t sl = vals[i + r];
         scratch_vals[i + r] = sl;
-        scratch_keys[i + r] = slot_keys[sl];
+        scratch_keys[i + r] = key_at(i + r);
     }
     for (uint32_t r = 0; r < L; ++r) {
         const uint32_t kr = scratch_keys[i + r], vr = scratch_vals[i + r];
@@ -697,13 +712,30 @@ __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ key
             if (j >= kRangeItems) kw[j] = ok ? keys[base + j] : 0xffffffffu;
         }
     }
-    const uint32_t vprev = base > 0 ? fx.vals[base - 1] : 0u;
+    uint32_t fprev;
+    if (fx.inst_keys) {  // the keys carried with the instances: coalesced, no gathers
+        if (base + kFixWin <= n) {
+            const uint4* pf = reinterpret_cast<const uint4*>(fx.inst_keys + base);
+#pragma unroll
+            for (int q = 0; q < kFixWin / 4; ++q) {
+                const uint4 v = pf[q];
+                fw[4 * q] = v.x; fw[4 * q + 1] = v.y; fw[4 * q + 2] = v.z; fw[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kFixWin; ++j) fw[j] = base + j < n ? fx.inst_keys[base + j] : 0u;
+        }
+        fprev = base > 0 ? fx.inst_keys[base - 1] : 0u;
+    }
+    const uint32_t vprev = base > 0 && !fx.inst_keys ? fx.vals[base - 1] : 0u;
     uint32_t kmin;  // (the window's loads are in flight meanwhile)
     const uint32_t s0 = coarse_shift(fx.key_range, fx.coarse, kmin);
     if (s0 == 0u) return;  // the coarse sort was exact
+    if (!fx.inst_keys) {  // gathered by slot
 #pragma unroll
-    for (int j = 0; j < kFixWin; ++j) fw[j] = base + j < n ? fx.slot_keys[vw[j]] : 0u;
-    const uint32_t fprev = base > 0 ? fx.slot_keys[vprev] : 0u;
+        for (int j = 0; j < kFixWin; ++j) fw[j] = base + j < n ? fx.slot_keys[vw[j]] : 0u;
+        fprev = base > 0 ? fx.slot_keys[vprev] : 0u;
+    }
     // same bit j: items j and j + 1 are one run (both valid, same tile and coarse key)
     uint32_t same = 0;
 #pragma unroll
@@ -729,7 +761,7 @@ __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ key
 #pragma unroll
         for (int j = 0; j < kFixWin; ++j)
             if (j == st) kst = kw[j], fst = fw[j];
-        fix_run(keys, n, fx.vals, fx.slot_keys, fx.scratch_keys, fx.scratch_vals, base + (uint32_t)st, kst,
+        fix_run(keys, n, fx.vals, fx.slot_keys, fx.inst_keys, fx.scratch_keys, fx.scratch_vals, base + (uint32_t)st, kst,
                 (fst - kmin) >> s0, kmin, s0);
     }
     const uint32_t pairs = same & own;  // adjacent pairs inside one owned run
@@ -2123,7 +2155,8 @@ size_t bin_hist_elems(size_t n_vis, int tbits, int passes) {
 
 int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted,
                           uint32_t n_vis, int tiles_x, int tbits, int passes, uint32_t* hist, uint32_t* totals,
-                          uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s) {
+                          uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s,
+                          const uint32_t* sorted_keys, uint32_t* inst_keys) {
     if (n_vis == 0) return GSR_OK;
     const int tb = tbits > 0 ? tbits : 1;  // one tile: a single digit value, generation order kept
     const int ps = passes > 0 ? passes : 1;
@@ -2135,9 +2168,17 @@ int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const 
 #define GSR_BIN_HIST(P, CB)                                                                                 \
     k_bin_hist<P, CB><<<nbb, kThreads, 0, s>>>(sorted_ids, trect, rect4_sorted, n_vis, tiles_x, pa, hist, nbb, \
                                                trect_sorted)
-#define GSR_BIN_SCATTER(P, CB)                                                                              \
-    k_bin_scatter<P, CB><<<nbb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tiles_x, pa, \
-                                                  hist, totals, nbb, tile_keys, tile_vals)
+#define GSR_BIN_SCATTER(P, CB)                                                                                  \
+    do {                                                                                                        \
+        if (inst_keys)                                                                                          \
+            k_bin_scatter<P, CB, true><<<nbb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis,     \
+                                                                tiles_x, pa, hist, totals, nbb, tile_keys,         \
+                                                                tile_vals, sorted_keys, inst_keys);                \
+        else                                                                                                    \
+            k_bin_scatter<P, CB, false><<<nbb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis,    \
+                                                                 tiles_x, pa, hist, totals, nbb, tile_keys,        \
+                                                                 tile_vals, nullptr, nullptr);                     \
+    } while (0)
     if (w <= 8) {
         if (packed) GSR_BIN_HIST(true, 8); else GSR_BIN_HIST(false, 8);
     } else {

@@ -432,6 +432,8 @@ struct RunFix {
     uint32_t coarse;
     uint32_t* scratch_keys;     // n_dup words each, free at this point (the tile sort's alternates)
     uint32_t* scratch_vals;
+    const uint32_t* inst_keys = nullptr;  // each list position's depth key (binning + tile sort payload), else
+                                          // gathered through slot_keys
 };
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, const RunFix& fix,
                        hipStream_t s);
@@ -444,7 +446,8 @@ int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges,
 size_t bin_hist_elems(size_t n_vis, int tbits, int passes);
 int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted,
                           uint32_t n_vis, int tiles_x, int tbits, int passes, uint32_t* hist, uint32_t* totals,
-                          uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s);
+                          uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s,
+                          const uint32_t* sorted_keys = nullptr, uint32_t* inst_keys = nullptr);
 // chunk_cnt must hold chunk_cnt_elems(num_tiles) entries (block totals after the tiles);
 // order: one entry per chunk (dispatch position -> chunk slot)
 size_t chunk_cnt_elems(int num_tiles);

@@ -390,6 +390,9 @@ static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_a
     // upper bound of the radix over the passes (device-chosen widths never exceed it)
     const uint32_t radix_max = 1u << ((bits + passes - 1) / passes);
     bool ident = identity_vals;
+    // a payload: the packed rects (rect_in, read by the first pass), or pay_io alone (the tile sort carrying
+    // the instances' depth keys)
+    const bool pay = rect_in != nullptr || pay_io != nullptr;
     for (int p = first_pass; p < passes; ++p) {
         const PassArgs pa{key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p,
                           drop_first && p == first_pass ? 1u : 0u, coarse};
@@ -399,7 +402,7 @@ static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_a
         GSR_LAUNCH_CHECK("rs_upsweep");
         k_rs_offsets<<<(radix_max + kOffWaves - 1) / kOffWaves, 64 * kOffWaves, 0, s>>>(tmp, nt, pa, totals);
         GSR_LAUNCH_CHECK("rs_offsets");
-        if (rect_in) {
+        if (pay) {
             k_rs_scatter<kR, true, kCB><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, kout, *vals_alt, n_dev,
                                                            (uint32_t)n, pa, tmp, totals, nt, p == first_pass ? rect_in : nullptr,
                                                            *pay_io, *pay_alt);
@@ -415,7 +418,7 @@ static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_a
             t = *keys_io; *keys_io = *keys_alt; *keys_alt = t;
         }
         t = *vals_io; *vals_io = *vals_alt; *vals_alt = t;
-        if (rect_in) {
+        if (pay) {
             t = *pay_io; *pay_io = *pay_alt; *pay_alt = t;
         }
     }
