@@ -237,11 +237,10 @@ __global__ __launch_bounds__(kThreads) void k_bin_write_views(BinViews vs, int t
 // The instances leave the binning already sorted by digit 0: the tile sort's
 // pass-0 upsweep and scatter launches and one read + write of every instance
 // are gone.  The remaining passes run as before (radix_sort_pairs from pass 1).
-template <int kCB, bool kKeys = false>
+template <int kCB>
 struct BinScatterLds {
     uint32_t k[kBinStage], v[kBinStage];    // a window of the block's instances, generation order
     uint32_t k2[kBinStage], v2[kBinStage];  // ... restaged in digit order
-    uint32_t u[kKeys ? kBinStage : 1], u2[kKeys ? kBinStage : 1];  // their splats' depth keys (kKeys)
     uint16_t wcnt[kThreads / 64][1 << kCB];  // per-wave digit counts, then per-wave prefixes
     uint32_t dbase[1 << kCB];                // window-local digit offsets
     uint32_t gbase[1 << kCB];                // global position of the digit's next instance
@@ -267,8 +266,7 @@ __device__ __forceinline__ void instance_at(uint32_t idx, const uint32_t* own_o,
                                             const uint32_t* __restrict__ sorted_ids,
                                             const uint2* __restrict__ trect_sorted,
                                             const uint32_t* __restrict__ rect4_sorted, int tiles_x, uint32_t& key,
-                                            uint32_t& val, const uint32_t* __restrict__ sorted_keys = nullptr,
-                                            uint32_t* skey = nullptr) {
+                                            uint32_t& val, bool sorted_pos = false) {
     uint32_t lo = 0, hi = kThreads;  // own_o[lo] <= idx < own_o[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -289,8 +287,7 @@ __device__ __forceinline__ void instance_at(uint32_t idx, const uint32_t* own_o,
             const uint32_t w = tx1 - tx0 + 1u;
             const uint32_t dy = local / w;
             key = (ty0 + dy) * (uint32_t)tiles_x + tx0 + (local - dy * w);
-            val = sorted_ids[r];
-            if (sorted_keys) *skey = sorted_keys[r];
+            val = sorted_pos ? r : sorted_ids[r];
             return;
         }
         local -= n;
@@ -390,7 +387,10 @@ __global__ __launch_bounds__(kThreads) void k_bin_hist(const uint32_t* __restric
 }
 
 // kKeys: each instance also carries its splat's depth key (sorted_keys, in
-// depth order) to inst_keys, for the coarse depth order's run repair.
+// depth order) to inst_keys, for the coarse depth order's run repair.  The
+// window then stages each instance's depth-sorted position instead of its
+// slot, and the writes look up both (this block's 1024 splats: cache-hot):
+// staging the keys as well took 16 KB more LDS (a block fewer per CU).
 template <bool kPacked, int kCB, bool kKeys = false>
 __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_ids,
                                             const uint2* __restrict__ trect_sorted,
@@ -398,7 +398,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
                                             const PassArgs& pa, const uint32_t* __restrict__ hist_off,
                                             const uint32_t* __restrict__ totals, uint32_t nbb,
                                             uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ tile_vals,
-                                            uint32_t blk, BinScatterLds<kCB, kKeys>& L,
+                                            uint32_t blk, BinScatterLds<kCB>& L,
                                             const uint32_t* __restrict__ sorted_keys = nullptr,
                                             uint32_t* __restrict__ inst_keys = nullptr) {
     constexpr int kCap = 1 << kCB;
@@ -421,14 +421,13 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
     }
     // this thread's 4 consecutive depth-sorted splats
     const uint32_t base = blk * kBinBlock + threadIdx.x * kBinItems;
-    uint32_t id[kBinItems], sk[kBinItems];
+    uint32_t id[kBinItems];
     uint2 tr[kBinItems];
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
         const uint32_t r = base + k;
-        id[k] = r < n_vis ? sorted_ids[r] : 0u;
-        if constexpr (kKeys) sk[k] = r < n_vis ? sorted_keys[r] : 0u;
+        id[k] = kKeys ? r : r < n_vis ? sorted_ids[r] : 0u;  // kKeys: the sorted position
         if constexpr (kPacked)
             tr[k] = r < n_vis ? unpack_rect(rect4_sorted[r]) : make_uint2(0xffffu, 0u);
         else
@@ -465,7 +464,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
             const uint32_t cnt = min((uint32_t)kBinStage, total - c0);
             for (uint32_t j = threadIdx.x; j < cnt; j += kThreads)
                 instance_at<kPacked>(c0 + j, L.own_o, blk, sorted_ids, trect_sorted, rect4_sorted, tiles_x, L.k[j],
-                                     L.v[j], kKeys ? sorted_keys : nullptr, kKeys ? &L.u[j] : nullptr);
+                                     L.v[j], kKeys);
         } else if (o < c0 + (uint32_t)kBinStage && o + s > c0) {
             uint32_t idx = o;
 #pragma unroll
@@ -478,7 +477,6 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
                         if (idx >= c0 && idx < c0 + (uint32_t)kBinStage) {
                             L.k[idx - c0] = ty * (uint32_t)tiles_x + tx;
                             L.v[idx - c0] = id[k];
-                            if constexpr (kKeys) L.u[idx - c0] = sk[k];
                         }
             }
         }
@@ -547,7 +545,6 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
                 const uint32_t p = L.dbase[d] + L.wcnt[w][d] + rank[r];
                 L.k2[p] = key[r];
                 L.v2[p] = L.v[j];
-                if constexpr (kKeys) L.u2[p] = L.u[j];
             }
         }
         __syncthreads();
@@ -557,8 +554,13 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
             const uint32_t d = dg.of(kk);
             const uint32_t g = L.gbase[d] + (j - L.dbase[d]);
             tile_keys[g] = kk;
-            tile_vals[g] = L.v2[j];
-            if constexpr (kKeys) inst_keys[g] = L.u2[j];
+            if constexpr (kKeys) {
+                const uint32_t r = L.v2[j];
+                tile_vals[g] = sorted_ids[r];
+                inst_keys[g] = sorted_keys[r];
+            } else {
+                tile_vals[g] = L.v2[j];
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -581,7 +583,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(const uint32_t* __rest
                                                           uint32_t* __restrict__ tile_vals,
                                                           const uint32_t* __restrict__ sorted_keys,
                                                           uint32_t* __restrict__ inst_keys) {
-    __shared__ BinScatterLds<kCB, kKeys> L;
+    __shared__ BinScatterLds<kCB> L;
     bin_scatter<kPacked, kCB, kKeys>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tiles_x, pa, hist_off, totals,
                                      nbb, tile_keys, tile_vals, blockIdx.x, L, sorted_keys, inst_keys);
 }

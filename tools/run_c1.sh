@@ -1,9 +1,9 @@
-# coarse depth order with the keys carried by the binning and the tile sort: GPU tests, kernel traces, bench A/B
+# coarse depth order (keys via sorted positions in the binning): GPU tests, kernel traces, bench A/B
 set -o pipefail
-O=gpurun_out/c5
+O=gpurun_out/c6
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit 1
-timeout -k 10 600 bash tools/trace_ab.sh c5 "GSR_DEPTH_COARSE=0" "GSR_AB_DEFAULT=1" || exit 2
+timeout -k 10 600 python -u -m pytest tests/test_gpu_coarse_depth.py tests/test_gpu_parity.py tests/test_gpu_scale.py tests/test_gpu_variants.py tests/test_gpu_large_splats.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || exit 1
+timeout -k 10 600 bash tools/trace_ab.sh c6 "GSR_DEPTH_COARSE=0" "GSR_AB_DEFAULT=1" || exit 2
 for rep in 1 2; do
 for cfg in "D" "C GSR_DEPTH_COARSE=0"; do
   set -- $cfg; tag=$1; shift
