@@ -803,6 +803,10 @@ __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ key
         if (((own >> j) & 1u) && vw[j] != v0[j]) fx.vals[base + j] = vw[j];
 }
 
+// kFix: the coarse depth order's run repair (a separate instantiation: its
+// registers (153 VGPRs) made the plain kernel wait for room beside the
+// compositors in flight)
+template <bool kFix>
 __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, uint32_t n, uint2* __restrict__ ranges,
                                             uint32_t t, const RunFix& fx) {
     const uint32_t base = t * kRangeItems;
@@ -822,7 +826,7 @@ __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, u
     const uint32_t prev = base > 0 ? keys[base - 1] : 0xffffffffu;
     const uint32_t next = base + kRangeItems < n ? keys[base + kRangeItems] : 0xffffffffu;
     // the run repair first: its window loads are issued before the range stores
-    if (fx.coarse) fix_coarse_runs(keys, n, fx, base, k, prev);
+    if constexpr (kFix) fix_coarse_runs(keys, n, fx, base, k, prev);
 #pragma unroll
     for (int j = 0; j < kRangeItems; ++j) {
         const uint32_t i = base + j;
@@ -834,9 +838,10 @@ __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, u
     }
 }
 
+template <bool kFix>
 __global__ __launch_bounds__(kThreads) void k_tile_ranges(const uint32_t* __restrict__ keys, uint32_t n,
                                                           uint2* __restrict__ ranges, RunFix fx) {
-    tile_ranges(keys, n, ranges, blockIdx.x * kThreads + threadIdx.x, fx);
+    tile_ranges<kFix>(keys, n, ranges, blockIdx.x * kThreads + threadIdx.x, fx);
 }
 
 struct RangeViews {
@@ -846,9 +851,10 @@ struct RangeViews {
     RunFix fix[kMaxViews];
 };
 
+template <bool kFix>
 __global__ __launch_bounds__(kThreads) void k_tile_ranges_views(RangeViews vs) {
     const int v = blockIdx.y;
-    tile_ranges(vs.keys[v], vs.n[v], vs.ranges[v], blockIdx.x * kThreads + threadIdx.x, vs.fix[v]);
+    tile_ranges<kFix>(vs.keys[v], vs.n[v], vs.ranges[v], blockIdx.x * kThreads + threadIdx.x, vs.fix[v]);
 }
 
 struct CompositeArgs {
@@ -2203,7 +2209,10 @@ int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const 
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, const RunFix& fix, hipStream_t s) {
     if (n_dup == 0) return GSR_OK;
     const uint32_t per_block = kThreads * kRangeItems;
-    k_tile_ranges<<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, fix);
+    if (fix.coarse)
+        k_tile_ranges<true><<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, fix);
+    else
+        k_tile_ranges<false><<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, fix);
     GSR_LAUNCH_CHECK("tile_ranges");
     return GSR_OK;
 }
@@ -2396,16 +2405,21 @@ int launch_binning_sorted_views(FinishView* views, uint32_t* const* hist, uint32
 int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s) {
     RangeViews rv{};
     uint32_t n_max = 0;
+    bool fix = false;
     for (int i = 0; i < k; ++i) {
         rv.keys[i] = views[i].tile_keys;
         rv.ranges[i] = views[i].ranges;
         rv.n[i] = views[i].n_dup;
         rv.fix[i] = views[i].fix;
+        fix |= views[i].fix.coarse != 0;
         n_max = std::max(n_max, views[i].n_dup);
     }
     if (n_max == 0) return GSR_OK;
     const uint32_t per_block = kThreads * kRangeItems;
-    k_tile_ranges_views<<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
+    if (fix)
+        k_tile_ranges_views<true><<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
+    else
+        k_tile_ranges_views<false><<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
     GSR_LAUNCH_CHECK("tile_ranges_views");
     return GSR_OK;
 }

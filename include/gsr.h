@@ -303,7 +303,10 @@ int gsr_debug_stall(void* stream, uint32_t microseconds);
  *                          Gaussian, slot n-1-id, N records (culled slots hold
  *                          no record).  Separate cull: compacted, slot s = the
  *                          s-th visible Gaussian in DESCENDING id order, V records.
- *   GSR_DEBUG_DEPTH_ORDER  uint32 record slots, front-to-back
+ *   GSR_DEBUG_DEPTH_ORDER  uint32 record slots, front-to-back.  A frame alone
+ *                          (gsr_render) sorts only the top 16 bits of its depth
+ *                          key range (GSR_DEPTH_COARSE_ALONE, 0 = exact): equal
+ *                          coarse keys in slot order; the tile lists are exact.
  *   GSR_DEBUG_TILE_RANGES  uint32 pairs [begin, end) per 16x16 tile (row-major tiles)
  *   GSR_DEBUG_TILE_LIST    uint32 record slots of all (tile, splat) instances, by tile then depth */
 enum { GSR_DEBUG_RECORDS = 0, GSR_DEBUG_DEPTH_ORDER = 1, GSR_DEBUG_TILE_RANGES = 2, GSR_DEBUG_TILE_LIST = 3 };
