@@ -1,4 +1,4 @@
-# coarse depth order (keys via sorted positions in the binning): GPU tests, kernel traces, bench A/B
+# A/B of the coarse depth order on one box (profiles/r4_s32, run c6): GPU tests, frame-alone kernel traces, bench
 set -o pipefail
 O=gpurun_out/c6
 mkdir -p $O
