@@ -690,16 +690,24 @@ static_assert(kFixWin <= 32, "run masks are 32-bit");
 __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ keys, uint32_t n, const RunFix& fx,
                                                 uint32_t base, const uint32_t (&k)[kRangeItems], uint32_t prev) {
     uint32_t kw[kFixWin], vw[kFixWin], fw[kFixWin];
+    // the window's slots: with carried keys only once a run needs sorting (most windows' runs are in order)
+    auto load_vals = [&]() {
+        if (base + kFixWin <= n) {
+            const uint4* pv = reinterpret_cast<const uint4*>(fx.vals + base);  // (base: a multiple of 16)
+#pragma unroll
+            for (int q = 0; q < kFixWin / 4; ++q) {
+                const uint4 v = pv[q];
+                vw[4 * q] = v.x; vw[4 * q + 1] = v.y; vw[4 * q + 2] = v.z; vw[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kFixWin; ++j) vw[j] = base + j < n ? fx.vals[base + j] : 0u;
+        }
+    };
 #pragma unroll
     for (int j = 0; j < kRangeItems; ++j) kw[j] = k[j];
     if (base + kFixWin <= n) {
-        const uint4* pv = reinterpret_cast<const uint4*>(fx.vals + base);  // (base: a multiple of 16)
         const uint4* pk = reinterpret_cast<const uint4*>(keys + base + kRangeItems);
-#pragma unroll
-        for (int q = 0; q < kFixWin / 4; ++q) {
-            const uint4 v = pv[q];
-            vw[4 * q] = v.x; vw[4 * q + 1] = v.y; vw[4 * q + 2] = v.z; vw[4 * q + 3] = v.w;
-        }
 #pragma unroll
         for (int q = 0; q < kFixExtra / 4; ++q) {
             const uint4 v = pk[q];
@@ -708,12 +716,9 @@ __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ key
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < kFixWin; ++j) {
-            const bool ok = base + j < n;
-            vw[j] = ok ? fx.vals[base + j] : 0u;
-            if (j >= kRangeItems) kw[j] = ok ? keys[base + j] : 0xffffffffu;
-        }
+        for (int j = kRangeItems; j < kFixWin; ++j) kw[j] = base + j < n ? keys[base + j] : 0xffffffffu;
     }
+    if (!fx.inst_keys) load_vals();  // the keys are gathered through the slots
     uint32_t fprev;
     if (fx.inst_keys) {  // the keys carried with the instances: coalesced, no gathers
         if (base + kFixWin <= n) {
@@ -776,6 +781,7 @@ __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ key
     return;
 #endif
     if (!descent) return;
+    if (fx.inst_keys) load_vals();
     // the longest owned run: rounds of the transposition sort
     uint32_t len = 1, rounds = 1;
 #pragma unroll
