@@ -684,11 +684,19 @@ __device__ __forceinline__ uint32_t coarse_shift(const uint32_t* key_range, uint
 // as many rounds as the longest run, puts each in (full key, slot) order.  A
 // run that reaches the window's end is left to fix_run (global memory).
 constexpr int kFixExtra = 8;
-constexpr int kFixWin = kRangeItems + kFixExtra;
-static_assert(kFixWin <= 32, "run masks are 32-bit");
+// instances per thread of the repairing kernel (GSR_FIX_ITEMS build knob): 8
+// (twice the waves of 16, the window's loads overlap more): 13.9 -> 10.8 us,
+// 12: 12.0 (profiles/r4_s32/c9)
+#ifndef GSR_FIX_ITEMS
+#define GSR_FIX_ITEMS 8
+#endif
+constexpr int kFixItems = GSR_FIX_ITEMS;
+static_assert(kFixItems % 4 == 0 && kFixItems + kFixExtra <= 32, "run masks are 32-bit");
 
+template <int kItems>
 __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ keys, uint32_t n, const RunFix& fx,
-                                                uint32_t base, const uint32_t (&k)[kRangeItems], uint32_t prev) {
+                                                uint32_t base, const uint32_t (&k)[kItems], uint32_t prev) {
+    constexpr int kFixWin = kItems + kFixExtra;
     uint32_t kw[kFixWin], vw[kFixWin], fw[kFixWin];
     // the window's slots: with carried keys only once a run needs sorting (most windows' runs are in order)
     auto load_vals = [&]() {
@@ -705,18 +713,18 @@ __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ key
         }
     };
 #pragma unroll
-    for (int j = 0; j < kRangeItems; ++j) kw[j] = k[j];
+    for (int j = 0; j < kItems; ++j) kw[j] = k[j];
     if (base + kFixWin <= n) {
-        const uint4* pk = reinterpret_cast<const uint4*>(keys + base + kRangeItems);
+        const uint4* pk = reinterpret_cast<const uint4*>(keys + base + kItems);
 #pragma unroll
         for (int q = 0; q < kFixExtra / 4; ++q) {
             const uint4 v = pk[q];
-            kw[kRangeItems + 4 * q] = v.x; kw[kRangeItems + 4 * q + 1] = v.y;
-            kw[kRangeItems + 4 * q + 2] = v.z; kw[kRangeItems + 4 * q + 3] = v.w;
+            kw[kItems + 4 * q] = v.x; kw[kItems + 4 * q + 1] = v.y;
+            kw[kItems + 4 * q + 2] = v.z; kw[kItems + 4 * q + 3] = v.w;
         }
     } else {
 #pragma unroll
-        for (int j = kRangeItems; j < kFixWin; ++j) kw[j] = base + j < n ? keys[base + j] : 0xffffffffu;
+        for (int j = kItems; j < kFixWin; ++j) kw[j] = base + j < n ? keys[base + j] : 0xffffffffu;
     }
     if (!fx.inst_keys) load_vals();  // the keys are gathered through the slots
     uint32_t fprev;
@@ -754,7 +762,7 @@ __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ key
     uint32_t own = cont0 ? 0u : 1u;
 #pragma unroll
     for (int j = 1; j < kFixWin; ++j) {
-        const bool in = ((same >> (j - 1)) & 1u) ? ((own >> (j - 1)) & 1u) != 0u : j < kRangeItems;
+        const bool in = ((same >> (j - 1)) & 1u) ? ((own >> (j - 1)) & 1u) != 0u : j < kItems;
         if (in) own |= 1u << j;
     }
     // a run that may go on past the window: fix_run from its start, out of the register sort
@@ -812,33 +820,33 @@ __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ key
 // kFix: the coarse depth order's run repair (a separate instantiation: its
 // registers (153 VGPRs) made the plain kernel wait for room beside the
 // compositors in flight)
-template <bool kFix>
+template <bool kFix, int kItems = kFix ? kFixItems : kRangeItems>
 __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, uint32_t n, uint2* __restrict__ ranges,
                                             uint32_t t, const RunFix& fx) {
-    const uint32_t base = t * kRangeItems;
+    const uint32_t base = t * kItems;
     if (base >= n) return;
-    uint32_t k[kRangeItems];
-    if (base + kRangeItems <= n) {
+    uint32_t k[kItems];
+    if (base + kItems <= n) {
         const uint4* p = reinterpret_cast<const uint4*>(keys + base);  // (base: a multiple of 16)
 #pragma unroll
-        for (int q = 0; q < kRangeItems / 4; ++q) {
+        for (int q = 0; q < kItems / 4; ++q) {
             const uint4 v = p[q];
             k[4 * q] = v.x; k[4 * q + 1] = v.y; k[4 * q + 2] = v.z; k[4 * q + 3] = v.w;
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < kRangeItems; ++j) k[j] = base + j < n ? keys[base + j] : 0xffffffffu;
+        for (int j = 0; j < kItems; ++j) k[j] = base + j < n ? keys[base + j] : 0xffffffffu;
     }
     const uint32_t prev = base > 0 ? keys[base - 1] : 0xffffffffu;
-    const uint32_t next = base + kRangeItems < n ? keys[base + kRangeItems] : 0xffffffffu;
+    const uint32_t next = base + kItems < n ? keys[base + kItems] : 0xffffffffu;
     // the run repair first: its window loads are issued before the range stores
-    if constexpr (kFix) fix_coarse_runs(keys, n, fx, base, k, prev);
+    if constexpr (kFix) fix_coarse_runs<kItems>(keys, n, fx, base, k, prev);
 #pragma unroll
-    for (int j = 0; j < kRangeItems; ++j) {
+    for (int j = 0; j < kItems; ++j) {
         const uint32_t i = base + j;
         if (i >= n) break;
         const uint32_t before = j == 0 ? prev : k[j - 1];
-        const uint32_t after = (j + 1 < kRangeItems) ? (i + 1 < n ? k[j + 1] : 0xffffffffu) : next;
+        const uint32_t after = (j + 1 < kItems) ? (i + 1 < n ? k[j + 1] : 0xffffffffu) : next;
         if (i == 0 || before != k[j]) ranges[k[j]].x = i;
         if (i == n - 1 || after != k[j]) ranges[k[j]].y = i + 1;
     }
@@ -2214,7 +2222,7 @@ int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const 
 
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, const RunFix& fix, hipStream_t s) {
     if (n_dup == 0) return GSR_OK;
-    const uint32_t per_block = kThreads * kRangeItems;
+    const uint32_t per_block = kThreads * (fix.coarse ? kFixItems : kRangeItems);
     if (fix.coarse)
         k_tile_ranges<true><<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, fix);
     else
@@ -2421,7 +2429,7 @@ int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s) {
         n_max = std::max(n_max, views[i].n_dup);
     }
     if (n_max == 0) return GSR_OK;
-    const uint32_t per_block = kThreads * kRangeItems;
+    const uint32_t per_block = kThreads * (fix ? kFixItems : kRangeItems);
     if (fix)
         k_tile_ranges_views<true><<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
     else
