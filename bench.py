@@ -301,6 +301,37 @@ def frame_valu_issue(args, share, ms_per_frame):
             "source": f"profiles/{d}/pmc_summary.csv (*_views kernels)"}
 
 
+def busy_union_ms(spans):
+    """Union of [start, end) intervals in 100 MHz ticks, in ms: the time the
+    kernel was executing, launches that overlap counted once."""
+    tot, cur = 0, None
+    for a, b in sorted(spans):
+        if cur is None or a > cur[1]:
+            if cur is not None:
+                tot += cur[1] - cur[0]
+            cur = [a, b]
+        else:
+            cur[1] = max(cur[1], b)
+    if cur is not None:
+        tot += cur[1] - cur[0]
+    return tot * 1e-5
+
+
+def rocprof_busy(args):
+    """The committed rocprofv3 kernel trace's figure for the same kernel and
+    command (profiles/<LATEST>/composite_busy.json, tools/busy_union.py): the
+    union of the k_composite_views launches' intervals per 20-frame region."""
+    if args.config != "c2" or args.n or args.width or args.height or args.box != "none":
+        return None
+    try:
+        d = open(PMC_PROFILE).read().strip()
+        got = json.load(open(os.path.join(ROOT, "profiles", d, "composite_busy.json")))
+        return {"us_per_view": got["us_per_view"], "busy_us_per_region": got["busy_us_per_region_median"],
+                "regions": got["regions_of_the_bench_shape"], "source": f"profiles/{d}/composite_busy.json"}
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def _free_port():
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -609,15 +640,21 @@ def main():
         pipe.next = 0
         gp_elapsed = timed_region(lambda: pipelined(calls), 1, dev)
         tot_ms, tot_l, tot_v, tot_span = 0.0, 0, 0, 0.0
+        spans = []  # every launch's in-kernel (start, end), 100 MHz ticks, device-wide clock
         for c in leads:
             cms, cl, cv, csp = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
             _lib.check(lib.gsr_context_group_times(c.handle, ctypes.byref(cms), ctypes.byref(cl), ctypes.byref(cv),
                                                    ctypes.byref(csp)), "group_times")
             tot_ms, tot_l, tot_v, tot_span = tot_ms + cms.value, tot_l + cl.value, tot_v + cv.value, tot_span + csp.value
+            buf = (ctypes.c_uint64 * 128)()
+            got = lib.gsr_context_group_spans(c.handle, buf, 64)
+            _lib.check(0 if got >= 0 else int(got), "group_spans")
+            spans += [(buf[2 * i], buf[2 * i + 1]) for i in range(min(int(got), 64))]
             _lib.check(lib.gsr_context_set_profiling(c.handle, 0), "set_profiling")
         vstats = [c.stats() for c in ctxs]
         group_comp = dict(launches=tot_l, views=tot_v, ms_per_launch=tot_span / max(tot_l, 1),
                           event_ms_per_launch=tot_ms / max(tot_l, 1), views_per_launch=tot_v / max(tot_l, 1),
+                          busy_ms=busy_union_ms(spans), span_launches=len(spans),
                           mean_instances=float(np.mean([v["n_instances"] for v in vstats])),
                           instrumented_ms_per_frame=1e3 * gp_elapsed / timed_frames)
 
@@ -696,46 +733,60 @@ def main():
         if dom == "composite":
             roof["valu_issue"] = valu_issue(KERNEL_SYMBOL[dom], args, stage[dom])
         frame_valu = frame_valu_issue(args, share, ms_per_step)
-        if group_comp is not None and group_comp["launches"] > 0:
-            # the timed region's dominant kernel: k_composite_views<0>, one launch per
-            # group; its algorithmic bytes are the single-view formula per view
+        if group_comp is not None and group_comp["launches"] > 0 and group_comp["busy_ms"] > 0:
+            # The timed region's dominant kernel: k_composite_views<0>, one launch per group.
+            # Its time is the union of its launches' in-kernel spans over a repeat of the timed
+            # region (the four groups' launches overlap at the end of the region: a launch's own
+            # span counts waits for CUs the others hold, and their spans summed exceed the
+            # region), i.e. the time the chip was running it; per view, at most ms_per_step.
             vpl = group_comp["views_per_launch"]
-            alg_view = group_comp["mean_instances"] * (48 + 4) + ntiles * 8 + W * H * 12
-            alg_launch = alg_view * vpl
-            live_ms = group_comp["ms_per_launch"]
-            prof = rocprof_avg_ms("k_composite_views<0>", args)
-            # achieved / frac: the committed rocprofv3 average of this kernel under this same
-            # bench command (profiles/LATEST/kernel_stats.csv); the live in-kernel span of this
-            # run's launches is kept beside it as the contended figure (the region's groups
-            # composite concurrently, so each launch's span includes waits for CUs other
-            # groups' launches hold)
-            ms_launch = prof["ms"] if prof else live_ms
+            views = group_comp["views"]
+            busy_ms = group_comp["busy_ms"]
+            us_view = 1e3 * busy_ms / views
+            ms_launch = busy_ms / group_comp["launches"]
+            # SURVEY 8(d)'s algorithmic bytes: B_frame per view (every Gaussian record read once,
+            # the float32 image written once); beside it the kernel's own bytes (its instances'
+            # 48-B records + 4-B ids, tile ranges, image)
+            alg_launch = b_frame * vpl
             ach = alg_launch / (ms_launch * 1e-3) / 1e9
-            ach_live = alg_launch / (live_ms * 1e-3) / 1e9
+            alg_view_local = group_comp["mean_instances"] * (48 + 4) + ntiles * 8 + W * H * 12
+            ach_local = alg_view_local * vpl / (ms_launch * 1e-3) / 1e9
             single = {k: roof.pop(k) for k in ("kernel", "achieved", "frac", "traffic", "alg_bytes_per_launch",
                                                "ms_per_launch", "traffic_source", "valu_issue") if k in roof}
             single["kernel"] = "k_composite<0> (one view at a time, gsr_render)"
             gt = pmc_traffic("k_composite_views<0>", args)
+            prof = rocprof_avg_ms("k_composite_views<0>", args)
+            rbusy = rocprof_busy(args)
             roof.update({"kernel": "k_composite_views<0> (the timed region's compositing, one launch per group "
                                    f"of {vpl:g} views)",
+                         "basis": "SURVEY 8(d) B_frame = N*R + W*H*12 per view composited",
                          "achieved": ach, "frac": ach / HBM_PEAK_GBS, "alg_bytes_per_launch": alg_launch,
-                         "ms_per_launch": ms_launch,
-                         "ms_per_launch_source": prof["source"] + f" (average of {prof['calls']} launches)"
-                         if prof else "live in-kernel span (no committed profile for this command)",
+                         "alg_bytes_per_view": b_frame,
+                         "ms_per_launch": ms_launch, "us_per_view": us_view,
+                         "timing": f"union of the in-kernel spans (first block start to last wave end, 100 MHz "
+                                   f"s_memrealtime) of the {group_comp['span_launches']} k_composite_views launches "
+                                   f"of a repeat of the timed region ({group_comp['instrumented_ms_per_frame']:.4f} "
+                                   f"ms/frame instrumented), over its {views} views; ms_per_launch = that busy time "
+                                   f"/ launches",
+                         "cross_check": {"us_per_view_le_ms_per_step": us_view <= 1e3 * ms_per_step,
+                                         "ms_per_step_us": 1e3 * ms_per_step,
+                                         "achieved_le_peak": ach <= HBM_PEAK_GBS,
+                                         "rocprof_us_per_view": rbusy["us_per_view"] if rbusy else None,
+                                         "rocprof_source": rbusy["source"] if rbusy else None},
+                         "kernel_local": {"alg_bytes_per_launch": alg_view_local * vpl, "alg_bytes_per_view":
+                                          alg_view_local, "achieved": ach_local, "frac": ach_local / HBM_PEAK_GBS,
+                                          "basis": "the kernel's own bytes: instances x (48-B record + 4-B id) + "
+                                                   "tiles x 8 + W*H*12 per view"},
                          "views_per_launch": vpl,
-                         "us_per_view": 1e3 * ms_launch / vpl, "alg_bytes_per_view": alg_view,
                          "traffic": gt[0] if gt else None, "traffic_per_view": gt[0] / vpl if gt else None,
                          "traffic_source": gt[1] if gt else None,
-                         "rocprof": prof,
+                         "rocprof": rbusy, "rocprof_stats_avg_launch": prof,
                          "contended_span": {
-                             "ms_per_launch": live_ms, "achieved": ach_live, "frac": ach_live / HBM_PEAK_GBS,
+                             "ms_per_launch": group_comp["ms_per_launch"],
                              "event_ms_per_launch": group_comp["event_ms_per_launch"],
-                             "timing": f"in-kernel span of every k_composite_views launch (first block start to "
-                                       f"last wave end, s_memrealtime), {group_comp['launches']} launches over a "
-                                       f"repeat of the timed pipeline ({group_comp['instrumented_ms_per_frame']:.4f} "
-                                       f"ms/frame instrumented); event_ms_per_launch: HIP events around the same "
-                                       f"launches on the group's stream, which also count the dispatch's wait "
-                                       f"behind other streams"},
+                             "timing": "each launch's own in-kernel span, averaged (overlapping launches each count "
+                                       "the others' time: not the kernel's cost); event_ms_per_launch: HIP events "
+                                       "around the same launches on the group's stream"},
                          "single_view": single})
         roof["frame_valu_issue"] = frame_valu
         if frame_valu:

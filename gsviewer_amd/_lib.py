@@ -132,6 +132,7 @@ SIGNATURES = {
     "gsr_debug_stall": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "gsr_context_set_profiling": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gsr_context_stage_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+    "gsr_context_group_spans": (ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64]),
     "gsr_context_group_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                                ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]),
     # gsr_io.h
@@ -149,7 +150,7 @@ SIGNATURES = {
 
 STAGES = ["cull", "preprocess", "depth_sort", "binning", "tile_sort", "tile_ranges", "composite", "sync", "merge"]
 
-GSR_DEBUG_RECORDS, GSR_DEBUG_DEPTH_ORDER, GSR_DEBUG_TILE_RANGES, GSR_DEBUG_TILE_LIST = 0, 1, 2, 3
+GSR_DEBUG_RECORDS, GSR_DEBUG_DEPTH_ORDER, GSR_DEBUG_TILE_RANGES, GSR_DEBUG_TILE_LIST, GSR_DEBUG_SLOT_KEYS = 0, 1, 2, 3, 4
 
 ABI_VERSION = 6
 MAX_VIEWS = 8  # GSR_MAX_VIEWS (include/gsr.h)

@@ -196,6 +196,8 @@ struct BinView {
     uint32_t* tile_keys;
     uint32_t* tile_vals;
     uint32_t n_vis;
+    const uint32_t* slot_keys;  // (fused binning with keys: see bin_scatter's kKeys)
+    uint32_t* inst_keys;
 };
 struct BinViews {
     BinView v[kMaxViews];
@@ -287,7 +289,7 @@ __device__ __forceinline__ void instance_at(uint32_t idx, const uint32_t* own_o,
             const uint32_t w = tx1 - tx0 + 1u;
             const uint32_t dy = local / w;
             key = (ty0 + dy) * (uint32_t)tiles_x + tx0 + (local - dy * w);
-            val = sorted_pos ? r : sorted_ids[r];
+            val = sorted_pos || !sorted_ids ? r : sorted_ids[r];
             return;
         }
         local -= n;
@@ -305,7 +307,7 @@ __device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t* scratch) {
     return m;
 }
 
-// (sorted rect of depth-sorted splat r)
+// (sorted rect of depth-sorted splat r; sorted_ids null: slot r's)
 template <bool kPacked>
 __device__ __forceinline__ uint2 sorted_rect(const uint32_t* __restrict__ sorted_ids, const uint2* __restrict__ trect,
                                              const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis, uint32_t r,
@@ -313,6 +315,7 @@ __device__ __forceinline__ uint2 sorted_rect(const uint32_t* __restrict__ sorted
     if constexpr (kPacked) {
         return unpack_rect(rect4_sorted[r]);
     } else {
+        if (!sorted_ids) return trect[r];
         const uint2 tr = trect[sorted_ids[r]];  // (a record slot: not below n_vis with the fused cull)
         trect_sorted[r] = tr;
         return tr;
@@ -386,11 +389,11 @@ __global__ __launch_bounds__(kThreads) void k_bin_hist(const uint32_t* __restric
                            h, own);
 }
 
-// kKeys: each instance also carries its splat's depth key (sorted_keys, in
-// depth order) to inst_keys, for the coarse depth order's run repair.  The
-// window then stages each instance's depth-sorted position instead of its
-// slot, and the writes look up both (this block's 1024 splats: cache-hot):
-// staging the keys as well took 16 KB more LDS (a block fewer per CU).
+// kKeys: each instance also carries its splat's depth key (sorted_keys, by
+// sorted position: with sorted_ids null, the slot keys) to inst_keys, for the
+// per-tile depth sort.  The window then stages each instance's sorted
+// position instead of its slot, and the writes look up both (this block's
+// 1024 splats: cache-hot).
 template <bool kPacked, int kCB, bool kKeys = false>
 __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_ids,
                                             const uint2* __restrict__ trect_sorted,
@@ -427,7 +430,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
         const uint32_t r = base + k;
-        id[k] = kKeys ? r : r < n_vis ? sorted_ids[r] : 0u;  // kKeys: the sorted position
+        id[k] = kKeys || !sorted_ids ? r : r < n_vis ? sorted_ids[r] : 0u;  // kKeys: the sorted position
         if constexpr (kPacked)
             tr[k] = r < n_vis ? unpack_rect(rect4_sorted[r]) : make_uint2(0xffffu, 0u);
         else
@@ -556,7 +559,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
             tile_keys[g] = kk;
             if constexpr (kKeys) {
                 const uint32_t r = L.v2[j];
-                tile_vals[g] = sorted_ids[r];
+                tile_vals[g] = sorted_ids ? sorted_ids[r] : r;
                 inst_keys[g] = sorted_keys[r];
             } else {
                 tile_vals[g] = L.v2[j];
@@ -607,14 +610,15 @@ __global__ __launch_bounds__(kThreads) void k_bin_hist_views(BinSortViews vs, in
                            v.trect_sorted, blockIdx.x, h, own);
 }
 
-template <bool kPacked, int kCB>
+template <bool kPacked, int kCB, bool kKeys>
 __global__ __launch_bounds__(kThreads) void k_bin_scatter_views(BinSortViews vs, int tiles_x, PassArgs pa,
                                                                 uint32_t nbb) {
     __shared__ BinScatterLds<kCB> L;
     const BinView& v = vs.v[blockIdx.y];
     if (blockIdx.x * kBinBlock >= v.n_vis) return;
-    bin_scatter<kPacked, kCB>(v.sorted_ids, v.trect_sorted, v.rect4_sorted, v.n_vis, tiles_x, pa, vs.hist[blockIdx.y],
-                              vs.totals[blockIdx.y], nbb, v.tile_keys, v.tile_vals, blockIdx.x, L);
+    bin_scatter<kPacked, kCB, kKeys>(v.sorted_ids, v.trect_sorted, v.rect4_sorted, v.n_vis, tiles_x, pa,
+                                     vs.hist[blockIdx.y], vs.totals[blockIdx.y], nbb, v.tile_keys, v.tile_vals,
+                                     blockIdx.x, L, v.slot_keys, v.inst_keys);
 }
 
 // Tile ranges from the tile-sorted keys: kRangeItems consecutive instances per
@@ -624,205 +628,9 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter_views(BinSortViews vs,
 // compositors for CU slots.)
 constexpr int kRangeItems = 16;
 
-// The repair of one run of a coarse depth order, [i, i + L): instances of one
-// tile with equal coarse keys, in slot order (the stable coarse sort's).  The
-// exact order is (full key, slot); a run without a descent of the full key is
-// already in it.  Otherwise its (key, slot) pairs are copied to scratch and
-// each one is written at its rank.  One thread owns the run (the thread
-// holding its first instance), so its reads all precede its writes; other
-// threads read the run's slots only for their (tile, coarse key), which the
-// permutation leaves unchanged.  O(L^2), but L is a handful at C2.
-__device__ __noinline__ void fix_run(const uint32_t* __restrict__ keys, uint32_t n, uint32_t* vals,
-                                     const uint32_t* __restrict__ slot_keys, const uint32_t* __restrict__ inst_keys,
-                                     uint32_t* __restrict__ scratch_keys, uint32_t* __restrict__ scratch_vals,
-                                     uint32_t i, uint32_t tile, uint32_t cv, uint32_t kmin, uint32_t s0) {
-    // the depth key of list position q (inst_keys: carried by the binning and the tile sort; else gathered)
-    auto key_at = [&](uint32_t q) { return inst_keys ? inst_keys[q] : slot_keys[vals[q]]; };
-    uint32_t fprev = key_at(i);
-    uint32_t L = 1;
-    bool descent = false;
-    for (uint32_t q = i + 1; q < n; ++q) {
-        if (keys[q] != tile) break;
-        const uint32_t f = key_at(q);
-        if (((f - kmin) >> s0) != cv) break;
-        descent |= f < fprev;
-        fprev = f;
-        ++L;
-    }
-    if (!descent) return;
-    for (uint32_t r = 0; r < L; ++r) {
-        const uint32_t sl = vals[i + r];
-        scratch_vals[i + r] = sl;
-        scratch_keys[i + r] = key_at(i + r);
-    }
-    for (uint32_t r = 0; r < L; ++r) {
-        const uint32_t kr = scratch_keys[i + r], vr = scratch_vals[i + r];
-        uint32_t rank = 0;
-        for (uint32_t q = 0; q < L; ++q) {
-            const uint32_t kq = scratch_keys[i + q], vq = scratch_vals[i + q];
-            rank += (kq < kr || (kq == kr && vq < vr)) ? 1u : 0u;
-        }
-        vals[i + rank] = vr;
-    }
-}
-
-// kmin and the coarse shift of the frame's depth sort (digit_params, PassArgs::coarse)
-__device__ __forceinline__ uint32_t coarse_shift(const uint32_t* key_range, uint32_t coarse, uint32_t& kmin) {
-    kmin = ~key_range[0];
-    const uint32_t kmax = key_range[1];
-    const uint32_t B = kmax > kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
-    if (kmax < kmin) kmin = 0u;
-    return B > coarse ? B - coarse : 0u;
-}
-
-// The thread's kRangeItems instances: every run of equal (tile, coarse key)
-// that starts among them is repaired, in registers over a window of the
-// thread's items and the kFixExtra after them (all loads issued at once: a
-// chain of dependent loads per run cost ~200 us at C2).  Runs are short (C2,
-// 16 coarse bits: 41 % of the instances in runs, the longest 8; 22 bits: 1 %,
-// 4), so an odd-even transposition sort restricted to pairs inside one run,
-// as many rounds as the longest run, puts each in (full key, slot) order.  A
-// run that reaches the window's end is left to fix_run (global memory).
-constexpr int kFixExtra = 8;
-// instances per thread of the repairing kernel (GSR_FIX_ITEMS build knob): 8
-// (twice the waves of 16, the window's loads overlap more): 13.9 -> 10.8 us,
-// 12: 12.0 (profiles/r4_s32/c9)
-#ifndef GSR_FIX_ITEMS
-#define GSR_FIX_ITEMS 8
-#endif
-constexpr int kFixItems = GSR_FIX_ITEMS;
-static_assert(kFixItems % 4 == 0 && kFixItems + kFixExtra <= 32, "run masks are 32-bit");
-
-template <int kItems>
-__device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ keys, uint32_t n, const RunFix& fx,
-                                                uint32_t base, const uint32_t (&k)[kItems], uint32_t prev) {
-    constexpr int kFixWin = kItems + kFixExtra;
-    uint32_t kw[kFixWin], vw[kFixWin], fw[kFixWin];
-    // the window's slots: with carried keys only once a run needs sorting (most windows' runs are in order)
-    auto load_vals = [&]() {
-        if (base + kFixWin <= n) {
-            const uint4* pv = reinterpret_cast<const uint4*>(fx.vals + base);  // (base: a multiple of 16)
-#pragma unroll
-            for (int q = 0; q < kFixWin / 4; ++q) {
-                const uint4 v = pv[q];
-                vw[4 * q] = v.x; vw[4 * q + 1] = v.y; vw[4 * q + 2] = v.z; vw[4 * q + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < kFixWin; ++j) vw[j] = base + j < n ? fx.vals[base + j] : 0u;
-        }
-    };
-#pragma unroll
-    for (int j = 0; j < kItems; ++j) kw[j] = k[j];
-    if (base + kFixWin <= n) {
-        const uint4* pk = reinterpret_cast<const uint4*>(keys + base + kItems);
-#pragma unroll
-        for (int q = 0; q < kFixExtra / 4; ++q) {
-            const uint4 v = pk[q];
-            kw[kItems + 4 * q] = v.x; kw[kItems + 4 * q + 1] = v.y;
-            kw[kItems + 4 * q + 2] = v.z; kw[kItems + 4 * q + 3] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int j = kItems; j < kFixWin; ++j) kw[j] = base + j < n ? keys[base + j] : 0xffffffffu;
-    }
-    if (!fx.inst_keys) load_vals();  // the keys are gathered through the slots
-    uint32_t fprev;
-    if (fx.inst_keys) {  // the keys carried with the instances: coalesced, no gathers
-        if (base + kFixWin <= n) {
-            const uint4* pf = reinterpret_cast<const uint4*>(fx.inst_keys + base);
-#pragma unroll
-            for (int q = 0; q < kFixWin / 4; ++q) {
-                const uint4 v = pf[q];
-                fw[4 * q] = v.x; fw[4 * q + 1] = v.y; fw[4 * q + 2] = v.z; fw[4 * q + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < kFixWin; ++j) fw[j] = base + j < n ? fx.inst_keys[base + j] : 0u;
-        }
-        fprev = base > 0 ? fx.inst_keys[base - 1] : 0u;
-    }
-    const uint32_t vprev = base > 0 && !fx.inst_keys ? fx.vals[base - 1] : 0u;
-    uint32_t kmin;  // (the window's loads are in flight meanwhile)
-    const uint32_t s0 = coarse_shift(fx.key_range, fx.coarse, kmin);
-    if (s0 == 0u) return;  // the coarse sort was exact
-    if (!fx.inst_keys) {  // gathered by slot
-#pragma unroll
-        for (int j = 0; j < kFixWin; ++j) fw[j] = base + j < n ? fx.slot_keys[vw[j]] : 0u;
-        fprev = base > 0 ? fx.slot_keys[vprev] : 0u;
-    }
-    // same bit j: items j and j + 1 are one run (both valid, same tile and coarse key)
-    uint32_t same = 0;
-#pragma unroll
-    for (int j = 0; j + 1 < kFixWin; ++j)
-        if (base + j + 1 < n && kw[j] == kw[j + 1] && ((fw[j] - kmin) >> s0) == ((fw[j + 1] - kmin) >> s0))
-            same |= 1u << j;
-    // own bit j: item j is in a run that starts among the thread's items
-    const bool cont0 = base > 0 && prev == kw[0] && ((fprev - kmin) >> s0) == ((fw[0] - kmin) >> s0);
-    uint32_t own = cont0 ? 0u : 1u;
-#pragma unroll
-    for (int j = 1; j < kFixWin; ++j) {
-        const bool in = ((same >> (j - 1)) & 1u) ? ((own >> (j - 1)) & 1u) != 0u : j < kItems;
-        if (in) own |= 1u << j;
-    }
-    // a run that may go on past the window: fix_run from its start, out of the register sort
-    if ((own >> (kFixWin - 1)) & 1u) {
-        int st = kFixWin - 1;
-#pragma unroll
-        for (int j = kFixWin - 2; j >= 0; --j)
-            if (st == j + 1 && ((same >> j) & 1u)) st = j;
-        own &= (1u << st) - 1u;
-        uint32_t kst = 0, fst = 0;  // items st (selected: a dynamic index would put the arrays in scratch)
-#pragma unroll
-        for (int j = 0; j < kFixWin; ++j)
-            if (j == st) kst = kw[j], fst = fw[j];
-        fix_run(keys, n, fx.vals, fx.slot_keys, fx.inst_keys, fx.scratch_keys, fx.scratch_vals, base + (uint32_t)st, kst,
-                (fst - kmin) >> s0, kmin, s0);
-    }
-    const uint32_t pairs = same & own;  // adjacent pairs inside one owned run
-    uint32_t descent = 0;
-#pragma unroll
-    for (int j = 0; j + 1 < kFixWin; ++j)
-        if (((pairs >> j) & 1u) && fw[j] > fw[j + 1]) descent = 1u;  // slots ascend in a run: only keys descend
-#ifdef GSR_EXP_FIX_NOSORT  // experiment build: the window's loads and tests only (timing; lists unrepaired)
-    asm volatile("" ::"v"(descent));
-    return;
-#endif
-    if (!descent) return;
-    if (fx.inst_keys) load_vals();
-    // the longest owned run: rounds of the transposition sort
-    uint32_t len = 1, rounds = 1;
-#pragma unroll
-    for (int j = 0; j + 1 < kFixWin; ++j) {
-        len = ((pairs >> j) & 1u) ? len + 1u : 1u;
-        rounds = max(rounds, len);
-    }
-    uint32_t v0[kFixWin];
-#pragma unroll
-    for (int j = 0; j < kFixWin; ++j) v0[j] = vw[j];
-    for (uint32_t r = 0; r < rounds; ++r) {
-#pragma unroll
-        for (int j = 0; j + 1 < kFixWin; ++j) {
-            if ((j & 1) != (int)(r & 1u) || !((pairs >> j) & 1u)) continue;
-            const bool gt = fw[j] > fw[j + 1] || (fw[j] == fw[j + 1] && vw[j] > vw[j + 1]);
-            const uint32_t fa = fw[j], va = vw[j];
-            fw[j] = gt ? fw[j + 1] : fa;
-            vw[j] = gt ? vw[j + 1] : va;
-            fw[j + 1] = gt ? fa : fw[j + 1];
-            vw[j + 1] = gt ? va : vw[j + 1];
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < kFixWin; ++j)
-        if (((own >> j) & 1u) && vw[j] != v0[j]) fx.vals[base + j] = vw[j];
-}
-
-// kFix: the coarse depth order's run repair (a separate instantiation: its
-// registers (153 VGPRs) made the plain kernel wait for room beside the
-// compositors in flight)
-template <bool kFix, int kItems = kFix ? kFixItems : kRangeItems>
+template <int kItems = kRangeItems>
 __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, uint32_t n, uint2* __restrict__ ranges,
-                                            uint32_t t, const RunFix& fx) {
+                                            uint32_t t) {
     const uint32_t base = t * kItems;
     if (base >= n) return;
     uint32_t k[kItems];
@@ -839,8 +647,6 @@ __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, u
     }
     const uint32_t prev = base > 0 ? keys[base - 1] : 0xffffffffu;
     const uint32_t next = base + kItems < n ? keys[base + kItems] : 0xffffffffu;
-    // the run repair first: its window loads are issued before the range stores
-    if constexpr (kFix) fix_coarse_runs<kItems>(keys, n, fx, base, k, prev);
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
         const uint32_t i = base + j;
@@ -852,23 +658,20 @@ __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, u
     }
 }
 
-template <bool kFix>
 __global__ __launch_bounds__(kThreads) void k_tile_ranges(const uint32_t* __restrict__ keys, uint32_t n,
-                                                          uint2* __restrict__ ranges, RunFix fx) {
-    tile_ranges<kFix>(keys, n, ranges, blockIdx.x * kThreads + threadIdx.x, fx);
+                                                          uint2* __restrict__ ranges) {
+    tile_ranges(keys, n, ranges, blockIdx.x * kThreads + threadIdx.x);
 }
 
 struct RangeViews {
     const uint32_t* keys[kMaxViews];
     uint2* ranges[kMaxViews];
     uint32_t n[kMaxViews];
-    RunFix fix[kMaxViews];
 };
 
-template <bool kFix>
 __global__ __launch_bounds__(kThreads) void k_tile_ranges_views(RangeViews vs) {
     const int v = blockIdx.y;
-    tile_ranges<kFix>(vs.keys[v], vs.n[v], vs.ranges[v], blockIdx.x * kThreads + threadIdx.x, vs.fix[v]);
+    tile_ranges(vs.keys[v], vs.n[v], vs.ranges[v], blockIdx.x * kThreads + threadIdx.x);
 }
 
 struct CompositeArgs {
@@ -963,6 +766,13 @@ __device__ __forceinline__ uint32_t first_class_of(uint2 r, uint32_t chunk, uint
     return first_major && (r.y - r.x) >= chunk ? 0u : partial_class_of(r, chunk, classes);
 }
 
+// Rows of the per-block totals (tot[row * blocks + block]): 0 the extra
+// chunks, 1 the full chunks, 1 + k (k < classes) the partial chunks of length
+// class k, then the per-tile depth sort's tiles of class c (tds_class_of) at
+// row 1 + classes + c.
+__device__ __forceinline__ uint32_t tds_row(uint32_t classes, uint32_t c) { return 1u + classes + c; }
+constexpr int kChunkRows = 1 + kMaxLenClasses + kTdsClasses;
+
 __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
                                             uint32_t classes, bool first_major, uint32_t* __restrict__ tot,
                                             uint32_t (*lds)[kThreads / 64]) {
@@ -972,6 +782,7 @@ __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, in
     const uint32_t e = wave_reduce_sum(valid ? chunks_of(r, chunk) - 1u : 0u);
     const uint32_t f = wave_reduce_sum(first_full_of(r, chunk, first_major));
     const uint32_t pc = valid ? first_class_of(r, chunk, classes, first_major) : 0u;
+    const uint32_t tc = tds_class_of(r.y - r.x);
     const int w = threadIdx.x >> 6;
     if (__lane_id() == 0) {
         lds[0][w] = e;
@@ -981,8 +792,12 @@ __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, in
         const uint32_t n = (uint32_t)__popcll(__ballot(pc == k));
         if (__lane_id() == 0) lds[1 + k][w] = n;
     }
+    for (uint32_t c = 0; c < (uint32_t)kTdsClasses; ++c) {
+        const uint32_t n = (uint32_t)__popcll(__ballot(tc == c));
+        if (__lane_id() == 0) lds[tds_row(classes, c)][w] = n;
+    }
     __syncthreads();
-    if (threadIdx.x <= classes)
+    if (threadIdx.x < tds_row(classes, kTdsClasses))
         tot[threadIdx.x * gridDim.x + blockIdx.x] =
             lds[threadIdx.x][0] + lds[threadIdx.x][1] + lds[threadIdx.x][2] + lds[threadIdx.x][3];
 }
@@ -990,7 +805,7 @@ __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, in
 __global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restrict__ ranges, int num_tiles,
                                                           uint32_t chunk, uint32_t classes,
                                                           uint32_t* __restrict__ tot, uint32_t first_major) {
-    __shared__ uint32_t lds[1 + kMaxLenClasses][kThreads / 64];
+    __shared__ uint32_t lds[kChunkRows][kThreads / 64];
     chunk_count(ranges, num_tiles, chunk, classes, first_major != 0, tot, lds);
 }
 
@@ -999,6 +814,8 @@ struct ChunkWriteLds {
     uint32_t cls[kMaxLenClasses][kThreads / 64];  // partials of class k per wave
     uint32_t pre[1 + kMaxLenClasses];             // sums over the earlier blocks
     uint32_t base[kMaxLenClasses];                // first dispatch position of each class
+    uint32_t tcls[kTdsClasses][kThreads / 64];    // per-tile depth sort: tiles of class c per wave
+    uint32_t tpos[kTdsClasses];                   // ... the block's first work-list position of class c
 };
 
 __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
@@ -1006,11 +823,39 @@ __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, in
                                             uint32_t* __restrict__ chunk_cnt, uint32_t* __restrict__ chunk_base,
                                             uint32_t* __restrict__ n_extra_dev, uint4* __restrict__ desc,
                                             uint32_t* __restrict__ order, float4* __restrict__ tmax,
-                                            ChunkWriteLds& sh) {
+                                            uint32_t* __restrict__ tds_list, ChunkWriteLds& sh) {
     const int t = blockIdx.x * kThreads + threadIdx.x;
     const int w = threadIdx.x >> 6;
+    uint32_t* cls_tot = const_cast<uint32_t*>(tot) + tds_row(classes, kTdsClasses) * gridDim.x;
+    if (tds_list && w == 1) {  // wave 1: the depth sort's work list positions of this block's classes
+        uint32_t ps[kTdsClasses], as[kTdsClasses];
+#pragma unroll
+        for (int c = 0; c < kTdsClasses; ++c) ps[c] = as[c] = 0u;
+        for (uint32_t b = __lane_id(); b < gridDim.x; b += 64) {
+            uint32_t v[kTdsClasses];
+#pragma unroll
+            for (int c = 0; c < kTdsClasses; ++c) v[c] = tot[tds_row(classes, c) * gridDim.x + b];
+#pragma unroll
+            for (int c = 0; c < kTdsClasses; ++c) {
+                ps[c] += b < blockIdx.x ? v[c] : 0u;
+                as[c] += v[c];
+            }
+        }
+        uint32_t run = 0, n_wg = 0;
+#pragma unroll
+        for (int c = 0; c < kTdsClasses; ++c) {
+            const uint32_t p = wave_reduce_sum(ps[c]);
+            const uint32_t a = wave_reduce_sum(as[c]);
+            if (__lane_id() == 0) sh.tpos[c] = run + p;
+            run += a;
+            if (c + 1 == kTdsBlockClasses) n_wg = run;
+        }
+        if (blockIdx.x == 0 && __lane_id() == 0) {  // (tds_counts)
+            cls_tot[classes + 1] = n_wg;
+            cls_tot[classes + 2] = run - n_wg;
+        }
+    }
     if (w == 0) {  // wave 0: offsets of this block = sums of the earlier blocks' totals
-        uint32_t* cls_tot = const_cast<uint32_t*>(tot) + (1 + classes) * gridDim.x;
         // every row's loads issued before any is summed: one memory round trip,
         // not one per class (a row-by-row loop waited 1 + classes times)
         uint32_t ps[1 + kMaxLenClasses], as[1 + kMaxLenClasses];
@@ -1055,9 +900,23 @@ __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, in
         if (pc == k) rank = (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
         if (__lane_id() == 0) sh.cls[k][w] = (uint32_t)__popcll(m);
     }
+    const uint32_t tc = tds_class_of(r.y - r.x);
+    uint32_t trank = 0;  // among this wave's tiles of depth-sort class tc
+    if (tds_list) {
+        for (uint32_t c = 0; c < (uint32_t)kTdsClasses; ++c) {
+            const uint64_t m = __ballot(tc == c);
+            if (tc == c) trank = (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
+            if (__lane_id() == 0) sh.tcls[c][w] = (uint32_t)__popcll(m);
+        }
+    }
     const uint32_t mine = valid ? cnt - 1u : 0u;
     uint32_t total, total_f;
     const uint32_t excl = block_exclusive<kThreads>(mine, sh.scan[0], total);  // (its barrier also publishes sh)
+    if (tds_list && tc < (uint32_t)kTdsClasses) {
+        uint32_t pos = sh.tpos[tc] + trank;
+        for (int i = 0; i < w; ++i) pos += sh.tcls[tc][i];
+        tds_list[pos] = (uint32_t)t;
+    }
     const uint32_t excl_f = block_exclusive<kThreads>(full, sh.scan[1], total_f);
     const uint32_t extra = sh.pre[0] + excl;
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_extra_dev = sh.pre[0] + total;
@@ -1109,10 +968,11 @@ __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restric
                                                           uint32_t* __restrict__ chunk_base,
                                                           uint32_t* __restrict__ n_extra_dev,
                                                           uint4* __restrict__ desc, uint32_t* __restrict__ order,
-                                                          float4* __restrict__ tmax, uint32_t first_major) {
+                                                          float4* __restrict__ tmax, uint32_t first_major,
+                                                          uint32_t* __restrict__ tds_list) {
     __shared__ ChunkWriteLds sh;
     chunk_write(ranges, num_tiles, chunk, classes, first_major != 0, tot, chunk_cnt, chunk_base, n_extra_dev, desc,
-                order, tmax, sh);
+                order, tmax, tds_list, sh);
 }
 
 struct ChunkView {
@@ -1123,6 +983,7 @@ struct ChunkView {
     uint4* desc;
     uint32_t* order;
     float4* tmax;
+    uint32_t* tds_list;
 };
 struct ChunkViews {
     ChunkView v[kMaxViews];
@@ -1130,7 +991,7 @@ struct ChunkViews {
 
 __global__ __launch_bounds__(kThreads) void k_chunk_count_views(ChunkViews vs, int num_tiles, uint32_t chunk,
                                                                 uint32_t classes, uint32_t first_major) {
-    __shared__ uint32_t lds[1 + kMaxLenClasses][kThreads / 64];
+    __shared__ uint32_t lds[kChunkRows][kThreads / 64];
     const ChunkView& v = vs.v[blockIdx.y];
     chunk_count(v.ranges, num_tiles, chunk, classes, first_major != 0, v.chunk_cnt + num_tiles, lds);
 }
@@ -1140,7 +1001,7 @@ __global__ __launch_bounds__(kThreads) void k_chunk_write_views(ChunkViews vs, i
     __shared__ ChunkWriteLds sh;
     const ChunkView& v = vs.v[blockIdx.y];
     chunk_write(v.ranges, num_tiles, chunk, classes, first_major != 0, v.chunk_cnt + num_tiles, v.chunk_cnt,
-                v.chunk_base, v.n_extra_dev, v.desc, v.order, v.tmax, sh);
+                v.chunk_base, v.n_extra_dev, v.desc, v.order, v.tmax, v.tds_list, sh);
 }
 
 // Bits [lo, hi] of a 16-bit mask, clamped to [0, 15]; 0 if the range is empty.
@@ -1992,7 +1853,9 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_views(MergeViews vs, Co
 // it on the reference's own shaders (tests/golden/llvmpipe_golden.npz,
 // oracle/gl_oracle.py blend8): colour and alpha to unorm8 by
 // rint(fl32(v * 255/256) * 256), then dst = min(255, mul8(c, a) +
-// mul8(dst, 255 - a)) with the exactly rounded mul8(x, y) = x y / 255.  The
+// mul8(dst, 255 - a)) with llvmpipe's approximation of x y / 255,
+// mul8(x, y) = (t + (t >> 8) + 128) >> 8, t = x y (lp_build_mul_norm; it
+// differs from round(x y / 255) on 24 of the 65536 pairs).  The
 // falloff is the record's log2-scaled quadratic, so alpha can differ from the
 // oracle's expf(power) by an ulp, which moves it across an 8-bit rounding
 // boundary rarely.
@@ -2175,58 +2038,73 @@ size_t bin_hist_elems(size_t n_vis, int tbits, int passes) {
     return ((n_vis + kBinBlock - 1) / kBinBlock) * ((size_t)1 << ((tbits + passes - 1) / passes));
 }
 
-int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted,
-                          uint32_t n_vis, int tiles_x, int tbits, int passes, uint32_t* hist, uint32_t* totals,
-                          uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s,
-                          const uint32_t* sorted_keys, uint32_t* inst_keys) {
-    if (n_vis == 0) return GSR_OK;
-    const int tb = tbits > 0 ? tbits : 1;  // one tile: a single digit value, generation order kept
-    const int ps = passes > 0 ? passes : 1;
-    const int w = (tb + ps - 1) / ps;
+// The binning's digit parameters (tile sort pass 0) and its blocks.
+static int bin_pass0(const BinSortArgs& a, PassArgs& pa, int& w, bool scatter) {
+    const int tb = a.tbits > 0 ? a.tbits : 1;  // one tile: a single digit value, generation order kept
+    const int ps = a.passes > 0 ? a.passes : 1;
+    w = (tb + ps - 1) / ps;
     if (w > 11) return set_error(GSR_ERR_INVALID, "binning: tile digit wider than 11 bits");
-    const uint32_t nbb = (n_vis + kBinBlock - 1) / kBinBlock;
-    const PassArgs pa{nullptr, (uint32_t)tb, (uint32_t)ps, 0u};
-    const bool packed = rect4_sorted != nullptr;
-#define GSR_BIN_HIST(P, CB)                                                                                 \
-    k_bin_hist<P, CB><<<nbb, kThreads, 0, s>>>(sorted_ids, trect, rect4_sorted, n_vis, tiles_x, pa, hist, nbb, \
-                                               trect_sorted)
-#define GSR_BIN_SCATTER(P, CB)                                                                                  \
-    do {                                                                                                        \
-        if (inst_keys)                                                                                          \
-            k_bin_scatter<P, CB, true><<<nbb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis,     \
-                                                                tiles_x, pa, hist, totals, nbb, tile_keys,         \
-                                                                tile_vals, sorted_keys, inst_keys);                \
-        else                                                                                                    \
-            k_bin_scatter<P, CB, false><<<nbb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis,    \
-                                                                 tiles_x, pa, hist, totals, nbb, tile_keys,        \
-                                                                 tile_vals, nullptr, nullptr);                     \
-    } while (0)
+    if (!a.sorted_ids && (a.rect4_sorted || (scatter && (!a.slot_keys || !a.inst_keys))))
+        return set_error(GSR_ERR_INVALID, "binning: slot order takes the plain rects and carries the keys");
+    pa = PassArgs{nullptr, (uint32_t)tb, (uint32_t)ps, 0u};
+    return GSR_OK;
+}
+
+int launch_binning_hist(const BinSortArgs& a, hipStream_t s) {
+    if (a.n_vis == 0) return GSR_OK;
+    PassArgs pa;
+    int w, rc;
+    if ((rc = bin_pass0(a, pa, w, false))) return rc;
+    const uint32_t nbb = (a.n_vis + kBinBlock - 1) / kBinBlock;
+    const bool packed = a.rect4_sorted != nullptr;
+    // slot order: the rects are read where they lie (trect_sorted aliases trect, nothing is written to it)
+    uint2* tsorted = a.sorted_ids ? a.trect_sorted : const_cast<uint2*>(a.trect);
+#define GSR_BIN_HIST(P, CB)                                                                                  \
+    k_bin_hist<P, CB><<<nbb, kThreads, 0, s>>>(a.sorted_ids, a.trect, a.rect4_sorted, a.n_vis, a.tiles_x, pa, \
+                                               a.hist, nbb, tsorted)
     if (w <= 8) {
         if (packed) GSR_BIN_HIST(true, 8); else GSR_BIN_HIST(false, 8);
     } else {
         if (packed) GSR_BIN_HIST(true, 11); else GSR_BIN_HIST(false, 11);
     }
+#undef GSR_BIN_HIST
     GSR_LAUNCH_CHECK("bin_hist");
-    int rc;
-    if ((rc = radix_offsets(hist, nbb, tb, ps, 0, totals, s))) return rc;
+    return radix_offsets(a.hist, nbb, (int)pa.bits, (int)pa.passes, 0, a.totals, s);
+}
+
+int launch_binning_scatter(const BinSortArgs& a, hipStream_t s) {
+    if (a.n_vis == 0) return GSR_OK;
+    PassArgs pa;
+    int w, rc;
+    if ((rc = bin_pass0(a, pa, w, true))) return rc;
+    const uint32_t nbb = (a.n_vis + kBinBlock - 1) / kBinBlock;
+    const bool packed = a.rect4_sorted != nullptr;
+    const uint2* tsorted = a.sorted_ids ? a.trect_sorted : a.trect;
+#define GSR_BIN_SCATTER(P, CB)                                                                                      \
+    do {                                                                                                            \
+        if (a.inst_keys)                                                                                            \
+            k_bin_scatter<P, CB, true><<<nbb, kThreads, 0, s>>>(a.sorted_ids, tsorted, a.rect4_sorted, a.n_vis,     \
+                                                                a.tiles_x, pa, a.hist, a.totals, nbb, a.tile_keys,  \
+                                                                a.tile_vals, a.slot_keys, a.inst_keys);             \
+        else                                                                                                        \
+            k_bin_scatter<P, CB, false><<<nbb, kThreads, 0, s>>>(a.sorted_ids, tsorted, a.rect4_sorted, a.n_vis,    \
+                                                                 a.tiles_x, pa, a.hist, a.totals, nbb, a.tile_keys, \
+                                                                 a.tile_vals, nullptr, nullptr);                    \
+    } while (0)
     if (w <= 8) {
         if (packed) GSR_BIN_SCATTER(true, 8); else GSR_BIN_SCATTER(false, 8);
     } else {
         if (packed) GSR_BIN_SCATTER(true, 11); else GSR_BIN_SCATTER(false, 11);
     }
-    GSR_LAUNCH_CHECK("bin_scatter");
-#undef GSR_BIN_HIST
 #undef GSR_BIN_SCATTER
+    GSR_LAUNCH_CHECK("bin_scatter");
     return GSR_OK;
 }
 
-int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, const RunFix& fix, hipStream_t s) {
+int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, hipStream_t s) {
     if (n_dup == 0) return GSR_OK;
-    const uint32_t per_block = kThreads * (fix.coarse ? kFixItems : kRangeItems);
-    if (fix.coarse)
-        k_tile_ranges<true><<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, fix);
-    else
-        k_tile_ranges<false><<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, fix);
+    const uint32_t per_block = kThreads * kRangeItems;
+    k_tile_ranges<<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges);
     GSR_LAUNCH_CHECK("tile_ranges");
     return GSR_OK;
 }
@@ -2258,17 +2136,22 @@ static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float*
 }
 
 size_t chunk_cnt_elems(int num_tiles) {
-    return (size_t)num_tiles + (1 + kMaxLenClasses) * ((size_t)num_tiles / kThreads + 1) + kMaxLenClasses + 1;
+    return (size_t)num_tiles + kChunkRows * ((size_t)num_tiles / kThreads + 1) + kMaxLenClasses + 3;
 }
 
+// after the block totals: the chunks per class (classes + 1 words), then the depth sort's two counts
 const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes) {
     const size_t g = ((size_t)num_tiles + kThreads - 1) / kThreads;
-    return chunk_cnt + num_tiles + (1 + classes) * g;
+    return chunk_cnt + num_tiles + (1 + classes + kTdsClasses) * g;
+}
+
+const uint32_t* tds_counts(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes) {
+    return chunk_class_totals(chunk_cnt, num_tiles, classes) + classes + 1;
 }
 
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
-                  hipStream_t s, bool first_major) {
+                  hipStream_t s, bool first_major, uint32_t* tds_list) {
 #ifndef GSR_COMP_BOUND
     tmax = nullptr;  // the published maxima are only read by the bound variant
 #endif
@@ -2279,7 +2162,7 @@ int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t c
     k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot, first_major ? 1u : 0u);
     GSR_LAUNCH_CHECK("chunk_count");
     k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot, chunk_cnt, chunk_base, n_extra_dev,
-                                         desc, order, tmax, first_major ? 1u : 0u);
+                                         desc, order, tmax, first_major ? 1u : 0u, tds_list);
     GSR_LAUNCH_CHECK("chunk_write");
     return GSR_OK;
 }
@@ -2373,26 +2256,42 @@ int launch_binning_views(FinishView* views, int k, int tiles_x, uint32_t stage_l
     return GSR_OK;
 }
 
-int launch_binning_sorted_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
-                                int tbits, int passes, hipStream_t s) {
-    BinSortViews bv{};
-    uint32_t nbb = 0;
+// A group's fused binning (views of one frame size), in the same two halves.
+static int bin_views_args(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tbits,
+                          int passes, BinSortViews& bv, uint32_t& nbb, PassArgs& pa, int& w, bool scatter) {
+    bv = BinSortViews{};
+    nbb = 0;
     for (int i = 0; i < k; ++i) {
         const FinishView& f = views[i];
-        bv.v[i] = BinView{f.sorted_ids, f.trect, f.rect4_sorted, f.trect_sorted, f.bin_tmp, f.tile_keys, f.tile_vals,
-                          f.n_vis};
+        // slot order: the rects are read where they lie
+        uint2* tsorted = f.sorted_ids ? f.trect_sorted : const_cast<uint2*>(f.trect);
+        bv.v[i] = BinView{f.sorted_ids, f.trect, f.rect4_sorted, tsorted, f.bin_tmp, f.tile_keys, f.tile_vals,
+                          f.n_vis, f.slot_keys, f.inst_keys};
         bv.hist[i] = hist[i];
         bv.totals[i] = totals[i];
-        if ((f.rect4_sorted != nullptr) != (views[0].rect4_sorted != nullptr))
-            return set_error(GSR_ERR_INVALID, "binning: packed rectangles on some views only");
+        if ((f.rect4_sorted != nullptr) != (views[0].rect4_sorted != nullptr) ||
+            (scatter && (f.inst_keys != nullptr) != (views[0].inst_keys != nullptr)))
+            return set_error(GSR_ERR_INVALID, "binning: packed rectangles or carried keys on some views only");
+        if (!f.sorted_ids && (f.rect4_sorted || (scatter && (!f.slot_keys || !f.inst_keys))))
+            return set_error(GSR_ERR_INVALID, "binning: slot order takes the plain rects and carries the keys");
         nbb = std::max(nbb, (f.n_vis + kBinBlock - 1) / kBinBlock);
     }
-    if (nbb == 0) return GSR_OK;
     const int tb = tbits > 0 ? tbits : 1;
     const int ps = passes > 0 ? passes : 1;
-    const int w = (tb + ps - 1) / ps;
+    w = (tb + ps - 1) / ps;
     if (w > 11) return set_error(GSR_ERR_INVALID, "binning: tile digit wider than 11 bits");
-    const PassArgs pa{nullptr, (uint32_t)tb, (uint32_t)ps, 0u};
+    pa = PassArgs{nullptr, (uint32_t)tb, (uint32_t)ps, 0u};
+    return GSR_OK;
+}
+
+int launch_binning_hist_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
+                              int tbits, int passes, hipStream_t s) {
+    BinSortViews bv;
+    uint32_t nbb;
+    PassArgs pa;
+    int w, rc;
+    if ((rc = bin_views_args(views, hist, totals, k, tbits, passes, bv, nbb, pa, w, false))) return rc;
+    if (nbb == 0) return GSR_OK;
     const bool packed = views[0].rect4_sorted != nullptr;
     const dim3 grid(nbb, (unsigned)k);
     if (w <= 8) {
@@ -2403,15 +2302,31 @@ int launch_binning_sorted_views(FinishView* views, uint32_t* const* hist, uint32
         else k_bin_hist_views<false, 11><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
     }
     GSR_LAUNCH_CHECK("bin_hist_views");
-    int rc;
-    if ((rc = radix_offsets_views(hist, totals, k, nbb, tb, ps, 0, s))) return rc;
+    return radix_offsets_views(hist, totals, k, nbb, (int)pa.bits, (int)pa.passes, 0, s);
+}
+
+int launch_binning_scatter_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k,
+                                 int tiles_x, int tbits, int passes, hipStream_t s) {
+    BinSortViews bv;
+    uint32_t nbb;
+    PassArgs pa;
+    int w, rc;
+    if ((rc = bin_views_args(views, hist, totals, k, tbits, passes, bv, nbb, pa, w, true))) return rc;
+    if (nbb == 0) return GSR_OK;
+    const bool packed = views[0].rect4_sorted != nullptr;
+    const bool keys = views[0].inst_keys != nullptr;
+    const dim3 grid(nbb, (unsigned)k);
+#define GSR_BIN_SCATTER_V(P, CB)                                                                   \
+    do {                                                                                           \
+        if (keys) k_bin_scatter_views<P, CB, true><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);  \
+        else k_bin_scatter_views<P, CB, false><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);      \
+    } while (0)
     if (w <= 8) {
-        if (packed) k_bin_scatter_views<true, 8><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
-        else k_bin_scatter_views<false, 8><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+        if (packed) GSR_BIN_SCATTER_V(true, 8); else GSR_BIN_SCATTER_V(false, 8);
     } else {
-        if (packed) k_bin_scatter_views<true, 11><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
-        else k_bin_scatter_views<false, 11><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+        if (packed) GSR_BIN_SCATTER_V(true, 11); else GSR_BIN_SCATTER_V(false, 11);
     }
+#undef GSR_BIN_SCATTER_V
     GSR_LAUNCH_CHECK("bin_scatter_views");
     return GSR_OK;
 }
@@ -2419,21 +2334,15 @@ int launch_binning_sorted_views(FinishView* views, uint32_t* const* hist, uint32
 int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s) {
     RangeViews rv{};
     uint32_t n_max = 0;
-    bool fix = false;
     for (int i = 0; i < k; ++i) {
         rv.keys[i] = views[i].tile_keys;
         rv.ranges[i] = views[i].ranges;
         rv.n[i] = views[i].n_dup;
-        rv.fix[i] = views[i].fix;
-        fix |= views[i].fix.coarse != 0;
         n_max = std::max(n_max, views[i].n_dup);
     }
     if (n_max == 0) return GSR_OK;
-    const uint32_t per_block = kThreads * (fix ? kFixItems : kRangeItems);
-    if (fix)
-        k_tile_ranges_views<true><<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
-    else
-        k_tile_ranges_views<false><<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
+    const uint32_t per_block = kThreads * kRangeItems;
+    k_tile_ranges_views<<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
     GSR_LAUNCH_CHECK("tile_ranges_views");
     return GSR_OK;
 }
@@ -2449,7 +2358,7 @@ int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk,
 #else
         float4* tmax = nullptr;  // the published maxima are only read by the bound variant
 #endif
-        cv.v[i] = ChunkView{f.ranges, f.chunk_cnt, f.chunk_base, f.n_extra_dev, f.desc, f.order, tmax};
+        cv.v[i] = ChunkView{f.ranges, f.chunk_cnt, f.chunk_base, f.n_extra_dev, f.desc, f.order, tmax, f.tds_list};
     }
     const dim3 grid((unsigned)((num_tiles + kThreads - 1) / kThreads), (unsigned)k);
     k_chunk_count_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk, classes, first_major ? 1u : 0u);

@@ -197,11 +197,6 @@ struct PassArgs {
     // keys are read (not the device count) and keys outside {kmin, kmax}
     // (culled slots, key 0xffffffff) are dropped; later passes see only V
     uint32_t drop = 0;
-    // Coarse depth order (the frame's depth sort): only the top `coarse` bits
-    // of the B-bit key range are sorted (0: all B).  Equal coarse keys keep
-    // their input (slot) order; tile_ranges restores the exact order inside
-    // each tile's list (RunFix).
-    uint32_t coarse = 0;
 };
 
 struct Digit {
@@ -213,7 +208,7 @@ struct Digit {
 
 __device__ __forceinline__ Digit digit_params(const PassArgs& p) {
     Digit d;
-    uint32_t B, s0 = 0;
+    uint32_t B;
     if (p.key_range) {
         d.kmin = ~p.key_range[0];
         const uint32_t kmax = p.key_range[1];
@@ -221,17 +216,13 @@ __device__ __forceinline__ Digit digit_params(const PassArgs& p) {
         // an empty range ({0, 0}: nothing visible) keeps no key: every slot is then culled (0xffffffff)
         d.lim = kmax >= d.kmin ? kmax - d.kmin : 0xfffffffeu;
         if (kmax < d.kmin) d.kmin = 0u;
-        if (p.coarse && B > p.coarse) {
-            s0 = B - p.coarse;
-            B = p.coarse;
-        }
     } else {
         d.kmin = 0u;
         d.lim = 0xffffffffu;
         B = p.bits;
     }
     d.w = max(1u, (B + p.passes - 1u) / p.passes);
-    d.shift = s0 + p.pass * d.w;
+    d.shift = p.pass * d.w;
     d.mask = (1u << d.w) - 1u;
     return d;
 }
@@ -292,8 +283,6 @@ struct RadixViewArgs {
     uint32_t** pay_io = nullptr;
     uint32_t** pay_alt = nullptr;
     bool drop_first = false;  // see radix_sort_pairs
-    uint32_t coarse = 0;      // see PassArgs::coarse
-    bool keys_last = true;    // the last pass writes the sorted keys (else keys_io keeps its input)
 };
 int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
                            hipStream_t s, int first_pass = 0);
@@ -313,13 +302,14 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
                      int bits, int passes, const uint32_t* key_range, uint32_t* tmp,
                      uint32_t* totals, hipStream_t s, const uint2* rect_in = nullptr,
                      uint32_t** pay_io = nullptr, uint32_t** pay_alt = nullptr, int first_pass = 0,
-                     bool drop_first = false, uint32_t coarse = 0, bool keys_last = true);
+                     bool drop_first = false);
 // drop_first (needs key_range): the keys are the fused cull's n slots; the
 // first pass reads all n and drops the culled ones (PassArgs::drop), later
 // passes run over the device count n_dev = V.
-// Payload (rect_in non-null): the tile rectangles rect_in[n] (uint2, in the
-// input order) travel with the pairs packed to 32 bits (pack_rect: frames of
-// at most 256 x 256 tiles); the sorted packed rectangles end in *pay_io.
+// Payload (pay_io non-null): a 32-bit word travels with each pair, read from
+// *pay_io (or, with rect_in non-null, the first pass packs the tile rectangles
+// rect_in[n] (uint2, in the input order) to 32 bits: pack_rect, frames of at
+// most 256 x 256 tiles); the sorted payload ends in *pay_io.
 constexpr int kPackedRectTiles = 256;
 
 // scene.hip
@@ -422,41 +412,82 @@ uint32_t clamp_stage_limit(long v);
 int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted, uint32_t n_vis,
                    int tiles_x, uint32_t* tmp, uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals,
                    uint32_t stage_limit, hipStream_t s);
-// Repair of a coarse depth order inside the tile lists (k_tile_ranges): runs of
-// one tile's instances with equal coarse depth keys are put in (full key, slot)
-// order, in place.  coarse == 0 (an exact depth sort): nothing to repair.
-struct RunFix {
-    uint32_t* vals;             // the tile list (slots), repaired in place
-    const uint32_t* slot_keys;  // the full depth key of every slot
-    const uint32_t* key_range;  // the frame's {~kmin, kmax}
-    uint32_t coarse;
-    uint32_t* scratch_keys;     // n_dup words each, free at this point (the tile sort's alternates)
-    uint32_t* scratch_vals;
-    const uint32_t* inst_keys = nullptr;  // each list position's depth key (binning + tile sort payload), else
-                                          // gathered through slot_keys
-};
-int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, const RunFix& fix,
-                       hipStream_t s);
+int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, hipStream_t s);
 // The binning with the tile sort's first radix pass fused in (composite.hip,
 // k_bin_hist / k_bin_scatter): the instances end in (tile_keys, tile_vals)
 // ordered by digit 0 of the tile sort (tbits bits in `passes` passes); the
 // sort then continues from pass 1 (radix_sort_pairs first_pass = 1).  hist
 // holds bin_hist_elems(n_vis, tbits, passes) uint32, totals
 // radix_totals_elems().  tbits = 0 (one tile): generation order.
+// sorted_ids null: the splats in slot order (the per-tile depth sort's
+// binning: slot r is splat r, its rect trect[r]; trect_sorted unused); then
+// slot_keys (the preprocess's depth key per slot) ride along to inst_keys.
+// In two halves: the counts and their offsets (launch_binning_hist, which needs
+// no instance buffer), then the scatter (launch_binning_scatter).
 size_t bin_hist_elems(size_t n_vis, int tbits, int passes);
-int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted,
-                          uint32_t n_vis, int tiles_x, int tbits, int passes, uint32_t* hist, uint32_t* totals,
-                          uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s,
-                          const uint32_t* sorted_keys = nullptr, uint32_t* inst_keys = nullptr);
+struct BinSortArgs {
+    const uint32_t* sorted_ids;  // null: slot order
+    const uint2* trect;
+    const uint32_t* rect4_sorted;
+    uint32_t n_vis;
+    int tiles_x, tbits, passes;
+    uint32_t* hist;
+    uint32_t* totals;
+    uint2* trect_sorted;
+    uint32_t* tile_keys;
+    uint32_t* tile_vals;
+    const uint32_t* slot_keys = nullptr;
+    uint32_t* inst_keys = nullptr;
+};
+int launch_binning_hist(const BinSortArgs& a, hipStream_t s);
+int launch_binning_scatter(const BinSortArgs& a, hipStream_t s);
+// tile_sort.hip: the per-tile depth sort (see there).  Lists of 2 ..
+// kTdsCapWave instances take one wave, up to kTdsCapBlock one workgroup in
+// registers, longer ones one workgroup through global scratch.
+constexpr uint32_t kTdsCapWave = 1024;
+constexpr uint32_t kTdsCapBlock = 24576;
+// Work-list length classes, longest first: 0 (> kTdsCapBlock), 1 (> 8192),
+// 2 (> 2048), 3 (> kTdsCapWave) take a workgroup each; 4 (> 256), 5 (> 64),
+// 6 (>= 2) a wave each; kTdsClasses: nothing to sort.
+constexpr int kTdsClasses = 7;
+constexpr int kTdsBlockClasses = 4;
+__host__ __device__ constexpr uint32_t tds_class_of(uint32_t len) {
+    return len > kTdsCapBlock ? 0u
+           : len > 8192u      ? 1u
+           : len > 2048u      ? 2u
+           : len > kTdsCapWave ? 3u
+           : len > 256u       ? 4u
+           : len > 64u        ? 5u
+           : len >= 2u        ? 6u
+                              : (uint32_t)kTdsClasses;
+}
+struct TileSortView {
+    const uint2* ranges;
+    const uint32_t* list;    // the work list (launch_chunks' tds_list)
+    const uint32_t* counts;  // {workgroup-class tiles, wave-class tiles} (tds_counts)
+    uint32_t* keys;          // each list position's depth key (the tile sort's payload); permuted
+    uint32_t* vals;          // the tile lists (slots): sorted in place
+    uint32_t* keys_alt;      // n_dup words each of scratch (the tile sort's alternate buffers)
+    uint32_t* vals_alt;
+    uint32_t n_dup;
+};
+// debug (GSR_DEBUG_TDS, timing experiments only; 0 in production): 1 skips the
+// workgroup-class lists, 2 the wave-class lists, 4 sorts one digit pass only
+int launch_tile_depth_sort(const TileSortView* views, int k, int num_tiles, hipStream_t s, uint32_t debug = 0);
+
 // chunk_cnt must hold chunk_cnt_elems(num_tiles) entries (block totals after the tiles);
 // order: one entry per chunk (dispatch position -> chunk slot)
 size_t chunk_cnt_elems(int num_tiles);
+// the per-tile depth sort's work-list counts, written by launch_chunks (2 words in chunk_cnt)
+const uint32_t* tds_counts(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes);
 // classes (2 .. kMaxLenClasses): dispatch order = full chunks, then the partial
 // ones in classes - 1 length classes, longest first; the frame's chunk count
 // of each class lands at chunk_class_totals(chunk_cnt, num_tiles, classes)
+// tds_list (nullable, num_tiles words): the per-tile depth sort's work list, the
+// tiles with >= 2 instances by tds_class_of, class-major, tile order within a class
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
-                  hipStream_t s, bool first_major = false);
+                  hipStream_t s, bool first_major = false, uint32_t* tds_list = nullptr);
 const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes);
 int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n_chunks_dev, uint32_t max_chunks,
                      const uint32_t* chunk_cnt, const uint32_t* chunk_base, uint32_t* sat,
@@ -479,7 +510,8 @@ int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const fl
 // the frame size, t_min, background, output layout and chunk length.
 struct FinishView {
     // binning (n_vis, n_dup: this view's exact counts)
-    const uint32_t* sorted_ids;
+    const uint32_t* sorted_ids;  // null: slot order (the per-tile depth sort), slot_keys ride along
+    const uint32_t* slot_keys;
     const uint2* trect;
     const uint32_t* rect4_sorted;  // nullable, on every view or none (launch_binning)
     uint32_t n_vis, n_dup;
@@ -487,7 +519,8 @@ struct FinishView {
     uint2* trect_sorted;
     uint32_t* tile_keys;  // tile-sorted (keys, vals) after the tile sort
     uint32_t* tile_vals;
-    RunFix fix;           // coarse depth order repair (vals, scratch set after the tile sort)
+    uint32_t* inst_keys;  // per-tile depth sort: the instances' depth keys (binning + tile sort payload), else null
+    uint32_t* tds_list;   // ... its work list (num_tiles words), else null
     // chunks, composite, merge
     uint2* ranges;
     uint32_t* chunk_cnt;
@@ -503,9 +536,12 @@ struct FinishView {
 };
 // binning: bin_tmp of each view holds its per-block instance counts
 int launch_binning_views(FinishView* views, int k, int tiles_x, uint32_t stage_limit, hipStream_t s);
-// ... and with the tile sort's pass 0 fused in (hist[v], totals[v] per view)
-int launch_binning_sorted_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
-                                int tbits, int passes, hipStream_t s);
+// ... and with the tile sort's pass 0 fused in (hist[v], totals[v] per view), in
+// the two halves of launch_binning_hist / launch_binning_scatter
+int launch_binning_hist_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
+                              int tbits, int passes, hipStream_t s);
+int launch_binning_scatter_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k,
+                                 int tiles_x, int tbits, int passes, hipStream_t s);
 int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s);
 // first_major: every tile's first chunk dispatched before any later chunk
 int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, uint32_t classes, bool first_major,

@@ -43,8 +43,9 @@ HIP kernels) as follows:
 * ``gl8`` blending is the RGBA8 framebuffer's fixed-point arithmetic as Mesa
   llvmpipe performs it: the fragment colour and alpha are converted to unorm8
   (``rint(fl32(v * 255/256) * 256)``), then
-  ``dst = min(255, mul8(src, a) + mul8(dst, 255 - a))`` with the exactly
-  rounded ``mul8(x, y) = (t + (t >> 8) + 128) >> 8``, ``t = x y``;
+  ``dst = min(255, mul8(src, a) + mul8(dst, 255 - a))`` with llvmpipe's
+  approximation of x y / 255, ``mul8(x, y) = (t + (t >> 8) + 128) >> 8``,
+  ``t = x y`` (not exactly rounded: 24 of the 65536 pairs differ);
 * ``coordxy`` at a pixel centre is the affine interpolation of the
   per-vertex values ``position*quadwh_scr`` (all four vertices have w = 1);
 * primitives with ``|ndc.z| > 1`` are clipped away entirely (all four
@@ -445,8 +446,9 @@ def to_unorm8(v):
 
 
 def mul8(x, y):
-    """Exactly rounded x*y/255 of two unorm8 values (Blinn's form, as
-    llvmpipe's lp_build_mul_norm)."""
+    """llvmpipe's approximation of x*y/255 for two unorm8 values (Blinn's
+    form, lp_build_mul_norm): not exactly rounded, it differs from
+    round(x*y/255) on 24 of the 65536 pairs; the llvmpipe goldens pin it."""
     t = x * y
     return (t + (t >> 8) + 128) >> 8
 

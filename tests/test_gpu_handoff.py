@@ -19,9 +19,16 @@ orderings every time (composite_chunk):
 The same contexts render two different views alternately (the partial slots
 then hold another frame's values), with small chunks and t_min > 0 on a dense,
 opaque scene (many multi-chunk tiles; later chunks saturate slices).  Every
-frame must equal the k_merge path's (GSR_TAIL_MERGE=0) bit for bit.  The
-verification builds -DGSR_TAIL_REVERT_SAT_ATOMIC / -DGSR_TAIL_REVERT_SC1_LOADS
-(the code before each fix) fail these checks (profiles/r4_*/README.md).
+frame must equal the k_merge path's (GSR_TAIL_MERGE=0) bit for bit.
+
+What this does NOT show: the verification builds -DGSR_TAIL_REVERT_SAT_ATOMIC
+and -DGSR_TAIL_REVERT_SC1_LOADS (the code before each round-3 fix) PASS these
+checks too (profiles/r4_s6/README.md), and a microbenchmark found the XCD L2
+coherent for exactly these accesses (profiles/r4_s5).  So the tests guard the
+fold's logic under forced orderings (chunk order, the saturation bound, slots
+holding another frame's values), not the two memory-visibility forms; round
+3's run-to-run mismatch has no confirmed cause ("Tail merge:
+determinism").
 """
 import numpy as np
 import pytest

@@ -1,0 +1,194 @@
+"""The per-tile depth sort (gsviewer_amd/csrc/tile_sort.hip, the default form).
+
+Each tile's list is binned in slot order and sorted by its instances' depth
+keys inside the tile, instead of a global depth sort before the binning.
+The order it must produce is the GL draw order restricted to the tile, the
+one /root/reference/render/renderer_ogl.py:16-26 draws back to front (read
+front to back; ties in descending Gaussian id).  Checked here, against the
+exact form (GSR_TILE_DEPTH_SORT=0: the global radix depth sort, then a stable
+binning in depth order; tests/test_gpu_parity.py checks that form's global
+order and tile lists against the oracle), bit for bit (tile lists, ranges,
+records, images):
+
+* every work-list class (tds_class_of: one wave per list of 2..1024, one
+  workgroup per list up to 24576 in registers, one workgroup through global
+  scratch beyond, several 12288-instance sub-blocks per pass);
+* lists whose keys are all equal, or take two values (ties by slot only);
+* the adversarial case of round 4's coarse order: a dense fronto-parallel
+  plane plus one far splat that stretches the frame's key range, at 1080p,
+  whose frame must also stay within 1.5x the exact form's time;
+* a group of views (gsr_render_finish_views), deep lists included.
+"""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from gsviewer_amd.camera import Camera
+from gsviewer_amd.gaussian_data import GaussianData
+from helpers import batched_frames, check_depth_order, compare_images, gpu_frame, uniforms_for
+from oracle import c_oracle as C
+from oracle import gl_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CAP_WAVE, CAP_BLOCK = 1024, 24576  # gsr_internal.h kTdsCapWave / kTdsCapBlock
+
+
+def tds_class(lens):
+    """gsr_internal.h tds_class_of (7: nothing to sort)."""
+    lens = np.asarray(lens, np.int64)
+    return np.select([lens > CAP_BLOCK, lens > 8192, lens > 2048, lens > CAP_WAVE, lens > 256, lens > 64, lens >= 2],
+                     [0, 1, 2, 3, 4, 5, 6], 7)
+
+
+def _settings(**kw):
+    from gsviewer_amd.rasterizer import RenderSettings
+    return RenderSettings(**kw)
+
+
+def _scene(xyz, scale, seed, opacity=(0.05, 0.6)):
+    rng = np.random.default_rng(seed)
+    n = len(xyz)
+    rot = rng.normal(0, 1, (n, 4)).astype(np.float32)
+    rot /= np.linalg.norm(rot, axis=1, keepdims=True)
+    return GaussianData(np.asarray(xyz, np.float32), rot, np.asarray(scale, np.float32),
+                        rng.uniform(*opacity, (n, 1)).astype(np.float32),
+                        rng.normal(0, 0.5, (n, 3)).astype(np.float32))
+
+
+def graded_scene(n=400_000, seed=11):
+    """Density falling off exponentially to the right of the frame: tile lists
+    from a few instances to > 24576 (every work-list class)."""
+    rng = np.random.default_rng(seed)
+    x = -1.6 + rng.exponential(0.35, n)
+    y = rng.uniform(-1.0, 1.0, n)
+    z = rng.uniform(-1.0, 1.0, n)
+    scale = np.exp(rng.uniform(np.log(0.004), np.log(0.03), (n, 3)))
+    return _scene(np.stack([x, y, z], 1), scale, seed)
+
+
+def plane_scene(n=250_000, seed=12, far=True, levels=0):
+    """A dense fronto-parallel plane (z = 0 facing the default camera): with
+    levels = 0 a jitter of 1e-4 in depth, else exactly `levels` distinct
+    depths; plus (far) one splat 400 units behind it, which stretches the
+    frame's depth-key range."""
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-1.0, 1.0, n)
+    y = rng.uniform(-0.6, 0.6, n)
+    z = rng.uniform(-1e-4, 1e-4, n) if levels == 0 else rng.integers(0, levels, n) * 0.01
+    scale = np.exp(rng.uniform(np.log(0.004), np.log(0.02), (n, 3)))
+    scale[:, 2] = 1e-4
+    xyz = np.stack([x, y, z], 1)
+    if far:
+        xyz = np.concatenate([xyz, [[0.0, 0.0, -400.0]]])
+        scale = np.concatenate([scale, [[2.0, 2.0, 2.0]]])
+    return _scene(xyz, scale, seed, opacity=(0.02, 0.2))
+
+
+def _frames(monkeypatch, g, cam, st, form):
+    monkeypatch.setenv("GSR_TILE_DEPTH_SORT", "1" if form == "tile" else "0")
+    return gpu_frame(g, cam, st, with_debug=True)
+
+
+def _same(a, b, what=""):
+    for key in ("tile_list", "ranges", "records", "image"):
+        np.testing.assert_array_equal(a[key], b[key], err_msg=f"{what} {key}")
+    assert a["stats"] == b["stats"], what
+
+
+def test_every_class_matches_exact_form(gpu, monkeypatch):
+    g = graded_scene()
+    cam = Camera(540, 960)
+    st = _settings(t_min=0.0)
+    tile = _frames(monkeypatch, g, cam, st, "tile")
+    exact = _frames(monkeypatch, g, cam, st, "exact")
+    _same(tile, exact)
+    assert check_depth_order(exact, O.vertex_stage(g.flat(), g.sh_dim, uniforms_for(cam)))
+    lens = (tile["ranges"][:, 1] - tile["ranges"][:, 0]).astype(np.int64)
+    classes = set(tds_class(lens).tolist())
+    assert {0, 1, 2, 3, 4, 5, 6} <= classes, sorted(classes)
+    assert lens.max() > 2 * 12288, lens.max()  # several sub-blocks per pass on the global path
+
+
+def test_deep_lists_image_against_oracle(gpu, monkeypatch):
+    """The global path's frame against the C oracle at the stated tolerances
+    (small frame: every tile deep)."""
+    g = graded_scene(n=120_000, seed=5)
+    cam = Camera(96, 160)
+    st = _settings(t_min=0.0)
+    res = _frames(monkeypatch, g, cam, st, "tile")
+    lens = res["ranges"][:, 1].astype(np.int64) - res["ranges"][:, 0]
+    assert lens.max() > CAP_BLOCK, lens.max()
+    ref = C.render(g.flat(), g.sh_dim, uniforms_for(cam), mode="float")
+    compare_images(res["image"], ref)
+
+
+@pytest.mark.parametrize("levels", [1, 2])
+def test_equal_depths(gpu, monkeypatch, levels):
+    """Lists whose depth keys are all equal (nothing to sort: slot order) or
+    take two values."""
+    g = plane_scene(n=60_000, far=False, levels=levels)
+    cam = Camera(270, 480)
+    st = _settings(t_min=1e-4)
+    tile = _frames(monkeypatch, g, cam, st, "tile")
+    exact = _frames(monkeypatch, g, cam, st, "exact")
+    _same(tile, exact, f"levels {levels}")
+    assert tile["stats"]["n_instances"] > 50_000
+
+
+def _frame_ms(monkeypatch, g, cam, st, form, reps=10):
+    from gsviewer_amd.rasterizer import HipContext, HipScene, camera_from, render_into
+    monkeypatch.setenv("GSR_TILE_DEPTH_SORT", "1" if form == "tile" else "0")
+    scene = HipScene.from_gaussian_data(g)
+    ctx = HipContext()
+    out = torch.empty((cam.h, cam.w, 3), dtype=torch.float32, device="cuda")
+    c = camera_from(cam)
+    st.out_layout = 1
+    render_into(ctx, scene, c, st, out)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        render_into(ctx, scene, c, st, out)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    ctx.close()
+    scene.close()
+    return 1e3 * float(np.median(ts))
+
+
+def test_plane_with_far_splat(gpu, monkeypatch):
+    """Round 4's adversarial case for the coarse depth order:
+    a dense fronto-parallel plane plus one far splat at 1080p.  Bit-identical
+    to the exact form, and its frame within 1.5x the exact form's."""
+    g = plane_scene()
+    cam = Camera(1080, 1920)
+    st = _settings(t_min=1e-4)
+    tile = _frames(monkeypatch, g, cam, st, "tile")
+    exact = _frames(monkeypatch, g, cam, st, "exact")
+    _same(tile, exact)
+    lens = tile["ranges"][:, 1].astype(np.int64) - tile["ranges"][:, 0]
+    assert lens.max() > 1000, lens.max()
+    ms_tile = _frame_ms(monkeypatch, g, cam, _settings(t_min=1e-4), "tile")
+    ms_exact = _frame_ms(monkeypatch, g, cam, _settings(t_min=1e-4), "exact")
+    print(f"plane + far splat, 1080p: per-tile {ms_tile:.3f} ms, exact {ms_exact:.3f} ms")
+    assert ms_tile <= 1.5 * ms_exact, (ms_tile, ms_exact)
+
+
+@pytest.mark.parametrize("scene_kind", ["graded", "plane"])
+def test_group_matches_exact_form(gpu, monkeypatch, scene_kind):
+    from gsviewer_amd.rasterizer import HipScene
+    g = graded_scene(n=200_000) if scene_kind == "graded" else plane_scene(n=100_000)
+    cams = [Camera(270, 480).yaw(v * 20.0) for v in range(3)]
+    res = {}
+    for form in ("tile", "exact"):
+        monkeypatch.setenv("GSR_TILE_DEPTH_SORT", "1" if form == "tile" else "0")
+        scene = HipScene.from_gaussian_data(g)
+        res[form] = batched_frames(scene, cams, _settings(t_min=1e-4), group=3, debug_views=(0, 1, 2))
+        scene.close()
+    for v in range(3):
+        a, b = res["tile"][v], res["exact"][v]
+        for key in ("tile_list", "ranges", "records", "image"):
+            np.testing.assert_array_equal(a[key], b[key], err_msg=f"view {v} {key}")

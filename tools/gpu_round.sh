@@ -34,6 +34,8 @@ else
 fi
 step rocprof_stats 240 bash -c "rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- $B > $O/bench_under_rocprof.json 2> $O/rocprof.err"
 find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \;
+# the compositing kernel's busy time per view (union of its overlapping launches), bench.py's cross-check
+step busy_union 60 bash -c "python tools/busy_union.py \$(find $O/prof -name '*kernel_trace.csv' | head -1) > $O/composite_busy.json"
 if [ "$MODE" != quick ]; then
     step pmc 800 bash tools/pmc.sh $TAG traffic
 fi
