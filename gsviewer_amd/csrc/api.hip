@@ -188,6 +188,7 @@ struct gsr_context {
     uint32_t bin_stage_limit = 0xffffffffu;       // blocks of at most this many instances stage them (build cap)
     uint32_t debug_handoff = 0;                   // tail-merge test knob (GSR_DEBUG_HANDOFF; 0 in production)
     uint32_t debug_tds = 0;                       // per-tile sort timing knob (GSR_DEBUG_TDS; 0 in production)
+    gsr::DevBuf<uint64_t> tds_stamps;             // ... its stamps (debug_tds & 8; not in the workspace)
     bool fused_cull = true;                       // culling inside the preprocess (launch_preprocess_fc)
     int depth_passes_alone = kDepthPassesAlone;   // depth sort passes of gsr_render's frames (exact form)
     int depth_passes_now = 0;                     // this frame's (0: kDepthPasses)
@@ -196,10 +197,12 @@ struct gsr_context {
     bool rect_payload = true;                     // the exact form's depth sort carries the packed tile rects
                                                   // (GSR_NO_RECT_PAYLOAD: gathered by the binning; A/B knob)
     gsr::DevBuf<uint32_t> tpay_a, tpay_b;  // the instances' depth keys through the tile sort (per-tile sort)
-    gsr::DevBuf<uint32_t> tds_list;        // the per-tile sort's work list (num_tiles)
+    uint32_t tds_coarse_cap = 8;           // coarse depth bits folded into the tile keys, at most
+                                           // (GSR_TDS_COARSE_BITS; TileBits takes what the passes have room for)
     // the per-tile sort's binning counts: enqueued before the host knows D, so
     // in a buffer of their own (radix_tmp may grow with D before the scatter reads them)
     gsr::DevBuf<uint32_t> bin_hist;
+    gsr::DevBuf<uint2> big_runs;           // the per-tile sort's runs of > kTdsCapWave instances (start, length)
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
     uint32_t seq = 0;                       // frame sequence number the host waits for
     uint32_t* host_counters_dev = nullptr;  // its device address
@@ -250,7 +253,7 @@ void each_buf(gsr_context* c, F&& f) {
     f(c->vis_mask); f(c->wave_counts); f(c->block_ranges); f(c->scan_tmp); f(c->recs);
     f(c->keys_a); f(c->keys_b); f(c->vals_a); f(c->vals_b); f(c->trect); f(c->trect_sorted);
     f(c->rect4_a); f(c->rect4_b); f(c->bin_tmp); f(c->tkeys_a); f(c->tkeys_b); f(c->tvals_a); f(c->tvals_b);
-    f(c->tpay_a); f(c->tpay_b); f(c->tds_list); f(c->bin_hist);
+    f(c->tpay_a); f(c->tpay_b); f(c->bin_hist); f(c->big_runs);
     f(c->radix_tmp); f(c->zero); f(c->chunk_cnt); f(c->chunk_base); f(c->chunk_desc); f(c->chunk_order);
     f(c->partial); f(c->tmax); f(c->done_ctr);
 }
@@ -338,18 +341,20 @@ int bits_for(uint32_t v) {  // bits needed to represent values < v
 // Per-frame scratch block: [0,4) counters {V, D, extra chunks, -} are
 // overwritten every frame; from `cleared` on, the depth-key range
 // {~kmin, kmax}, the radix digit totals (depth sort, tile sort), the tile
-// ranges (uint2, 16-B aligned), the saturation words (4 per tile) and the
+// ranges (uint2, 16-B aligned), the saturation words (4 per tile), the
 // chunk completion counters of the tail merge (1 per tile, right after the
-// saturation words) are zeroed by k_cull.
+// saturation words) and the per-tile depth sort's count of long runs are
+// zeroed by k_cull (or the fused preprocess, from `ranges` on).
 struct ZeroLayout {
     size_t counters = 0, cleared = 4, key_range = 4, totals_depth = 8, totals_tile = 0, ranges = 0, sat = 0,
-           total = 0;
+           big_runs = 0, total = 0;
     explicit ZeroLayout(int num_tiles) {
         const size_t tot = radix_totals_elems();
         totals_tile = totals_depth + tot;
         ranges = (totals_tile + tot + 3) & ~(size_t)3;
         sat = ranges + 2 * (size_t)num_tiles;
-        total = sat + 5 * (size_t)num_tiles;
+        big_runs = sat + 5 * (size_t)num_tiles;
+        total = big_runs + 4;
     }
 };
 
@@ -486,14 +491,27 @@ int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const 
 }
 
 // The tile sort's digits for a frame of num_tiles tiles.
+// The tile sort of a frame: the tile id's bits, the passes of <= 11-bit digits
+// they take (the binning is pass 0), and, for the per-tile depth sort, the
+// coarse depth bits folded into the keys below the tile id (InstKey,
+// composite.hip): what room 8-bit digits leave in those passes, so they cost
+// no pass (13 tile bits at 1080p: 2 passes of 8, 3 coarse bits; 4K: 15 + 1).
 struct TileBits {
     int bits, passes;
-    explicit TileBits(int num_tiles) : bits(bits_for((uint32_t)num_tiles)), passes(radix_passes_for(bits)) {}
+    uint32_t cb = 0;
+    TileBits(int num_tiles, bool tds, uint32_t cap) : bits(bits_for((uint32_t)num_tiles)), passes(radix_passes_for(bits)) {
+        // up to 8-bit digits: the 256-digit kernels (2048 digits over 1.76 M instances cost binning + tile sort
+        // 65 -> 170 us at C2, profiles/r5_s9)
+        const int room = sort_passes() * 8 - std::max(bits, 1);
+        if (tds && room > 0) cb = std::min(cap, (uint32_t)room);
+    }
+    int key_bits() const { return std::max(bits, 1) + (int)cb; }
+    int sort_passes() const { return std::max(passes, 1); }
 };
 
 // The per-tile depth sort's binning of a context's frame (slot order, keys carried).
 BinSortArgs tds_binning(gsr_context* c, const FrameUniforms& u, uint32_t n_slots) {
-    const TileBits tb(u.tiles_x * u.tiles_y);
+    const TileBits tb(u.tiles_x * u.tiles_y, true, c->tds_coarse_cap);
     const ZeroLayout zl(u.tiles_x * u.tiles_y);
     BinSortArgs a{};
     a.sorted_ids = nullptr;
@@ -510,6 +528,8 @@ BinSortArgs tds_binning(gsr_context* c, const FrameUniforms& u, uint32_t n_slots
     a.tile_vals = c->tvals_a.p;
     a.slot_keys = c->keys_a.p;
     a.inst_keys = c->tpay_a.p;
+    a.coarse_bits = tb.cb;
+    a.key_range = c->zero.p + zl.key_range;
     return a;
 }
 
@@ -521,9 +541,8 @@ uint32_t binning_slots(const gsr_context* c, size_t n, uint32_t n_vis) {
 
 // The per-tile sort's binning counts of a frame (sized before they are enqueued).
 int ensure_bin_hist(gsr_context* c, size_t n_slots, int num_tiles) {
-    const TileBits tb(num_tiles);
-    return c->bin_hist.ensure(bin_hist_elems(std::max<size_t>(n_slots, 1), tb.bits > 0 ? tb.bits : 1,
-                                             tb.passes > 0 ? tb.passes : 1),
+    const TileBits tb(num_tiles, true, c->tds_coarse_cap);
+    return c->bin_hist.ensure(bin_hist_elems(std::max<size_t>(n_slots, 1), tb.key_bits(), tb.sort_passes()),
                               "bin_hist");
 }
 
@@ -783,6 +802,10 @@ int gsr_context_create(gsr_context** out) {
         (*out)->bin_stage_limit = gsr::clamp_stage_limit(std::strtol(e, nullptr, 10));
     if (const char* e = std::getenv("GSR_DEBUG_HANDOFF")) (*out)->debug_handoff = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("GSR_DEBUG_TDS")) (*out)->debug_tds = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("GSR_TDS_COARSE_BITS")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 0 && v <= 8) (*out)->tds_coarse_cap = (uint32_t)v;
+    }
     if (const char* e = std::getenv("GSR_WAIT_TIMEOUT_MS")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1) (*out)->wait_timeout_ms = v;
@@ -802,6 +825,7 @@ int gsr_context_destroy(gsr_context* c) {
         for (auto& e : row)
             if (e) (void)hipEventDestroy(e);
     c->stamps.release();
+    c->tds_stamps.release();
     delete c;
     return GSR_OK;
 }
@@ -838,9 +862,9 @@ int gsr_context_reserve(gsr_context* c, int64_t n, int32_t width, int32_t height
     if ((rc = c->tvals_b.ensure(d, "tile_vals"))) return rc;
     if (c->tile_depth_sort) {  // the instances' depth keys through the tile sort, the per-tile sort's work list
         if ((rc = ensure_bin_hist(c, un, num_tiles))) return rc;
+        if ((rc = c->big_runs.ensure(d / (kTdsCapWave + 1) + 1, "big_runs"))) return rc;
         if ((rc = c->tpay_a.ensure(d, "tile_pay"))) return rc;
         if ((rc = c->tpay_b.ensure(d, "tile_pay"))) return rc;
-        if ((rc = c->tds_list.ensure((size_t)num_tiles, "tds_list"))) return rc;
     }
     if ((rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(d), radix_tmp_elems(un), rhist}), "radix_tmp"))) return rc;
     const size_t mc = (size_t)num_tiles + d / std::min(c->chunk, c->chunk_views) + 1;
@@ -1123,10 +1147,11 @@ int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream) {
         const bool bin_now = ctxs[0]->fused_cull && n > 0;
         if (bin_now) {
             const int num_tiles = f0.u.tiles_x * f0.u.tiles_y;
-            const TileBits tb(num_tiles);
+            const TileBits tb(num_tiles, true, ctxs[0]->tds_coarse_cap);
             FinishView fv[GSR_MAX_VIEWS];
             uint32_t* hist[GSR_MAX_VIEWS];
             uint32_t* ttot[GSR_MAX_VIEWS];
+            const uint32_t* kr[GSR_MAX_VIEWS];
             for (int v = 0; v < k; ++v) {
                 gsr_context* c = ctxs[v];
                 if ((rc = ensure_bin_hist(c, n, num_tiles))) return rc;
@@ -1139,8 +1164,12 @@ int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream) {
                 fv[v].inst_keys = a.inst_keys;
                 hist[v] = a.hist;
                 ttot[v] = a.totals;
+                kr[v] = a.key_range;
+                if (c->tds_coarse_cap != ctxs[0]->tds_coarse_cap)
+                    return set_error(GSR_ERR_INVALID, "render_begin_sorts: contexts differ in GSR_TDS_COARSE_BITS");
             }
-            if ((rc = launch_binning_hist_views(fv, hist, ttot, k, f0.u.tiles_x, tb.bits, tb.passes, s))) return rc;
+            if ((rc = launch_binning_hist_views(fv, hist, ttot, k, f0.u.tiles_x, tb.bits, tb.passes, s, tb.cb, kr)))
+                return rc;
         }
         for (int v = 0; v < k; ++v) {
             PendingFrame& f = ctxs[v]->pend;
@@ -1205,7 +1234,7 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     if (n_vis > 0 && !f.tds) c->last_depth_order = f.va;
 
     uint32_t* tile_list = c->tvals_a.p;
-    const TileBits tb(num_tiles);
+    const TileBits tb(num_tiles, f.tds, c->tds_coarse_cap);
     const bool fused = f.tds || c->bin_fused;  // (the per-tile sort's binning is always the fused one)
     uint32_t *tpa = c->tpay_a.p, *tpb = c->tpay_b.p;
     if (n_dup > 0) {
@@ -1214,14 +1243,13 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         if ((rc = c->tvals_a.ensure(n_dup, "tile_vals"))) return rc;
         if ((rc = c->tvals_b.ensure(n_dup, "tile_vals"))) return rc;
         if ((rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(n_dup), radix_tmp_elems(n),
-                                                bin_hist_elems(n, tb.bits > 0 ? tb.bits : 1,
-                                                               tb.passes > 0 ? tb.passes : 1)}),
+                                                bin_hist_elems(n, tb.key_bits(), tb.sort_passes())}),
                                       "radix_tmp")))
             return rc;
         if (f.tds) {
             if ((rc = c->tpay_a.ensure(n_dup, "tile_pay"))) return rc;
             if ((rc = c->tpay_b.ensure(n_dup, "tile_pay"))) return rc;
-            if ((rc = c->tds_list.ensure((size_t)num_tiles, "tds_list"))) return rc;
+            if ((rc = c->big_runs.ensure(n_dup / (kTdsCapWave + 1) + 1, "big_runs"))) return rc;
             tpa = c->tpay_a.p, tpb = c->tpay_b.p;
             const uint32_t slots = binning_slots(c, n, n_vis);
             if (!f.binned && (rc = ensure_bin_hist(c, slots, num_tiles))) return rc;  // (binned: sized in begin)
@@ -1252,20 +1280,37 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     if ((rc = prof_mark(c, slot, GSR_STAGE_BINNING, s))) return rc;
     uint32_t *tka = c->tkeys_a.p, *tkb = c->tkeys_b.p, *tva = c->tvals_a.p, *tvb = c->tvals_b.p;
     if (n_dup > 0) {
-        if (tb.bits > 0 && (rc = radix_sort_pairs(&tka, &tva, &tkb, &tvb, false, n_dup, nullptr, tb.bits, tb.passes,
-                                                  nullptr, c->radix_tmp.p, c->zero.p + zl.totals_tile, s, nullptr,
-                                                  f.tds ? &tpa : nullptr, f.tds ? &tpb : nullptr, fused ? 1 : 0)))
+        // (the exact form with a single tile: no key bits, nothing to sort)
+        if ((tb.bits > 0 || f.tds) &&
+            (rc = radix_sort_pairs(&tka, &tva, &tkb, &tvb, false, n_dup, nullptr, tb.key_bits(), tb.sort_passes(),
+                                   nullptr, c->radix_tmp.p, c->zero.p + zl.totals_tile, s, nullptr,
+                                   f.tds ? &tpa : nullptr, f.tds ? &tpb : nullptr, fused ? 1 : 0)))
             return rc;
         tile_list = tva;
         c->last_tile_list = tva;
     }
     if ((rc = prof_mark(c, slot, GSR_STAGE_TILE_SORT, s))) return rc;
-    if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, ranges, s))) return rc;
+    uint32_t* big_count = c->zero.p + zl.big_runs;
+    if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, ranges, s, tb.cb, f.tds ? c->big_runs.p : nullptr,
+                                              big_count)))
+        return rc;
+    if ((rc = prof_mark(c, slot, GSR_STAGE_RANGES, s))) return rc;
+    if (f.tds && n_dup > 0) {  // each tile's runs of one coarse depth bucket to (depth key, slot) order
+        const TileSortView tv{tka, tpa, tva, tpb, tvb, n_dup, c->big_runs.p, big_count};
+        uint64_t* stamps = nullptr;
+        if (c->debug_tds & 8u) {
+            const size_t words = 8 * ((size_t)n_dup / kTdsSpan + 1);
+            if ((rc = c->tds_stamps.ensure(words, "tds_stamps"))) return rc;
+            GSR_HIP_CHECK(hipMemsetAsync(c->tds_stamps.p, 0, words * 8, s));
+            stamps = c->tds_stamps.p;
+        }
+        if ((rc = launch_tile_depth_sort(&tv, 1, s, c->debug_tds, stamps))) return rc;
+        if ((rc = prof_mark(c, slot, GSR_STAGE_DEPTH_SORT, s))) return rc;
+    }
 
-    // compositing chunks: at most one per tile plus one per `chunk` instances (and, per-tile sort, its work list)
+    // compositing chunks: at most one per tile plus one per `chunk` instances
     const size_t max_chunks = (size_t)num_tiles + n_dup / c->chunk + 1;
-    const bool chunks = f.blend != GSR_BLEND_UNORM8 || f.tds;
-    if (chunks) {
+    if (f.blend != GSR_BLEND_UNORM8) {
         if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
         if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
         if ((rc = c->chunk_desc.ensure(max_chunks, "chunk_desc"))) return rc;
@@ -1273,17 +1318,10 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
         if ((rc = c->tmax.ensure(max_chunks, "tmax"))) return rc;
         if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->len_classes, c->chunk_cnt.p, c->chunk_base.p,
-                                counters + 2, c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s, c->first_major_alone,
-                                f.tds && n_dup > 0 ? c->tds_list.p : nullptr)))
+                                counters + 2, c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s, c->first_major_alone)))
             return rc;
     }
     if ((rc = prof_mark(c, slot, GSR_STAGE_RANGES, s))) return rc;
-    if (f.tds && n_dup > 0) {
-        const TileSortView tv{ranges, c->tds_list.p, tds_counts(c->chunk_cnt.p, num_tiles, c->len_classes),
-                              tpa, tva, tpb, tvb, n_dup};
-        if ((rc = launch_tile_depth_sort(&tv, 1, num_tiles, s, c->debug_tds))) return rc;
-        if ((rc = prof_mark(c, slot, GSR_STAGE_DEPTH_SORT, s))) return rc;
-    }
 
     if (f.blend == GSR_BLEND_UNORM8) {  // the RGBA8 framebuffer: whole lists, back to front, no chunks
         if ((rc = launch_composite_unorm8(ranges, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.bg,
@@ -1388,8 +1426,10 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         if (tds) {  // (every view's, so that each has the buffers even without instances)
             if ((rc = c->tpay_a.ensure(std::max<uint32_t>(n_dup, 1), "tile_pay"))) return rc;
             if ((rc = c->tpay_b.ensure(std::max<uint32_t>(n_dup, 1), "tile_pay"))) return rc;
+            if ((rc = c->big_runs.ensure(n_dup / (kTdsCapWave + 1) + 1, "big_runs"))) return rc;
         }
-        if (tds && (rc = c->tds_list.ensure((size_t)num_tiles, "tds_list"))) return rc;
+        if (tds && c->tds_coarse_cap != c0->tds_coarse_cap)
+            return set_error(GSR_ERR_INVALID, "render_finish_views: contexts differ in GSR_TDS_COARSE_BITS");
         const size_t mc = (size_t)num_tiles + n_dup / c->chunk_views + 1;
         max_chunks = std::max(max_chunks, mc);
         if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
@@ -1416,7 +1456,8 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         fv[v].tile_keys = tka[v];
         fv[v].tile_vals = tva[v];
         fv[v].inst_keys = tds ? tpa[v] : nullptr;
-        fv[v].tds_list = tds ? c->tds_list.p : nullptr;
+        fv[v].big_runs = tds ? c->big_runs.p : nullptr;
+        fv[v].big_count = c->zero.p + zl.big_runs;
         fv[v].ranges = reinterpret_cast<uint2*>(c->zero.p + zl.ranges);
         fv[v].chunk_cnt = c->chunk_cnt.p;
         fv[v].chunk_base = c->chunk_base.p;
@@ -1432,17 +1473,17 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
                               c->zero.p + zl.totals_tile, nullptr, tds ? &tpa[v] : nullptr, tds ? &tpb[v] : nullptr};
     }
     // every view's sort temporaries cover the largest view (the grids do)
-    const TileBits tb(num_tiles);
+    const TileBits tb(num_tiles, tds, c0->tds_coarse_cap);
     const bool fused = tds || c0->bin_fused;  // (the per-tile sort's binning is always the fused one)
     uint32_t* hist[GSR_MAX_VIEWS];
     uint32_t* ttot[GSR_MAX_VIEWS];
+    const uint32_t* krange[GSR_MAX_VIEWS];
     for (int v = 0; v < k; ++v) {
         gsr_context* c = ctxs[v];
         if (n_dup_max > 0 &&
             (rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(n_dup_max), radix_tmp_elems(c->pend.n),
-                                                bin_hist_elems(std::max<size_t>(n_slots, c->pend.n),
-                                                               tb.bits > 0 ? tb.bits : 1,
-                                                               tb.passes > 0 ? tb.passes : 1)}),
+                                                bin_hist_elems(std::max<size_t>(n_slots, c->pend.n), tb.key_bits(),
+                                                               tb.sort_passes())}),
                                       "radix_tmp")))
             return rc;
         rv[v].tmp = c->radix_tmp.p;
@@ -1450,21 +1491,22 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         if (tds && !c->pend.binned && (rc = ensure_bin_hist(c, n_slots, num_tiles))) return rc;
         hist[v] = tds ? c->bin_hist.p : c->radix_tmp.p;  // (the per-tile form's counts: ensure_bin_hist)
         ttot[v] = c->zero.p + zl.totals_tile;
+        krange[v] = c->zero.p + zl.key_range;
     }
     if (n_slots > 0 && n_dup_max > 0) {
         if (fused) {
             // the counts, unless begin_sorts enqueued them (every view or none: the same form and cull)
             if (!(tds && c0->pend.binned) &&
-                (rc = launch_binning_hist_views(fv, hist, ttot, k, u0.tiles_x, tb.bits, tb.passes, s)))
+                (rc = launch_binning_hist_views(fv, hist, ttot, k, u0.tiles_x, tb.bits, tb.passes, s, tb.cb, krange)))
                 return rc;
-            rc = launch_binning_scatter_views(fv, hist, ttot, k, u0.tiles_x, tb.bits, tb.passes, s);
+            rc = launch_binning_scatter_views(fv, hist, ttot, k, u0.tiles_x, tb.bits, tb.passes, s, tb.cb, krange);
         } else {
             rc = launch_binning_views(fv, k, u0.tiles_x, c0->bin_stage_limit, s);
         }
         if (rc) return rc;
     }
-    if (n_dup_max > 0 && tb.bits > 0 &&
-        (rc = radix_sort_pairs_views(rv, k, false, n_dup_max, tb.bits, tb.passes, s, fused ? 1 : 0)))
+    if (n_dup_max > 0 && (tb.bits > 0 || tds) &&
+        (rc = radix_sort_pairs_views(rv, k, false, n_dup_max, tb.key_bits(), tb.sort_passes(), s, fused ? 1 : 0)))
         return rc;
     for (int v = 0; v < k; ++v) {
         fv[v].tile_keys = tka[v];
@@ -1472,18 +1514,17 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         fv[v].inst_keys = tds ? tpa[v] : nullptr;
         if (fv[v].n_dup > 0) ctxs[v]->last_tile_list = tva[v];
     }
-    if ((rc = launch_tile_ranges_views(fv, k, s))) return rc;
-    const PendingFrame& f0 = c0->pend;
-    const bool unorm8 = f0.blend == GSR_BLEND_UNORM8;
-    if (!unorm8 || tds)
-        if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk_views, c0->len_classes, c0->first_major, s))) return rc;
-    if (tds && n_dup_max > 0) {
+    if ((rc = launch_tile_ranges_views(fv, k, s, tb.cb))) return rc;
+    if (tds && n_dup_max > 0) {  // each tile's runs of one coarse depth bucket to (depth key, slot) order
         TileSortView tv[GSR_MAX_VIEWS];
         for (int v = 0; v < k; ++v)
-            tv[v] = TileSortView{fv[v].ranges, fv[v].tds_list, tds_counts(fv[v].chunk_cnt, num_tiles, c0->len_classes),
-                                 tpa[v], tva[v], tpb[v], tvb[v], fv[v].n_dup};
-        if ((rc = launch_tile_depth_sort(tv, k, num_tiles, s, c0->debug_tds))) return rc;
+            tv[v] = TileSortView{tka[v], tpa[v], tva[v], tpb[v], tvb[v], fv[v].n_dup, fv[v].big_runs, fv[v].big_count};
+        if ((rc = launch_tile_depth_sort(tv, k, s, c0->debug_tds))) return rc;
     }
+    const PendingFrame& f0 = c0->pend;
+    const bool unorm8 = f0.blend == GSR_BLEND_UNORM8;
+    if (!unorm8)
+        if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk_views, c0->len_classes, c0->first_major, s))) return rc;
     if (unorm8) {  // the RGBA8 framebuffer: one launch per view, no chunks
         for (int v = 0; v < k; ++v)
             if ((rc = launch_composite_unorm8(fv[v].ranges, fv[v].tile_vals, fv[v].recs, u0,
@@ -1660,6 +1701,10 @@ int64_t gsr_debug_copy(const gsr_context* c, int32_t what, void* dst, int64_t ma
         case GSR_DEBUG_DEPTH_ORDER: src = c->last_depth_order; bytes = c->stats.n_visible * 4; break;
         case GSR_DEBUG_TILE_RANGES: src = c->last_ranges; bytes = c->last_tiles * 8; break;
         case GSR_DEBUG_TILE_LIST: src = c->last_tile_list; bytes = c->stats.n_instances * 4; break;
+        case 5:  // (timing knob GSR_DEBUG_TDS & 8: the per-tile sort's block stamps, 8 words per block)
+            src = c->tds_stamps.p;
+            bytes = (int64_t)c->tds_stamps.cap * 8;
+            break;
         case GSR_DEBUG_SLOT_KEYS:  // (the fused cull's slots are not compacted: all n)
             src = c->keys_a.p;
             bytes = (c->fused_cull && c->stats.n_visible > 0 ? c->stats.n_gaussians : c->stats.n_visible) * 4;

@@ -259,6 +259,39 @@ struct BinScatterLds {
 // almost single-lane.
 constexpr uint32_t kSerialTiles = 64;
 
+// The tile sort's key of an instance.  Plain: the tile id.  With coarse
+// depth bits (the per-tile depth sort's binning, cb > 0): (tile << cb) |
+// bucket, the bucket the top cb bits of the splat's depth key within the
+// frame's key range, so the stable tile sort leaves each tile's list in runs
+// of equal bucket (slot order inside a run) and the per-tile depth sort
+// (tile_sort.hip) sorts runs, not whole tiles.  The bits come for free: the
+// tile sort's passes are fixed by the tile id's width, their digits widen
+// to take cb more bits (TileBits, api.hip).
+struct InstKey {
+    uint32_t cb = 0;    // coarse depth bits (0: the tile id alone)
+    uint32_t kmin = 0;  // the frame's smallest visible key
+    uint32_t s0 = 0;    // bucket = (key - kmin) >> s0
+    const uint32_t* slot_keys = nullptr;
+    __device__ __forceinline__ uint32_t bucket(uint32_t r) const {
+        return cb ? min((slot_keys[r] - kmin) >> s0, (1u << cb) - 1u) : 0u;
+    }
+    __device__ __forceinline__ uint32_t of(uint32_t tile, uint32_t bk) const { return cb ? (tile << cb) | bk : tile; }
+};
+
+__device__ __forceinline__ InstKey inst_key(uint32_t cb, const uint32_t* __restrict__ key_range,
+                                            const uint32_t* __restrict__ slot_keys) {
+    InstKey ik;
+    if (!cb || !key_range || !slot_keys) return ik;
+    ik.cb = cb;
+    ik.slot_keys = slot_keys;
+    const uint32_t nk = key_range[0], kmax = key_range[1];
+    ik.kmin = ~nk;
+    const uint32_t B = kmax > ik.kmin ? 32u - (uint32_t)__clz(kmax - ik.kmin) : 0u;
+    if (kmax < ik.kmin) ik.kmin = 0u;  // nothing visible: no instances
+    ik.s0 = B > cb ? B - cb : 0u;
+    return ik;
+}
+
 // Instance idx (generation order: depth-sorted splats, each one's tiles
 // row-major) of block blk -> (tile key, record slot), given own_o: the
 // exclusive offsets of the block's threads' instances (thread t owns splats
@@ -268,7 +301,7 @@ __device__ __forceinline__ void instance_at(uint32_t idx, const uint32_t* own_o,
                                             const uint32_t* __restrict__ sorted_ids,
                                             const uint2* __restrict__ trect_sorted,
                                             const uint32_t* __restrict__ rect4_sorted, int tiles_x, uint32_t& key,
-                                            uint32_t& val, bool sorted_pos = false) {
+                                            uint32_t& val, bool sorted_pos = false, const InstKey& ik = InstKey{}) {
     uint32_t lo = 0, hi = kThreads;  // own_o[lo] <= idx < own_o[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -288,7 +321,7 @@ __device__ __forceinline__ void instance_at(uint32_t idx, const uint32_t* own_o,
             const uint32_t tx0 = tr.x & 0xffffu, tx1 = tr.x >> 16, ty0 = tr.y & 0xffffu;
             const uint32_t w = tx1 - tx0 + 1u;
             const uint32_t dy = local / w;
-            key = (ty0 + dy) * (uint32_t)tiles_x + tx0 + (local - dy * w);
+            key = ik.of((ty0 + dy) * (uint32_t)tiles_x + tx0 + (local - dy * w), ik.bucket(r));
             val = sorted_pos || !sorted_ids ? r : sorted_ids[r];
             return;
         }
@@ -332,18 +365,20 @@ __device__ __forceinline__ void bin_hist(const uint32_t* __restrict__ sorted_ids
                                          const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis, int tiles_x,
                                          const PassArgs& pa, uint32_t* __restrict__ hist, uint32_t nbb,
                                          uint2* __restrict__ trect_sorted, uint32_t blk, uint32_t* h,
-                                         uint32_t* own) {
+                                         uint32_t* own, const InstKey& ik) {
     const Digit dg = digit_params(pa);
     const uint32_t radix = dg.mask + 1u;
     for (uint32_t d = threadIdx.x; d < radix; d += kThreads) h[d] = 0u;
     const uint32_t base = blk * kBinBlock + threadIdx.x;
     uint2 tr[kBinItems];
+    uint32_t bk[kBinItems];
     uint32_t nmax = 0;
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
         const uint32_t r = base + k * kThreads;
         tr[k] = r < n_vis ? sorted_rect<kPacked>(sorted_ids, trect, rect4_sorted, n_vis, r, trect_sorted)
                           : make_uint2(0xffffu, 0u);
+        bk[k] = ik.cb && rect_tiles(tr[k]) ? ik.bucket(r) : 0u;
         nmax = max(nmax, rect_tiles(tr[k]));
     }
     uint32_t* own_o = own;
@@ -353,7 +388,7 @@ __device__ __forceinline__ void bin_hist(const uint32_t* __restrict__ sorted_ids
             const uint32_t tx0 = tr[k].x & 0xffffu, tx1 = tr[k].x >> 16, ty0 = tr[k].y & 0xffffu, ty1 = tr[k].y >> 16;
             if (tx0 > tx1) continue;
             for (uint32_t ty = ty0; ty <= ty1; ++ty)
-                for (uint32_t tx = tx0; tx <= tx1; ++tx) atomicAdd(&h[dg.of(ty * (uint32_t)tiles_x + tx)], 1u);
+                for (uint32_t tx = tx0; tx <= tx1; ++tx) atomicAdd(&h[dg.of(ik.of(ty * (uint32_t)tiles_x + tx, bk[k]))], 1u);
         }
     } else {
         // thread t's instances in the consecutive layout: splats blk * kBinBlock + 4t .. 4t + 3
@@ -369,7 +404,7 @@ __device__ __forceinline__ void bin_hist(const uint32_t* __restrict__ sorted_ids
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < total; i += kThreads) {
             uint32_t key, val;
-            instance_at<kPacked>(i, own_o, blk, sorted_ids, trect_sorted, rect4_sorted, tiles_x, key, val);
+            instance_at<kPacked>(i, own_o, blk, sorted_ids, trect_sorted, rect4_sorted, tiles_x, key, val, false, ik);
             atomicAdd(&h[dg.of(key)], 1u);
         }
     }
@@ -382,11 +417,13 @@ __global__ __launch_bounds__(kThreads) void k_bin_hist(const uint32_t* __restric
                                                        const uint2* __restrict__ trect,
                                                        const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
                                                        int tiles_x, PassArgs pa, uint32_t* __restrict__ hist,
-                                                       uint32_t nbb, uint2* __restrict__ trect_sorted) {
+                                                       uint32_t nbb, uint2* __restrict__ trect_sorted, uint32_t cb,
+                                                       const uint32_t* __restrict__ key_range,
+                                                       const uint32_t* __restrict__ slot_keys) {
     __shared__ uint32_t h[1 << kCB];
     __shared__ uint32_t own[kThreads + 1 + 2 * kThreads / 64];
     bin_hist<kPacked, kCB>(sorted_ids, trect, rect4_sorted, n_vis, tiles_x, pa, hist, nbb, trect_sorted, blockIdx.x,
-                           h, own);
+                           h, own, inst_key(cb, key_range, slot_keys));
 }
 
 // kKeys: each instance also carries its splat's depth key (sorted_keys, by
@@ -403,7 +440,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
                                             uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ tile_vals,
                                             uint32_t blk, BinScatterLds<kCB>& L,
                                             const uint32_t* __restrict__ sorted_keys = nullptr,
-                                            uint32_t* __restrict__ inst_keys = nullptr) {
+                                            uint32_t* __restrict__ inst_keys = nullptr, const InstKey& ik = InstKey{}) {
     constexpr int kCap = 1 << kCB;
     constexpr int kDpt = kCap / kThreads > 0 ? kCap / kThreads : 1;  // digits per thread
     constexpr int kWaveItems = kBinStage / (kThreads / 64);           // window items per wave
@@ -424,7 +461,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
     }
     // this thread's 4 consecutive depth-sorted splats
     const uint32_t base = blk * kBinBlock + threadIdx.x * kBinItems;
-    uint32_t id[kBinItems];
+    uint32_t id[kBinItems], bk[kBinItems];
     uint2 tr[kBinItems];
     uint32_t s = 0;
 #pragma unroll
@@ -435,6 +472,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
             tr[k] = r < n_vis ? unpack_rect(rect4_sorted[r]) : make_uint2(0xffffu, 0u);
         else
             tr[k] = r < n_vis ? trect_sorted[r] : make_uint2(0xffffu, 0u);
+        bk[k] = ik.cb && rect_tiles(tr[k]) ? ik.bucket(r) : 0u;
         s += rect_tiles(tr[k]);
     }
     {  // global start of each digit's run of this block: digit base + the earlier blocks' counts
@@ -467,7 +505,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
             const uint32_t cnt = min((uint32_t)kBinStage, total - c0);
             for (uint32_t j = threadIdx.x; j < cnt; j += kThreads)
                 instance_at<kPacked>(c0 + j, L.own_o, blk, sorted_ids, trect_sorted, rect4_sorted, tiles_x, L.k[j],
-                                     L.v[j], kKeys);
+                                     L.v[j], kKeys, ik);
         } else if (o < c0 + (uint32_t)kBinStage && o + s > c0) {
             uint32_t idx = o;
 #pragma unroll
@@ -478,7 +516,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
                 for (uint32_t ty = ty0; ty <= ty1; ++ty)
                     for (uint32_t tx = tx0; tx <= tx1; ++tx, ++idx)
                         if (idx >= c0 && idx < c0 + (uint32_t)kBinStage) {
-                            L.k[idx - c0] = ty * (uint32_t)tiles_x + tx;
+                            L.k[idx - c0] = ik.of(ty * (uint32_t)tiles_x + tx, bk[k]);
                             L.v[idx - c0] = id[k];
                         }
             }
@@ -585,10 +623,12 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(const uint32_t* __rest
                                                           uint32_t* __restrict__ tile_keys,
                                                           uint32_t* __restrict__ tile_vals,
                                                           const uint32_t* __restrict__ sorted_keys,
-                                                          uint32_t* __restrict__ inst_keys) {
+                                                          uint32_t* __restrict__ inst_keys, uint32_t cb,
+                                                          const uint32_t* __restrict__ key_range) {
     __shared__ BinScatterLds<kCB> L;
     bin_scatter<kPacked, kCB, kKeys>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tiles_x, pa, hist_off, totals,
-                                     nbb, tile_keys, tile_vals, blockIdx.x, L, sorted_keys, inst_keys);
+                                     nbb, tile_keys, tile_vals, blockIdx.x, L, sorted_keys, inst_keys,
+                                     inst_key(cb, key_range, sorted_keys));
 }
 
 // Views of a group (blockIdx.y = view): hist / totals per view.
@@ -596,6 +636,8 @@ struct BinSortViews {
     BinView v[kMaxViews];
     uint32_t* hist[kMaxViews];
     const uint32_t* totals[kMaxViews];
+    const uint32_t* key_range[kMaxViews];  // (coarse depth bits: each view's frame key range)
+    uint32_t cb;
 };
 
 // Every view's count matrix has nbb (the largest view's blocks) columns; a
@@ -607,7 +649,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_hist_views(BinSortViews vs, in
     __shared__ uint32_t own[kThreads + 1 + 2 * kThreads / 64];
     const BinView& v = vs.v[blockIdx.y];
     bin_hist<kPacked, kCB>(v.sorted_ids, v.trect, v.rect4_sorted, v.n_vis, tiles_x, pa, vs.hist[blockIdx.y], nbb,
-                           v.trect_sorted, blockIdx.x, h, own);
+                           v.trect_sorted, blockIdx.x, h, own, inst_key(vs.cb, vs.key_range[blockIdx.y], v.slot_keys));
 }
 
 template <bool kPacked, int kCB, bool kKeys>
@@ -618,7 +660,8 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter_views(BinSortViews vs,
     if (blockIdx.x * kBinBlock >= v.n_vis) return;
     bin_scatter<kPacked, kCB, kKeys>(v.sorted_ids, v.trect_sorted, v.rect4_sorted, v.n_vis, tiles_x, pa,
                                      vs.hist[blockIdx.y], vs.totals[blockIdx.y], nbb, v.tile_keys, v.tile_vals,
-                                     blockIdx.x, L, v.slot_keys, v.inst_keys);
+                                     blockIdx.x, L, v.slot_keys, v.inst_keys,
+                                     inst_key(vs.cb, vs.key_range[blockIdx.y], v.slot_keys));
 }
 
 // Tile ranges from the tile-sorted keys: kRangeItems consecutive instances per
@@ -628,12 +671,18 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter_views(BinSortViews vs,
 // compositors for CU slots.)
 constexpr int kRangeItems = 16;
 
-template <int kItems = kRangeItems>
+// (keys >> cb: the tile id of a key with coarse depth bits, InstKey.)
+// kRuns (the per-tile depth sort): every run of equal full keys longer than
+// kTdsCapWave is appended to big_runs as (start, length): the thread holding
+// its last instance finds its start by binary search (the keys ascend) and
+// takes a slot with one atomic add (a few hundred runs per frame at C2).
+template <bool kRuns, int kItems = kRangeItems>
 __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, uint32_t n, uint2* __restrict__ ranges,
-                                            uint32_t t) {
+                                            uint32_t t, uint32_t cb, uint2* __restrict__ big_runs,
+                                            uint32_t* __restrict__ big_count) {
     const uint32_t base = t * kItems;
     if (base >= n) return;
-    uint32_t k[kItems];
+    uint32_t k[kItems];  // full keys
     if (base + kItems <= n) {
         const uint4* p = reinterpret_cast<const uint4*>(keys + base);  // (base: a multiple of 16)
 #pragma unroll
@@ -653,25 +702,45 @@ __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, u
         if (i >= n) break;
         const uint32_t before = j == 0 ? prev : k[j - 1];
         const uint32_t after = (j + 1 < kItems) ? (i + 1 < n ? k[j + 1] : 0xffffffffu) : next;
-        if (i == 0 || before != k[j]) ranges[k[j]].x = i;
-        if (i == n - 1 || after != k[j]) ranges[k[j]].y = i + 1;
+        const uint32_t tile = k[j] >> cb;
+        if (i == 0 || (before >> cb) != tile) ranges[tile].x = i;
+        if (i == n - 1 || (after >> cb) != tile) ranges[tile].y = i + 1;
+        if constexpr (kRuns) {
+            if ((i == n - 1 || after != k[j]) && i >= kTdsCapWave && keys[i - kTdsCapWave] == k[j]) {
+                uint32_t lo = 0, hi = i - kTdsCapWave;  // keys[hi] == k[j]: the run's start is in [0, hi]
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (keys[mid] < k[j]) lo = mid + 1;
+                    else hi = mid;
+                }
+                const uint32_t slot = atomicAdd(big_count, 1u);
+                big_runs[slot] = make_uint2(lo, i + 1 - lo);
+            }
+        }
     }
 }
 
+template <bool kRuns>
 __global__ __launch_bounds__(kThreads) void k_tile_ranges(const uint32_t* __restrict__ keys, uint32_t n,
-                                                          uint2* __restrict__ ranges) {
-    tile_ranges(keys, n, ranges, blockIdx.x * kThreads + threadIdx.x);
+                                                          uint2* __restrict__ ranges, uint32_t cb,
+                                                          uint2* __restrict__ big_runs, uint32_t* __restrict__ big_count) {
+    tile_ranges<kRuns>(keys, n, ranges, blockIdx.x * kThreads + threadIdx.x, cb, big_runs, big_count);
 }
 
 struct RangeViews {
     const uint32_t* keys[kMaxViews];
     uint2* ranges[kMaxViews];
     uint32_t n[kMaxViews];
+    uint2* big_runs[kMaxViews];
+    uint32_t* big_count[kMaxViews];
+    uint32_t cb;
 };
 
+template <bool kRuns>
 __global__ __launch_bounds__(kThreads) void k_tile_ranges_views(RangeViews vs) {
     const int v = blockIdx.y;
-    tile_ranges(vs.keys[v], vs.n[v], vs.ranges[v], blockIdx.x * kThreads + threadIdx.x);
+    tile_ranges<kRuns>(vs.keys[v], vs.n[v], vs.ranges[v], blockIdx.x * kThreads + threadIdx.x, vs.cb,
+                       vs.big_runs[v], vs.big_count[v]);
 }
 
 struct CompositeArgs {
@@ -766,13 +835,6 @@ __device__ __forceinline__ uint32_t first_class_of(uint2 r, uint32_t chunk, uint
     return first_major && (r.y - r.x) >= chunk ? 0u : partial_class_of(r, chunk, classes);
 }
 
-// Rows of the per-block totals (tot[row * blocks + block]): 0 the extra
-// chunks, 1 the full chunks, 1 + k (k < classes) the partial chunks of length
-// class k, then the per-tile depth sort's tiles of class c (tds_class_of) at
-// row 1 + classes + c.
-__device__ __forceinline__ uint32_t tds_row(uint32_t classes, uint32_t c) { return 1u + classes + c; }
-constexpr int kChunkRows = 1 + kMaxLenClasses + kTdsClasses;
-
 __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
                                             uint32_t classes, bool first_major, uint32_t* __restrict__ tot,
                                             uint32_t (*lds)[kThreads / 64]) {
@@ -782,7 +844,6 @@ __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, in
     const uint32_t e = wave_reduce_sum(valid ? chunks_of(r, chunk) - 1u : 0u);
     const uint32_t f = wave_reduce_sum(first_full_of(r, chunk, first_major));
     const uint32_t pc = valid ? first_class_of(r, chunk, classes, first_major) : 0u;
-    const uint32_t tc = tds_class_of(r.y - r.x);
     const int w = threadIdx.x >> 6;
     if (__lane_id() == 0) {
         lds[0][w] = e;
@@ -792,12 +853,8 @@ __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, in
         const uint32_t n = (uint32_t)__popcll(__ballot(pc == k));
         if (__lane_id() == 0) lds[1 + k][w] = n;
     }
-    for (uint32_t c = 0; c < (uint32_t)kTdsClasses; ++c) {
-        const uint32_t n = (uint32_t)__popcll(__ballot(tc == c));
-        if (__lane_id() == 0) lds[tds_row(classes, c)][w] = n;
-    }
     __syncthreads();
-    if (threadIdx.x < tds_row(classes, kTdsClasses))
+    if (threadIdx.x <= classes)
         tot[threadIdx.x * gridDim.x + blockIdx.x] =
             lds[threadIdx.x][0] + lds[threadIdx.x][1] + lds[threadIdx.x][2] + lds[threadIdx.x][3];
 }
@@ -805,7 +862,7 @@ __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, in
 __global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restrict__ ranges, int num_tiles,
                                                           uint32_t chunk, uint32_t classes,
                                                           uint32_t* __restrict__ tot, uint32_t first_major) {
-    __shared__ uint32_t lds[kChunkRows][kThreads / 64];
+    __shared__ uint32_t lds[1 + kMaxLenClasses][kThreads / 64];
     chunk_count(ranges, num_tiles, chunk, classes, first_major != 0, tot, lds);
 }
 
@@ -814,8 +871,6 @@ struct ChunkWriteLds {
     uint32_t cls[kMaxLenClasses][kThreads / 64];  // partials of class k per wave
     uint32_t pre[1 + kMaxLenClasses];             // sums over the earlier blocks
     uint32_t base[kMaxLenClasses];                // first dispatch position of each class
-    uint32_t tcls[kTdsClasses][kThreads / 64];    // per-tile depth sort: tiles of class c per wave
-    uint32_t tpos[kTdsClasses];                   // ... the block's first work-list position of class c
 };
 
 __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
@@ -823,39 +878,11 @@ __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, in
                                             uint32_t* __restrict__ chunk_cnt, uint32_t* __restrict__ chunk_base,
                                             uint32_t* __restrict__ n_extra_dev, uint4* __restrict__ desc,
                                             uint32_t* __restrict__ order, float4* __restrict__ tmax,
-                                            uint32_t* __restrict__ tds_list, ChunkWriteLds& sh) {
+                                            ChunkWriteLds& sh) {
     const int t = blockIdx.x * kThreads + threadIdx.x;
     const int w = threadIdx.x >> 6;
-    uint32_t* cls_tot = const_cast<uint32_t*>(tot) + tds_row(classes, kTdsClasses) * gridDim.x;
-    if (tds_list && w == 1) {  // wave 1: the depth sort's work list positions of this block's classes
-        uint32_t ps[kTdsClasses], as[kTdsClasses];
-#pragma unroll
-        for (int c = 0; c < kTdsClasses; ++c) ps[c] = as[c] = 0u;
-        for (uint32_t b = __lane_id(); b < gridDim.x; b += 64) {
-            uint32_t v[kTdsClasses];
-#pragma unroll
-            for (int c = 0; c < kTdsClasses; ++c) v[c] = tot[tds_row(classes, c) * gridDim.x + b];
-#pragma unroll
-            for (int c = 0; c < kTdsClasses; ++c) {
-                ps[c] += b < blockIdx.x ? v[c] : 0u;
-                as[c] += v[c];
-            }
-        }
-        uint32_t run = 0, n_wg = 0;
-#pragma unroll
-        for (int c = 0; c < kTdsClasses; ++c) {
-            const uint32_t p = wave_reduce_sum(ps[c]);
-            const uint32_t a = wave_reduce_sum(as[c]);
-            if (__lane_id() == 0) sh.tpos[c] = run + p;
-            run += a;
-            if (c + 1 == kTdsBlockClasses) n_wg = run;
-        }
-        if (blockIdx.x == 0 && __lane_id() == 0) {  // (tds_counts)
-            cls_tot[classes + 1] = n_wg;
-            cls_tot[classes + 2] = run - n_wg;
-        }
-    }
     if (w == 0) {  // wave 0: offsets of this block = sums of the earlier blocks' totals
+        uint32_t* cls_tot = const_cast<uint32_t*>(tot) + (1 + classes) * gridDim.x;
         // every row's loads issued before any is summed: one memory round trip,
         // not one per class (a row-by-row loop waited 1 + classes times)
         uint32_t ps[1 + kMaxLenClasses], as[1 + kMaxLenClasses];
@@ -900,23 +927,9 @@ __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, in
         if (pc == k) rank = (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
         if (__lane_id() == 0) sh.cls[k][w] = (uint32_t)__popcll(m);
     }
-    const uint32_t tc = tds_class_of(r.y - r.x);
-    uint32_t trank = 0;  // among this wave's tiles of depth-sort class tc
-    if (tds_list) {
-        for (uint32_t c = 0; c < (uint32_t)kTdsClasses; ++c) {
-            const uint64_t m = __ballot(tc == c);
-            if (tc == c) trank = (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull));
-            if (__lane_id() == 0) sh.tcls[c][w] = (uint32_t)__popcll(m);
-        }
-    }
     const uint32_t mine = valid ? cnt - 1u : 0u;
     uint32_t total, total_f;
     const uint32_t excl = block_exclusive<kThreads>(mine, sh.scan[0], total);  // (its barrier also publishes sh)
-    if (tds_list && tc < (uint32_t)kTdsClasses) {
-        uint32_t pos = sh.tpos[tc] + trank;
-        for (int i = 0; i < w; ++i) pos += sh.tcls[tc][i];
-        tds_list[pos] = (uint32_t)t;
-    }
     const uint32_t excl_f = block_exclusive<kThreads>(full, sh.scan[1], total_f);
     const uint32_t extra = sh.pre[0] + excl;
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_extra_dev = sh.pre[0] + total;
@@ -968,11 +981,10 @@ __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restric
                                                           uint32_t* __restrict__ chunk_base,
                                                           uint32_t* __restrict__ n_extra_dev,
                                                           uint4* __restrict__ desc, uint32_t* __restrict__ order,
-                                                          float4* __restrict__ tmax, uint32_t first_major,
-                                                          uint32_t* __restrict__ tds_list) {
+                                                          float4* __restrict__ tmax, uint32_t first_major) {
     __shared__ ChunkWriteLds sh;
     chunk_write(ranges, num_tiles, chunk, classes, first_major != 0, tot, chunk_cnt, chunk_base, n_extra_dev, desc,
-                order, tmax, tds_list, sh);
+                order, tmax, sh);
 }
 
 struct ChunkView {
@@ -983,7 +995,6 @@ struct ChunkView {
     uint4* desc;
     uint32_t* order;
     float4* tmax;
-    uint32_t* tds_list;
 };
 struct ChunkViews {
     ChunkView v[kMaxViews];
@@ -991,7 +1002,7 @@ struct ChunkViews {
 
 __global__ __launch_bounds__(kThreads) void k_chunk_count_views(ChunkViews vs, int num_tiles, uint32_t chunk,
                                                                 uint32_t classes, uint32_t first_major) {
-    __shared__ uint32_t lds[kChunkRows][kThreads / 64];
+    __shared__ uint32_t lds[1 + kMaxLenClasses][kThreads / 64];
     const ChunkView& v = vs.v[blockIdx.y];
     chunk_count(v.ranges, num_tiles, chunk, classes, first_major != 0, v.chunk_cnt + num_tiles, lds);
 }
@@ -1001,7 +1012,7 @@ __global__ __launch_bounds__(kThreads) void k_chunk_write_views(ChunkViews vs, i
     __shared__ ChunkWriteLds sh;
     const ChunkView& v = vs.v[blockIdx.y];
     chunk_write(v.ranges, num_tiles, chunk, classes, first_major != 0, v.chunk_cnt + num_tiles, v.chunk_cnt,
-                v.chunk_base, v.n_extra_dev, v.desc, v.order, v.tmax, v.tds_list, sh);
+                v.chunk_base, v.n_extra_dev, v.desc, v.order, v.tmax, sh);
 }
 
 // Bits [lo, hi] of a 16-bit mask, clamped to [0, 15]; 0 if the range is empty.
@@ -2040,7 +2051,10 @@ size_t bin_hist_elems(size_t n_vis, int tbits, int passes) {
 
 // The binning's digit parameters (tile sort pass 0) and its blocks.
 static int bin_pass0(const BinSortArgs& a, PassArgs& pa, int& w, bool scatter) {
-    const int tb = a.tbits > 0 ? a.tbits : 1;  // one tile: a single digit value, generation order kept
+    // (one tile: a single digit value, generation order kept)
+    const int tb = (a.tbits > 0 ? a.tbits : 1) + (int)a.coarse_bits;
+    if (a.coarse_bits && (!a.key_range || !a.slot_keys || a.sorted_ids))
+        return set_error(GSR_ERR_INVALID, "binning: coarse depth bits need slot order, the slot keys and the key range");
     const int ps = a.passes > 0 ? a.passes : 1;
     w = (tb + ps - 1) / ps;
     if (w > 11) return set_error(GSR_ERR_INVALID, "binning: tile digit wider than 11 bits");
@@ -2061,7 +2075,7 @@ int launch_binning_hist(const BinSortArgs& a, hipStream_t s) {
     uint2* tsorted = a.sorted_ids ? a.trect_sorted : const_cast<uint2*>(a.trect);
 #define GSR_BIN_HIST(P, CB)                                                                                  \
     k_bin_hist<P, CB><<<nbb, kThreads, 0, s>>>(a.sorted_ids, a.trect, a.rect4_sorted, a.n_vis, a.tiles_x, pa, \
-                                               a.hist, nbb, tsorted)
+                                               a.hist, nbb, tsorted, a.coarse_bits, a.key_range, a.slot_keys)
     if (w <= 8) {
         if (packed) GSR_BIN_HIST(true, 8); else GSR_BIN_HIST(false, 8);
     } else {
@@ -2085,11 +2099,12 @@ int launch_binning_scatter(const BinSortArgs& a, hipStream_t s) {
         if (a.inst_keys)                                                                                            \
             k_bin_scatter<P, CB, true><<<nbb, kThreads, 0, s>>>(a.sorted_ids, tsorted, a.rect4_sorted, a.n_vis,     \
                                                                 a.tiles_x, pa, a.hist, a.totals, nbb, a.tile_keys,  \
-                                                                a.tile_vals, a.slot_keys, a.inst_keys);             \
+                                                                a.tile_vals, a.slot_keys, a.inst_keys,              \
+                                                                a.coarse_bits, a.key_range);                        \
         else                                                                                                        \
             k_bin_scatter<P, CB, false><<<nbb, kThreads, 0, s>>>(a.sorted_ids, tsorted, a.rect4_sorted, a.n_vis,    \
                                                                  a.tiles_x, pa, a.hist, a.totals, nbb, a.tile_keys, \
-                                                                 a.tile_vals, nullptr, nullptr);                    \
+                                                                 a.tile_vals, nullptr, nullptr, 0u, nullptr);       \
     } while (0)
     if (w <= 8) {
         if (packed) GSR_BIN_SCATTER(true, 8); else GSR_BIN_SCATTER(false, 8);
@@ -2101,10 +2116,17 @@ int launch_binning_scatter(const BinSortArgs& a, hipStream_t s) {
     return GSR_OK;
 }
 
-int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, hipStream_t s) {
+int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, hipStream_t s, uint32_t cb,
+                       uint2* big_runs, uint32_t* big_count) {
     if (n_dup == 0) return GSR_OK;
+    if (big_runs && !big_count) return set_error(GSR_ERR_INVALID, "tile ranges: long runs need their counter");
     const uint32_t per_block = kThreads * kRangeItems;
-    k_tile_ranges<<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges);
+    if (big_runs)
+        k_tile_ranges<true><<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, cb,
+                                                                                   big_runs, big_count);
+    else
+        k_tile_ranges<false><<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, cb,
+                                                                                    nullptr, nullptr);
     GSR_LAUNCH_CHECK("tile_ranges");
     return GSR_OK;
 }
@@ -2136,22 +2158,17 @@ static CompositeArgs make_args(const FrameUniforms& u, float t_min, const float*
 }
 
 size_t chunk_cnt_elems(int num_tiles) {
-    return (size_t)num_tiles + kChunkRows * ((size_t)num_tiles / kThreads + 1) + kMaxLenClasses + 3;
+    return (size_t)num_tiles + (1 + kMaxLenClasses) * ((size_t)num_tiles / kThreads + 1) + kMaxLenClasses + 1;
 }
 
-// after the block totals: the chunks per class (classes + 1 words), then the depth sort's two counts
 const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes) {
     const size_t g = ((size_t)num_tiles + kThreads - 1) / kThreads;
-    return chunk_cnt + num_tiles + (1 + classes + kTdsClasses) * g;
-}
-
-const uint32_t* tds_counts(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes) {
-    return chunk_class_totals(chunk_cnt, num_tiles, classes) + classes + 1;
+    return chunk_cnt + num_tiles + (1 + classes) * g;
 }
 
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
-                  hipStream_t s, bool first_major, uint32_t* tds_list) {
+                  hipStream_t s, bool first_major) {
 #ifndef GSR_COMP_BOUND
     tmax = nullptr;  // the published maxima are only read by the bound variant
 #endif
@@ -2162,7 +2179,7 @@ int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t c
     k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot, first_major ? 1u : 0u);
     GSR_LAUNCH_CHECK("chunk_count");
     k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot, chunk_cnt, chunk_base, n_extra_dev,
-                                         desc, order, tmax, first_major ? 1u : 0u, tds_list);
+                                         desc, order, tmax, first_major ? 1u : 0u);
     GSR_LAUNCH_CHECK("chunk_write");
     return GSR_OK;
 }
@@ -2258,8 +2275,10 @@ int launch_binning_views(FinishView* views, int k, int tiles_x, uint32_t stage_l
 
 // A group's fused binning (views of one frame size), in the same two halves.
 static int bin_views_args(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tbits,
-                          int passes, BinSortViews& bv, uint32_t& nbb, PassArgs& pa, int& w, bool scatter) {
+                          int passes, BinSortViews& bv, uint32_t& nbb, PassArgs& pa, int& w, bool scatter,
+                          uint32_t coarse_bits, const uint32_t* const* key_range) {
     bv = BinSortViews{};
+    bv.cb = coarse_bits;
     nbb = 0;
     for (int i = 0; i < k; ++i) {
         const FinishView& f = views[i];
@@ -2269,6 +2288,9 @@ static int bin_views_args(FinishView* views, uint32_t* const* hist, uint32_t* co
                           f.n_vis, f.slot_keys, f.inst_keys};
         bv.hist[i] = hist[i];
         bv.totals[i] = totals[i];
+        bv.key_range[i] = key_range ? key_range[i] : nullptr;
+        if (coarse_bits && (!bv.key_range[i] || !f.slot_keys || f.sorted_ids))
+            return set_error(GSR_ERR_INVALID, "binning: coarse depth bits need slot order, the slot keys and the key range");
         if ((f.rect4_sorted != nullptr) != (views[0].rect4_sorted != nullptr) ||
             (scatter && (f.inst_keys != nullptr) != (views[0].inst_keys != nullptr)))
             return set_error(GSR_ERR_INVALID, "binning: packed rectangles or carried keys on some views only");
@@ -2276,7 +2298,7 @@ static int bin_views_args(FinishView* views, uint32_t* const* hist, uint32_t* co
             return set_error(GSR_ERR_INVALID, "binning: slot order takes the plain rects and carries the keys");
         nbb = std::max(nbb, (f.n_vis + kBinBlock - 1) / kBinBlock);
     }
-    const int tb = tbits > 0 ? tbits : 1;
+    const int tb = (tbits > 0 ? tbits : 1) + (int)coarse_bits;
     const int ps = passes > 0 ? passes : 1;
     w = (tb + ps - 1) / ps;
     if (w > 11) return set_error(GSR_ERR_INVALID, "binning: tile digit wider than 11 bits");
@@ -2285,12 +2307,14 @@ static int bin_views_args(FinishView* views, uint32_t* const* hist, uint32_t* co
 }
 
 int launch_binning_hist_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
-                              int tbits, int passes, hipStream_t s) {
+                              int tbits, int passes, hipStream_t s, uint32_t coarse_bits,
+                              const uint32_t* const* key_range) {
     BinSortViews bv;
     uint32_t nbb;
     PassArgs pa;
     int w, rc;
-    if ((rc = bin_views_args(views, hist, totals, k, tbits, passes, bv, nbb, pa, w, false))) return rc;
+    if ((rc = bin_views_args(views, hist, totals, k, tbits, passes, bv, nbb, pa, w, false, coarse_bits, key_range)))
+        return rc;
     if (nbb == 0) return GSR_OK;
     const bool packed = views[0].rect4_sorted != nullptr;
     const dim3 grid(nbb, (unsigned)k);
@@ -2306,12 +2330,14 @@ int launch_binning_hist_views(FinishView* views, uint32_t* const* hist, uint32_t
 }
 
 int launch_binning_scatter_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k,
-                                 int tiles_x, int tbits, int passes, hipStream_t s) {
+                                 int tiles_x, int tbits, int passes, hipStream_t s, uint32_t coarse_bits,
+                                 const uint32_t* const* key_range) {
     BinSortViews bv;
     uint32_t nbb;
     PassArgs pa;
     int w, rc;
-    if ((rc = bin_views_args(views, hist, totals, k, tbits, passes, bv, nbb, pa, w, true))) return rc;
+    if ((rc = bin_views_args(views, hist, totals, k, tbits, passes, bv, nbb, pa, w, true, coarse_bits, key_range)))
+        return rc;
     if (nbb == 0) return GSR_OK;
     const bool packed = views[0].rect4_sorted != nullptr;
     const bool keys = views[0].inst_keys != nullptr;
@@ -2331,18 +2357,27 @@ int launch_binning_scatter_views(FinishView* views, uint32_t* const* hist, uint3
     return GSR_OK;
 }
 
-int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s) {
+int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s, uint32_t cb) {
     RangeViews rv{};
+    rv.cb = cb;
     uint32_t n_max = 0;
+    const bool runs = views[0].big_runs != nullptr;
     for (int i = 0; i < k; ++i) {
         rv.keys[i] = views[i].tile_keys;
         rv.ranges[i] = views[i].ranges;
         rv.n[i] = views[i].n_dup;
+        rv.big_runs[i] = views[i].big_runs;
+        rv.big_count[i] = views[i].big_count;
+        if ((views[i].big_runs != nullptr) != runs || (runs && !views[i].big_count))
+            return set_error(GSR_ERR_INVALID, "tile ranges: long runs on some views only");
         n_max = std::max(n_max, views[i].n_dup);
     }
     if (n_max == 0) return GSR_OK;
     const uint32_t per_block = kThreads * kRangeItems;
-    k_tile_ranges_views<<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
+    if (runs)
+        k_tile_ranges_views<true><<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
+    else
+        k_tile_ranges_views<false><<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
     GSR_LAUNCH_CHECK("tile_ranges_views");
     return GSR_OK;
 }
@@ -2358,7 +2393,7 @@ int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk,
 #else
         float4* tmax = nullptr;  // the published maxima are only read by the bound variant
 #endif
-        cv.v[i] = ChunkView{f.ranges, f.chunk_cnt, f.chunk_base, f.n_extra_dev, f.desc, f.order, tmax, f.tds_list};
+        cv.v[i] = ChunkView{f.ranges, f.chunk_cnt, f.chunk_base, f.n_extra_dev, f.desc, f.order, tmax};
     }
     const dim3 grid((unsigned)((num_tiles + kThreads - 1) / kThreads), (unsigned)k);
     k_chunk_count_views<<<grid, kThreads, 0, s>>>(cv, num_tiles, chunk, classes, first_major ? 1u : 0u);

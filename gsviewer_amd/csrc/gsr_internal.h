@@ -412,7 +412,11 @@ uint32_t clamp_stage_limit(long v);
 int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted, uint32_t n_vis,
                    int tiles_x, uint32_t* tmp, uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals,
                    uint32_t stage_limit, hipStream_t s);
-int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, hipStream_t s);
+// cb: the keys' coarse depth bits (InstKey; the tile id is key >> cb).  big_runs
+// (nullable): every run of equal keys longer than kTdsCapWave is appended as
+// (start, length), *big_count (zeroed per frame) counting them, for the per-tile depth sort.
+int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, hipStream_t s, uint32_t cb = 0,
+                       uint2* big_runs = nullptr, uint32_t* big_count = nullptr);
 // The binning with the tile sort's first radix pass fused in (composite.hip,
 // k_bin_hist / k_bin_scatter): the instances end in (tile_keys, tile_vals)
 // ordered by digit 0 of the tile sort (tbits bits in `passes` passes); the
@@ -438,56 +442,48 @@ struct BinSortArgs {
     uint32_t* tile_vals;
     const uint32_t* slot_keys = nullptr;
     uint32_t* inst_keys = nullptr;
+    // coarse depth bits of the instance keys (slot order only): (tile << coarse_bits) | bucket of the
+    // splat's key in the frame's key_range (device {~kmin, kmax}); the digits span tbits + coarse_bits
+    uint32_t coarse_bits = 0;
+    const uint32_t* key_range = nullptr;
 };
 int launch_binning_hist(const BinSortArgs& a, hipStream_t s);
 int launch_binning_scatter(const BinSortArgs& a, hipStream_t s);
-// tile_sort.hip: the per-tile depth sort (see there).  Lists of 2 ..
-// kTdsCapWave instances take one wave, up to kTdsCapBlock one workgroup in
-// registers, longer ones one workgroup through global scratch.
+// tile_sort.hip: the per-tile depth sort (see there).  The tile-sorted
+// instances come in runs of equal (tile, coarse depth bucket) (InstKey,
+// composite.hip), each in slot order; every run is put in (depth key, slot)
+// order in place.  A block takes the runs that start in its kTdsSpan
+// instances: runs of 2 .. kTdsCapWave one wave each, up to kTdsCapBlock the
+// block in registers, longer ones the block through global scratch.
 constexpr uint32_t kTdsCapWave = 1024;
 constexpr uint32_t kTdsCapBlock = 24576;
-// Work-list length classes, longest first: 0 (> kTdsCapBlock), 1 (> 8192),
-// 2 (> 2048), 3 (> kTdsCapWave) take a workgroup each; 4 (> 256), 5 (> 64),
-// 6 (>= 2) a wave each; kTdsClasses: nothing to sort.
-constexpr int kTdsClasses = 7;
-constexpr int kTdsBlockClasses = 4;
-__host__ __device__ constexpr uint32_t tds_class_of(uint32_t len) {
-    return len > kTdsCapBlock ? 0u
-           : len > 8192u      ? 1u
-           : len > 2048u      ? 2u
-           : len > kTdsCapWave ? 3u
-           : len > 256u       ? 4u
-           : len > 64u        ? 5u
-           : len >= 2u        ? 6u
-                              : (uint32_t)kTdsClasses;
-}
+constexpr uint32_t kTdsSpan = 8192;
 struct TileSortView {
-    const uint2* ranges;
-    const uint32_t* list;    // the work list (launch_chunks' tds_list)
-    const uint32_t* counts;  // {workgroup-class tiles, wave-class tiles} (tds_counts)
-    uint32_t* keys;          // each list position's depth key (the tile sort's payload); permuted
-    uint32_t* vals;          // the tile lists (slots): sorted in place
-    uint32_t* keys_alt;      // n_dup words each of scratch (the tile sort's alternate buffers)
+    const uint32_t* tile_keys;  // the tile sort's keys ((tile << cb) | bucket): runs are their equal stretches
+    uint32_t* keys;             // each list position's depth key (the tile sort's payload); permuted
+    uint32_t* vals;             // the tile lists (slots): sorted in place
+    uint32_t* keys_alt;         // n_dup words each of scratch (the tile sort's alternate buffers)
     uint32_t* vals_alt;
     uint32_t n_dup;
+    const uint2* big_runs;      // the runs of > kTdsCapWave instances (k_tile_ranges), in no order
+    const uint32_t* big_count;
 };
 // debug (GSR_DEBUG_TDS, timing experiments only; 0 in production): 1 skips the
-// workgroup-class lists, 2 the wave-class lists, 4 sorts one digit pass only
-int launch_tile_depth_sort(const TileSortView* views, int k, int num_tiles, hipStream_t s, uint32_t debug = 0);
+// runs a block sorts, 2 the runs waves sort, 4 sorts one digit pass only;
+// stamps (8: the knob's stamp buffer): per block of view 0, 8 words of clock
+// stamps (start, after the long runs, after finding its runs, end) and counts
+int launch_tile_depth_sort(const TileSortView* views, int k, hipStream_t s, uint32_t debug = 0,
+                           uint64_t* stamps = nullptr);
 
 // chunk_cnt must hold chunk_cnt_elems(num_tiles) entries (block totals after the tiles);
 // order: one entry per chunk (dispatch position -> chunk slot)
 size_t chunk_cnt_elems(int num_tiles);
-// the per-tile depth sort's work-list counts, written by launch_chunks (2 words in chunk_cnt)
-const uint32_t* tds_counts(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes);
 // classes (2 .. kMaxLenClasses): dispatch order = full chunks, then the partial
 // ones in classes - 1 length classes, longest first; the frame's chunk count
 // of each class lands at chunk_class_totals(chunk_cnt, num_tiles, classes)
-// tds_list (nullable, num_tiles words): the per-tile depth sort's work list, the
-// tiles with >= 2 instances by tds_class_of, class-major, tile order within a class
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
-                  hipStream_t s, bool first_major = false, uint32_t* tds_list = nullptr);
+                  hipStream_t s, bool first_major = false);
 const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes);
 int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n_chunks_dev, uint32_t max_chunks,
                      const uint32_t* chunk_cnt, const uint32_t* chunk_base, uint32_t* sat,
@@ -520,7 +516,8 @@ struct FinishView {
     uint32_t* tile_keys;  // tile-sorted (keys, vals) after the tile sort
     uint32_t* tile_vals;
     uint32_t* inst_keys;  // per-tile depth sort: the instances' depth keys (binning + tile sort payload), else null
-    uint32_t* tds_list;   // ... its work list (num_tiles words), else null
+    uint2* big_runs;      // ... its runs of > kTdsCapWave instances (k_tile_ranges_views), else null
+    uint32_t* big_count;
     // chunks, composite, merge
     uint2* ranges;
     uint32_t* chunk_cnt;
@@ -539,10 +536,12 @@ int launch_binning_views(FinishView* views, int k, int tiles_x, uint32_t stage_l
 // ... and with the tile sort's pass 0 fused in (hist[v], totals[v] per view), in
 // the two halves of launch_binning_hist / launch_binning_scatter
 int launch_binning_hist_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
-                              int tbits, int passes, hipStream_t s);
+                              int tbits, int passes, hipStream_t s, uint32_t coarse_bits = 0,
+                              const uint32_t* const* key_range = nullptr);
 int launch_binning_scatter_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k,
-                                 int tiles_x, int tbits, int passes, hipStream_t s);
-int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s);
+                                 int tiles_x, int tbits, int passes, hipStream_t s, uint32_t coarse_bits = 0,
+                                 const uint32_t* const* key_range = nullptr);
+int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s, uint32_t cb = 0);
 // first_major: every tile's first chunk dispatched before any later chunk
 int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, uint32_t classes, bool first_major,
                         hipStream_t s);

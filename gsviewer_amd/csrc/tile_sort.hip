@@ -1,36 +1,45 @@
 // Per-tile depth sort (round 5): every tile's instance list put in the GL draw
 // order restricted to the tile, (depth key, slot), in place.
 //
-// The frame's instances are binned in slot order (no global depth sort) and
-// sorted by tile with the stable tile radix sort, so each tile's list leaves
-// the tile sort in ascending slot order with its instances' depth keys beside
-// it (the binning and the tile sort carry them).  A stable LSD radix sort of
-// one list by depth key then gives exactly (key, slot): the order the global
-// depth sort + stable binning produced before (renderer_ogl.py:16-26: GL draws
-// back to front in _sort_gaussian's order; the compositor walks it front to
-// back; ties in slot order, slot n-1-i for Gaussian i, see preprocess.hip).
+// The frame's instances are binned in slot order (no global depth sort) under
+// the key (tile << cb) | bucket, the bucket the top cb bits of the splat's
+// depth key in the frame's key range (InstKey, composite.hip), and sorted by
+// that key with the stable tile radix sort: each tile's list leaves it in
+// runs of equal bucket, buckets ascending, each run in ascending slot order,
+// with its instances' depth keys beside it (the binning and the tile sort
+// carry them).  A stable LSD radix sort of every run by depth key then gives
+// exactly (key, slot): the order the global depth sort + stable binning
+// produced (renderer_ogl.py:16-26: GL draws back to front in _sort_gaussian's
+// order; the compositor walks it front to back; ties in slot order, slot
+// n-1-i for Gaussian i, see preprocess.hip).  The cb bits cost no tile-sort
+// pass: the passes are fixed by the tile id's width and their 8-bit digits
+// have room for them (api.hip TileBits: 3 bits at 1080p, 1 at 4K; 11-bit
+// digits for 9 bits cost the binning and the tile sort 105 us, profiles/r5_s9).
 //
-// Why per tile: the work is a tile's own list, kept on chip (one read and one
-// write of each instance), no chain of global passes and launches; the digit
-// width follows each list's own key range.  The lists' total is D (1.76 M at
-// C2) against N for a global sort, but a frame alone spends its time on the
-// launch chain, not on ranking (api.hip: what it replaced).
+// Why runs: a deep tile (22 K instances at C2) sorted by one workgroup keeps
+// one CU busy for ~40 us (the ranking is VALU issue: ~50 instructions per
+// instance and pass at 4 cycles each, profiles/r5_s8), while the depth
+// buckets cut it into runs (at C2 the longest 9.4 K) that spread over the
+// chip, and the runs' narrower key ranges take fewer passes.  Why no global sort:
+// the work is each run's own instances, kept on chip (one read and one
+// write each), one launch instead of a chain of global passes.
 //
-// One launch, 1024-thread workgroups, a work list of the tiles by length
-// class, longest first (k_chunk_count / k_chunk_write build it with the chunk
-// descriptors, composite.hip):
-//   * 1025 .. 24576 instances: one workgroup per tile, the list in registers
-//     (24 per thread), per pass a stable ranking (ballot digit matching,
-//     per-wave digit counts in LDS) and one LDS exchange; the last pass writes
-//     the slots coalesced through LDS;
-//   * more (the deepest tiles of C3): one workgroup per tile, sub-blocks of
-//     12288 ranked as above and written as contiguous digit runs through global
-//     scratch (the tile sort's alternate buffers), an even number of passes so
-//     the result lands in place;
-//   * 2 .. 1024: one wave per tile, 16 items per lane, wave-local ranking and
-//     exchange, no workgroup barriers.
-// Block b < n_wg takes work-list entry b; the later blocks' 16 waves take the
-// wave-class entries in order.
+// One launch, one 1024-thread block per kTdsSpan instances:
+//   * runs of more than 1024 instances (k_tile_ranges lists them; a few
+//     hundred at C2) are dealt to the blocks in turn, each sorted by one whole
+//     block: up to 24576 the run in registers (24 per thread), per
+//     pass a stable ranking (ballot digit matching, per-wave digit counts in
+//     LDS) and one LDS exchange; the last pass writes the slots coalesced
+//     through LDS;
+//   * longer (a run that fills a deep tile: a depth range too narrow for the
+//     frame's buckets, the deepest tiles of C3): the whole block, sub-blocks
+//     of 12288 ranked as above and written as contiguous digit runs through
+//     global scratch (the tile sort's alternate buffers), an even number of
+//     passes so the result lands in place;
+//   * then each block finds the runs that start in its span (the last one may
+//     end past it) and sorts those of 2 .. 1024 instances, one wave per run,
+//     16 items per lane, wave-local ranking and exchange, no workgroup
+//     barriers.
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -84,20 +93,21 @@ __device__ void tds_wave(const uint32_t* __restrict__ keys, uint32_t* __restrict
     const uint32_t lane = __lane_id();
     const uint32_t nr = (L + 63u) / 64u;
     uint32_t k[kTdsLaneItems], v[kTdsLaneItems], rank[kTdsLaneItems];
+    // every load issued before any is used (a use right after each guarded load
+    // waited for it: 16 serial round trips per run, profiles/r5_s11)
+#pragma unroll
+    for (int j = 0; j < kTdsLaneItems; ++j) {
+        const uint32_t i = (uint32_t)j * 64u + lane;
+        const bool ok = (uint32_t)j < nr && i < L;
+        k[j] = ok ? keys[b + i] : 0xffffffffu;
+        v[j] = ok ? vals[b + i] : 0u;
+    }
     uint32_t lo = 0xffffffffu, hi = 0u;
 #pragma unroll
     for (int j = 0; j < kTdsLaneItems; ++j) {
-        k[j] = 0u;
-        v[j] = 0u;
-        if ((uint32_t)j < nr) {
-            const uint32_t i = (uint32_t)j * 64u + lane;
-            if (i < L) {
-                k[j] = keys[b + i];
-                v[j] = vals[b + i];
-                lo = min(lo, k[j]);
-                hi = max(hi, k[j]);
-            }
-        }
+        const bool ok = (uint32_t)j < nr && (uint32_t)j * 64u + lane < L;
+        lo = min(lo, k[j]);
+        hi = ok ? max(hi, k[j]) : hi;
     }
     const uint32_t kmin = wave_min(lo), kmax = wave_reduce_max(hi);
     if (kmax == kmin) return;  // equal keys: the slot order is the order
@@ -258,20 +268,19 @@ __device__ void tds_block(const uint32_t* __restrict__ keys, uint32_t* __restric
     const uint32_t span = (L + kTdsThreads - 1u) / kTdsThreads * 64u;
     const uint32_t nr = span / 64u;
     uint32_t k[kTdsItems], v[kTdsItems], rank[kTdsItems];
+#pragma unroll
+    for (int j = 0; j < kTdsItems; ++j) {  // (every load issued before any is used)
+        const uint32_t i = w * span + (uint32_t)j * 64u + lane;
+        const bool ok = (uint32_t)j < nr && i < L;
+        k[j] = ok ? keys[b + i] : 0xffffffffu;
+        v[j] = ok ? vals[b + i] : 0u;
+    }
     uint32_t lo = 0xffffffffu, hi = 0u;
 #pragma unroll
     for (int j = 0; j < kTdsItems; ++j) {
-        k[j] = 0u;
-        v[j] = 0u;
-        if ((uint32_t)j < nr) {
-            const uint32_t i = w * span + (uint32_t)j * 64u + lane;
-            if (i < L) {
-                k[j] = keys[b + i];
-                v[j] = vals[b + i];
-                lo = min(lo, k[j]);
-                hi = max(hi, k[j]);
-            }
-        }
+        const bool ok = (uint32_t)j < nr && w * span + (uint32_t)j * 64u + lane < L;
+        lo = min(lo, k[j]);
+        hi = ok ? max(hi, k[j]) : hi;
     }
     block_minmax(lo, hi, S);
     if (hi == lo) return;
@@ -318,16 +327,25 @@ __device__ void tds_block(const uint32_t* __restrict__ keys, uint32_t* __restric
 // each ranked in registers, restaged in LDS in digit order (keys and slots side
 // by side) and written as contiguous digit runs.
 constexpr uint32_t kTdsSub = kTdsCapBlock / 2;
+constexpr int kSweep = 8;  // loads in flight per thread in the global path's sweeps
 constexpr int kTdsSubItems = (int)kTdsSub / kTdsThreads;
 
 __device__ void tds_global(uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t* __restrict__ keys_alt,
                            uint32_t* __restrict__ vals_alt, uint32_t b, uint32_t L, TdsLds& S) {
     const uint32_t t = threadIdx.x, w = t >> 6, lane = __lane_id();
     uint32_t lo = 0xffffffffu, hi = 0u;
-    for (uint32_t i = t; i < L; i += kTdsThreads) {
-        const uint32_t kk = keys[b + i];
-        lo = min(lo, kk);
-        hi = max(hi, kk);
+    for (uint32_t i0 = 0; i0 < L; i0 += kSweep * kTdsThreads) {  // kSweep loads in flight per thread
+        uint32_t kk[kSweep];
+#pragma unroll
+        for (int j = 0; j < kSweep; ++j) {
+            const uint32_t i = i0 + (uint32_t)j * kTdsThreads + t;
+            kk[j] = i < L ? keys[b + i] : 0xffffffffu;
+        }
+#pragma unroll
+        for (int j = 0; j < kSweep; ++j) {
+            lo = min(lo, kk[j]);
+            hi = i0 + (uint32_t)j * kTdsThreads + t < L ? max(hi, kk[j]) : hi;
+        }
     }
     block_minmax(lo, hi, S);
     if (hi == lo) return;
@@ -346,7 +364,17 @@ __device__ void tds_global(uint32_t* __restrict__ keys, uint32_t* __restrict__ v
         // the list's digit counts -> the digits' first global positions
         if (t < (uint32_t)kTdsRadix) S.dbase[t] = 0u;
         __syncthreads();
-        for (uint32_t i = t; i < L; i += kTdsThreads) atomicAdd(&S.dbase[dg.of(ks[i])], 1u);
+        for (uint32_t i0 = 0; i0 < L; i0 += kSweep * kTdsThreads) {
+            uint32_t kk[kSweep];
+#pragma unroll
+            for (int j = 0; j < kSweep; ++j) {
+                const uint32_t i = i0 + (uint32_t)j * kTdsThreads + t;
+                kk[j] = i < L ? ks[i] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < kSweep; ++j)
+                if (i0 + (uint32_t)j * kTdsThreads + t < L) atomicAdd(&S.dbase[dg.of(kk[j])], 1u);
+        }
         __syncthreads();
         {
             const uint32_t c = t < (uint32_t)kTdsRadix ? S.dbase[t] : 0u;
@@ -399,72 +427,148 @@ __device__ void tds_global(uint32_t* __restrict__ keys, uint32_t* __restrict__ v
 }
 
 struct TdsView {
-    const uint2* ranges;
-    const uint32_t* list;    // tiles by length class (chunk_write)
-    const uint32_t* counts;  // {workgroup-class tiles, wave-class tiles}
-    uint32_t* keys;          // the instances' depth keys (tile sort payload); the oversized path permutes them
-    uint32_t* vals;          // the tile list (slots), sorted in place
-    uint32_t* keys_alt;      // scratch for the oversized path (n_dup words each)
+    const uint32_t* tkeys;  // the tile sort's keys: a run is a stretch of equal ones
+    uint32_t* keys;         // the instances' depth keys; the global path permutes them
+    uint32_t* vals;         // the tile lists (slots), sorted in place
+    uint32_t* keys_alt;     // scratch for the global path (n words each)
     uint32_t* vals_alt;
+    uint32_t n;
+    const uint2* big_runs;  // the runs of > kTdsCapWave (k_tile_ranges)
+    const uint32_t* big_count;
 };
 struct TdsViews {
     TdsView v[kMaxViews];
+    uint64_t* stamps;  // (timing knob GSR_DEBUG_TDS & 8: per block 4 clock stamps + 4 counts; else null)
 };
 
-// Persistent: a grid of at most one workgroup per CU (the LDS allows one)
-// walks the work units in order, unit u < n_wg a workgroup-class list, the
-// later units 16 wave-class lists each.  (A grid sized for the host's upper
-// bound of the workgroup-class lists, ~1700 blocks at C2 that mostly exit at
-// once, cost ~30 us of workgroup churn: profiles/r5_s6.)
+constexpr int kSpanItems = (int)kTdsSpan / kTdsThreads;  // instances per thread when finding the runs
+
+// Runs of a span, outside the sort's LDS (TdsLds): their starts (offsets from
+// the span's first instance) and the last one's end.
+struct TdsRunLds {
+    uint16_t start[kTdsSpan];
+    uint32_t n_runs, last_end;
+    uint32_t scan[kTdsWaves];
+};
+
 __global__ __launch_bounds__(kTdsThreads) void k_tile_depth_sort(TdsViews vs, uint32_t dbg) {
     __shared__ TdsLds S;
+    __shared__ TdsRunLds R;
     const TdsView& V = vs.v[blockIdx.y];
-    const uint32_t n_wg = V.counts[0], n_wave = V.counts[1];
-    const uint32_t units = n_wg + (n_wave + kTdsWaves - 1) / kTdsWaves;
-    const uint32_t w = threadIdx.x >> 6;
-    for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {  // (u is uniform: every barrier is reached)
-        if (u < n_wg) {
-            if (!(dbg & 1u)) {
-                const uint2 r = V.ranges[V.list[u]];
-                const uint32_t L = r.y - r.x;
-                if (L > kTdsCapBlock)
-                    tds_global(V.keys, V.vals, V.keys_alt, V.vals_alt, r.x, L, S);
-                else
-                    tds_block(V.keys, V.vals, r.x, L, S, dbg);
+    if (blockIdx.x * kTdsSpan >= V.n) return;  // (a view smaller than the grid's largest)
+    const uint32_t t = threadIdx.x, w = t >> 6, lane = __lane_id();
+    uint64_t* st = vs.stamps && blockIdx.y == 0 ? vs.stamps + 8 * (size_t)blockIdx.x : nullptr;
+    if (st && t == 0) st[0] = __builtin_amdgcn_s_memrealtime();
+    // A. the long runs, one workgroup each, dealt to the view's blocks in turn
+    const uint32_t n_big = *V.big_count;
+    const uint32_t blocks = (V.n + kTdsSpan - 1) / kTdsSpan;
+    uint32_t big_done = 0, big_items = 0;
+    for (uint32_t i = blockIdx.x; i < n_big; i += blocks) {
+        const uint2 br = V.big_runs[i];
+        ++big_done;
+        big_items += br.y;
+        if (!(dbg & 1u)) {
+            if (br.y > kTdsCapBlock)
+                tds_global(V.keys, V.vals, V.keys_alt, V.vals_alt, br.x, br.y, S);
+            else
+                tds_block(V.keys, V.vals, br.x, br.y, S, dbg);
+        }
+        __syncthreads();  // (the next run reuses the LDS)
+    }
+    if (st && t == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+    // B. the runs of 2 .. kTdsCapWave that start in this block's span, one wave each
+    const uint32_t p0 = blockIdx.x * kTdsSpan;
+    const uint32_t p1 = min(p0 + kTdsSpan, V.n);
+    {
+        const uint32_t q0 = p0 + t * kSpanItems;
+        uint32_t flags = 0, cnt = 0;
+        if (q0 < p1) {
+            uint32_t kk[kSpanItems];  // (every load issued before any is used)
+#pragma unroll
+            for (int j = 0; j < kSpanItems; ++j) kk[j] = q0 + (uint32_t)j < p1 ? V.tkeys[q0 + j] : 0u;
+            uint32_t prev = q0 > 0 ? V.tkeys[q0 - 1] : ~kk[0];
+#pragma unroll
+            for (int j = 0; j < kSpanItems; ++j) {
+                if (q0 + (uint32_t)j < p1 && kk[j] != prev) flags |= 1u << j;
+                prev = kk[j];
             }
-        } else {
-            const uint32_t j = (u - n_wg) * kTdsWaves + w;
-            if (j < n_wave && !(dbg & 2u)) {
-                const uint2 r = V.ranges[V.list[n_wg + j]];
-                tds_wave(V.keys, V.vals, r.x, r.y - r.x, S.wave[w], dbg);
+            cnt = (uint32_t)__popc(flags);
+        }
+        uint32_t total;
+        uint32_t o = block_exclusive<kTdsThreads>(cnt, R.scan, total);
+#pragma unroll
+        for (int j = 0; j < kSpanItems; ++j)
+            if (flags & (1u << j)) R.start[o++] = (uint16_t)(t * kSpanItems + (uint32_t)j);
+        if (t == 0) R.n_runs = total;
+    }
+    __syncthreads();
+    const uint32_t n_runs = R.n_runs;  // (0: the whole span continues a run begun before it)
+    // where the span's last run ends (it may go on past p1; a long one is not this block's): wave 0 looks
+    // at most kTdsCapWave + 1 instances past p1, 64 at a time
+    if (w == 0) {
+        uint32_t e = p1;
+        if (n_runs > 0 && p1 < V.n) {
+            const uint32_t key = V.tkeys[p0 + R.start[n_runs - 1]];
+            constexpr int kLook = (int)(kTdsCapWave + 64) / 64;  // 17 loads per lane, all in flight
+            uint32_t kk[kLook];
+#pragma unroll
+            for (int c = 0; c < kLook; ++c) {
+                const uint32_t i = p1 + (uint32_t)c * 64u + lane;
+                kk[c] = i < V.n ? V.tkeys[i] : ~key;
+            }
+            e = 0xffffffffu;
+#pragma unroll
+            for (int c = kLook - 1; c >= 0; --c) {  // the first mismatch: the lowest chunk that has one
+                const uint64_t m = __ballot(kk[c] != key);
+                if (m) e = p1 + (uint32_t)c * 64u + (uint32_t)__builtin_ctzll(m);
+            }
+            if (e == 0xffffffffu) e = V.n;  // longer than kTdsCapWave: a long run (part A)
+        }
+        if (lane == 0) R.last_end = min(e, V.n);
+    }
+    __syncthreads();
+    if (st && t == 0) st[2] = __builtin_amdgcn_s_memrealtime();
+    uint32_t small_items = 0;
+    if (!(dbg & 2u)) {
+        for (uint32_t r = w; r < n_runs; r += kTdsWaves) {
+            const uint32_t b = p0 + R.start[r];
+            const uint32_t e = r + 1 < n_runs ? p0 + R.start[r + 1] : R.last_end;
+            const uint32_t L = e - b;
+            if (L >= 2u && L <= kTdsCapWave) {
+                tds_wave(V.keys, V.vals, b, L, S.wave[w], dbg);
+                small_items += L;
             }
         }
-        __syncthreads();  // (the next unit reuses the LDS)
+    }
+    if (st) {
+        __syncthreads();
+        if (t == 0) {
+            st[3] = __builtin_amdgcn_s_memrealtime();
+            st[4] = big_done;
+            st[5] = big_items;
+            st[6] = n_runs;
+        }
+        if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(st + 7), (unsigned long long)small_items);
     }
 }
 
 }  // namespace
 
-int launch_tile_depth_sort(const TileSortView* views, int k, int num_tiles, hipStream_t s, uint32_t debug) {
+int launch_tile_depth_sort(const TileSortView* views, int k, hipStream_t s, uint32_t debug, uint64_t* stamps) {
     if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "tile depth sort: view count out of range");
     TdsViews tv{};
-    uint32_t wg_max = 0;
+    tv.stamps = stamps;
+    uint32_t n_max = 0;
     for (int i = 0; i < k; ++i) {
         const TileSortView& a = views[i];
-        tv.v[i] = TdsView{a.ranges, a.list, a.counts, a.keys, a.vals, a.keys_alt, a.vals_alt};
-        // an upper bound of the workgroup-class tiles: each holds more than kTdsCapWave instances
-        wg_max = std::max(wg_max, std::min((uint32_t)num_tiles, a.n_dup / (kTdsCapWave + 1u)));
+        if (a.n_dup && (!a.tile_keys || !a.keys || !a.vals || !a.keys_alt || !a.vals_alt || !a.big_runs ||
+                        !a.big_count))
+            return set_error(GSR_ERR_INVALID, "tile depth sort: null buffer");
+        tv.v[i] = TdsView{a.tile_keys, a.keys, a.vals, a.keys_alt, a.vals_alt, a.n_dup, a.big_runs, a.big_count};
+        n_max = std::max(n_max, a.n_dup);
     }
-    // at most the work units, and one block per CU per view (a block takes one CU: its LDS)
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-    }
-    const uint32_t units = wg_max + (uint32_t)(num_tiles + kTdsWaves - 1) / kTdsWaves;
-    const uint32_t grid = std::min(units, (uint32_t)cus);
-    if (units == 0) return GSR_OK;
+    if (n_max == 0) return GSR_OK;
+    const uint32_t grid = (n_max + kTdsSpan - 1) / kTdsSpan;
     k_tile_depth_sort<<<dim3(grid, (unsigned)k), kTdsThreads, 0, s>>>(tv, debug);
     GSR_LAUNCH_CHECK("tile_depth_sort");
     return GSR_OK;

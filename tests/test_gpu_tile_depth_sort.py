@@ -1,22 +1,28 @@
 """The per-tile depth sort (gsviewer_amd/csrc/tile_sort.hip, the default form).
 
-Each tile's list is binned in slot order and sorted by its instances' depth
-keys inside the tile, instead of a global depth sort before the binning.
-The order it must produce is the GL draw order restricted to the tile, the
-one /root/reference/render/renderer_ogl.py:16-26 draws back to front (read
-front to back; ties in descending Gaussian id).  Checked here, against the
-exact form (GSR_TILE_DEPTH_SORT=0: the global radix depth sort, then a stable
-binning in depth order; tests/test_gpu_parity.py checks that form's global
-order and tile lists against the oracle), bit for bit (tile lists, ranges,
-records, images):
+The instances are binned in slot order under the key (tile, coarse depth
+bucket) (composite.hip InstKey: the top cb bits of the splat's depth key in
+the frame's key range; cb fills the tile sort's 11-bit digits: 0 for frames of
+<= 2048 tiles, 9 at 1080p), and every run of equal key is sorted by its
+instances' depth keys.  The order it must produce is the GL draw order
+restricted to the tile, the one /root/reference/render/renderer_ogl.py:16-26
+draws back to front (read front to back; ties in descending Gaussian id).
+Checked here, against the exact form (GSR_TILE_DEPTH_SORT=0: the global radix
+depth sort, then a stable binning in depth order; tests/test_gpu_parity.py
+checks that form's global order and tile lists against the oracle), bit for
+bit (tile lists, ranges, records, images):
 
-* every work-list class (tds_class_of: one wave per list of 2..1024, one
-  workgroup per list up to 24576 in registers, one workgroup through global
-  scratch beyond, several 12288-instance sub-blocks per pass);
+* every run path: one wave per run of 2..1024, one workgroup per run up to
+  24576 in registers, one workgroup through global scratch beyond (several
+  12288-instance sub-blocks per pass) -- at 540x960 (2040 tiles, cb = 0) the
+  runs are whole tile lists of every length;
+* a single run of ~60k instances: a dense fronto-parallel plane in one tile,
+  one far splat stretching the frame's key range so that the plane's depths
+  share one coarse bucket;
 * lists whose keys are all equal, or take two values (ties by slot only);
-* the adversarial case of round 4's coarse order: a dense fronto-parallel
-  plane plus one far splat that stretches the frame's key range, at 1080p,
-  whose frame must also stay within 1.5x the exact form's time;
+* round 4's adversarial case for the coarse order: a dense plane plus one far
+  splat at 1080p (runs as long as the tile lists), whose frame must also stay
+  within 1.5x the exact form's time;
 * a group of views (gsr_render_finish_views), deep lists included.
 """
 import time
@@ -37,7 +43,8 @@ CAP_WAVE, CAP_BLOCK = 1024, 24576  # gsr_internal.h kTdsCapWave / kTdsCapBlock
 
 
 def tds_class(lens):
-    """gsr_internal.h tds_class_of (7: nothing to sort)."""
+    """Run classes by length (a run is a whole tile list when cb = 0): 0 global
+    path, 1-3 workgroup, 4-6 wave, 7 nothing to sort."""
     lens = np.asarray(lens, np.int64)
     return np.select([lens > CAP_BLOCK, lens > 8192, lens > 2048, lens > CAP_WAVE, lens > 256, lens > 64, lens >= 2],
                      [0, 1, 2, 3, 4, 5, 6], 7)
@@ -123,6 +130,30 @@ def test_deep_lists_image_against_oracle(gpu, monkeypatch):
     assert lens.max() > CAP_BLOCK, lens.max()
     ref = C.render(g.flat(), g.sh_dim, uniforms_for(cam), mode="float")
     compare_images(res["image"], ref)
+
+
+def test_single_long_run(gpu, monkeypatch):
+    """~60k instances in one tile and one coarse bucket: a plane of jittered
+    depth in front of the camera, one far splat stretching the key range."""
+    rng = np.random.default_rng(21)
+    n = 60_000
+    # (centred on a tile of the 160x96 frame: 9.6 px per unit at z = 0, tile centres 8 px off the image centre)
+    xyz = np.stack([0.83 + rng.uniform(-0.15, 0.15, n), 0.83 + rng.uniform(-0.1, 0.1, n),
+                    rng.uniform(-1e-4, 1e-4, n)], 1)
+    scale = np.exp(rng.uniform(np.log(0.002), np.log(0.006), (n, 3)))
+    scale[:, 2] = 1e-4
+    xyz = np.concatenate([xyz, [[0.0, 0.0, -400.0]]])
+    scale = np.concatenate([scale, [[2.0, 2.0, 2.0]]])
+    g = _scene(xyz, scale, 21, opacity=(0.01, 0.05))
+    cam = Camera(96, 160)
+    st = _settings(t_min=0.0)
+    tile = _frames(monkeypatch, g, cam, st, "tile")
+    exact = _frames(monkeypatch, g, cam, st, "exact")
+    _same(tile, exact)
+    lens = tile["ranges"][:, 1].astype(np.int64) - tile["ranges"][:, 0]
+    assert lens.max() > 2 * 12288, lens.max()
+    ref = C.render(g.flat(), g.sh_dim, uniforms_for(cam), mode="float")
+    compare_images(tile["image"], ref)
 
 
 @pytest.mark.parametrize("levels", [1, 2])

@@ -5,7 +5,8 @@ GSR_DEBUG_TDS setting given on the command line (timing-only knob of
 tile_sort.hip: 1 skips the workgroup-class lists, 2 the wave-class lists, 4
 sorts one digit pass), then the tile-length and per-list key-width census of
 the frame (default form).
-usage: python tools/tds_probe.py [--config c2|c3|c5] [--frames 30] DEBUG [DEBUG ...]"""
+usage: python tools/tds_probe.py [--config c2|c3|c5] [--frames 30] DEBUG[:COARSE_BITS[:FORM]] ...
+(FORM 0: the exact global depth sort, GSR_TILE_DEPTH_SORT=0)"""
 import argparse
 import ctypes
 import os
@@ -33,8 +34,15 @@ scene = HipScene.from_gaussian_data(g)
 cam = camera_from(Camera(h, w))
 out = torch.empty((h, w, 3), dtype=torch.float32, device="cuda")
 lib = _lib.load()
-for dbg in a.debug:
+for arg in a.debug:  # DEBUG[:COARSE_BITS[:TILE_DEPTH_SORT]]
+    parts = arg.split(":")
+    dbg = parts[0]
     os.environ["GSR_DEBUG_TDS"] = dbg
+    if len(parts) > 1:
+        os.environ["GSR_TDS_COARSE_BITS"] = parts[1]
+    else:
+        os.environ.pop("GSR_TDS_COARSE_BITS", None)
+    os.environ["GSR_TILE_DEPTH_SORT"] = parts[2] if len(parts) > 2 else "1"
     ctx = HipContext()
     st = RenderSettings(t_min=1e-4, out_layout=1)
     for _ in range(5):
@@ -47,10 +55,12 @@ for dbg in a.debug:
     ms = (ctypes.c_double * len(_lib.STAGES))()
     fr = ctypes.c_int64()
     _lib.check(lib.gsr_context_stage_times(ctx.handle, ms, ctypes.byref(fr)), "stage_times")
-    print(f"GSR_DEBUG_TDS={dbg}: " + " ".join(f"{k} {1e3 * ms[i] / max(fr.value, 1):.1f}"
+    print(f"{arg}: " + " ".join(f"{k} {1e3 * ms[i] / max(fr.value, 1):.1f}"
                                                for i, k in enumerate(_lib.STAGES)), flush=True)
     ctx.close()
 os.environ["GSR_DEBUG_TDS"] = "0"
+os.environ["GSR_TILE_DEPTH_SORT"] = "1"
+os.environ.pop("GSR_TDS_COARSE_BITS", None)
 ctx = HipContext()
 render_into(ctx, scene, cam, RenderSettings(t_min=1e-4, out_layout=1), out)
 torch.cuda.synchronize()
