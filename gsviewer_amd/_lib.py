@@ -150,7 +150,7 @@ SIGNATURES = {
 
 STAGES = ["cull", "preprocess", "depth_sort", "binning", "tile_sort", "tile_ranges", "composite", "sync", "merge"]
 
-GSR_DEBUG_RECORDS, GSR_DEBUG_DEPTH_ORDER, GSR_DEBUG_TILE_RANGES, GSR_DEBUG_TILE_LIST, GSR_DEBUG_SLOT_KEYS = 0, 1, 2, 3, 4
+GSR_DEBUG_RECORDS, GSR_DEBUG_DEPTH_ORDER, GSR_DEBUG_TILE_RANGES, GSR_DEBUG_TILE_LIST = 0, 1, 2, 3
 
 ABI_VERSION = 6
 MAX_VIEWS = 8  # GSR_MAX_VIEWS (include/gsr.h)

@@ -1,20 +1,14 @@
 // C ABI (include/gsr.h): scene lifetime, frame workspace, render orchestration.
 //
-// Frame pipeline on one stream (N = Gaussians, V = visible, D = instances),
-// the per-tile depth sort (the default, round 5):
-//   k_preprocess_fc(N): cull, records, depth keys, tile rects by slot; V, D and
-//   the key range on device; the zero block cleared (the last block stores
-//   (V, D, seq) to host-mapped memory)
-//   binning counts (k_bin_hist over the N slots in slot order) + their offsets
-//   [host polls for (V, D, seq) while the GPU counts]
-//   k_bin_scatter: the instances at the tile sort's pass-0 positions, each with
-//   its splat's depth key -> the tile sort's last pass (key as payload)
-//   k_tile_ranges -> chunk count / write (+ the depth sort's work list)
-//   -> k_tile_depth_sort: each tile's list to (depth key, slot)
-//   -> k_composite(chunks) -> k_merge
-// GSR_TILE_DEPTH_SORT=0 (the context's exact global form): a depth radix sort
-// of the V splats after the preprocess, the binning in depth order, and no
-// per-tile sort; the same lists, records and images bit for bit.
+// Frame pipeline on one stream (N = Gaussians, V = visible, D = instances):
+//   memset(per-frame zero block: counters, radix totals, tile ranges, saturation words)
+//   k_cull(N) -> scan(N/64 wave counts; total = V on device)
+//   k_preprocess(N): records, depth keys, tile rects; D accumulated on device
+//   (the last preprocess block stores (V, D, seq) to host-mapped memory)
+//   depth radix sort (grid sized by N, count V and key range read on device), 3 passes
+//   [host polls for (V, D, seq) while the GPU runs the depth sort]
+//   binning (reduce, scan, fused scan+write) -> stable tile radix sort over D
+//   k_tile_ranges -> chunk count / scan / write -> k_composite(chunks) -> k_merge
 // The only host wait overlaps GPU work, so no stage of the frame idles.
 #include <hip/hip_runtime.h>
 
@@ -118,8 +112,7 @@ namespace gsr {
 // A frame between gsr_render_begin and gsr_render_finish.
 struct PendingFrame {
     bool active = false;
-    bool tds = false;     // per-tile depth sort: the binning in slot order, no global depth sort
-    bool binned = false;  // ... its binning counts already enqueued (in begin, beside the host wait)
+    uint32_t coarse = 0;  // its depth sort's coarse bits (0: exact), for the run repair
     FrameUniforms u{};
     float t_min = 0.f;
     float bg[3] = {0.f, 0.f, 0.f};
@@ -134,23 +127,30 @@ struct PendingFrame {
     bool packed = false;                    // the depth sort carries them (frames of <= 256 x 256 tiles)
     bool sort_ready = false;  // gsr_render_begin_views done, gsr_render_begin_sort not yet
 };
-
-// Stage profiling of a frame (gsr_context_set_profiling(ctx, 1)): events at
-// stage boundaries; the interval up to mark i is charged to stage[i].
-constexpr int kProfMarks = 16;
-struct ProfMarks {
-    hipEvent_t ev[kProfMarks] = {};
-    int stage[kProfMarks] = {};
-    int n = 0;
-    bool pending = false;
-};
 }  // namespace gsr
 
 // compositing launches whose in-kernel spans one profiling run can record
 constexpr size_t kSpanLaunches = 64;
 
-// depth sort passes of a frame rendered alone (gsr_render; see kDepthPasses) in the exact global form
+// depth sort passes of a frame rendered alone (gsr_render; see kDepthPasses)
 constexpr int kDepthPassesAlone = 3;
+// Coarse depth order (round 4): a frame alone's depth sort (gsr_render_begin)
+// orders only the top 16 bits of its key range, 2 passes of 8 against 3 exact
+// passes of <= 9 (depth sort 76 -> 51 us), and keeps equal coarse keys in slot
+// order.  Only each tile's list needs the exact (key, slot) order: the
+// binning and the tile sort carry each instance's full depth key, and
+// k_tile_ranges restores the order run by run (RunFix; runs that outgrow its
+// register window go to k_long_runs, tile_sort.hip).  Needs the fused binning
+// (which carries the keys; GSR_BIN_FUSED=0 sorts exactly).  A group's frames
+// (gsr_render_begin_views / _sorts / _finish_views) keep the exact sort (4
+// passes of <= 8 bits): in flight the sort's VALU work is the same in 3 or 4
+// passes and the repair only costs (0.1356-0.1365 vs 0.1332-0.1353 ms per frame
+// with 3 passes of 8), and one depth order for the group's paths keeps each
+// finish reading what its sort step left.  With a coarse sort the
+// frame's global depth order (GSR_DEBUG_DEPTH_ORDER) is the coarse one;
+// gsr_sort_depth stays exact.
+constexpr uint32_t kDepthCoarseAlone = 16;
+constexpr uint32_t kDepthCoarseMax = 16;  // 2 passes of <= 8 bits: the last pass's keys are the carried ones
 
 struct gsr_context {
     gsr::DevBuf<uint64_t> vis_mask;
@@ -187,22 +187,16 @@ struct gsr_context {
     bool tail_merge_alone = false;                // ... and a frame alone's (else k_merge)
     uint32_t bin_stage_limit = 0xffffffffu;       // blocks of at most this many instances stage them (build cap)
     uint32_t debug_handoff = 0;                   // tail-merge test knob (GSR_DEBUG_HANDOFF; 0 in production)
-    uint32_t debug_tds = 0;                       // per-tile sort timing knob (GSR_DEBUG_TDS; 0 in production)
-    gsr::DevBuf<uint64_t> tds_stamps;             // ... its stamps (debug_tds & 8; not in the workspace)
     bool fused_cull = true;                       // culling inside the preprocess (launch_preprocess_fc)
-    int depth_passes_alone = kDepthPassesAlone;   // depth sort passes of gsr_render's frames (exact form)
+    int depth_passes_alone = kDepthPassesAlone;   // depth sort passes of gsr_render's frames
     int depth_passes_now = 0;                     // this frame's (0: kDepthPasses)
-    // the per-tile depth sort (GSR_TILE_DEPTH_SORT=0: the exact global depth sort before the binning)
-    bool tile_depth_sort = true;
-    bool rect_payload = true;                     // the exact form's depth sort carries the packed tile rects
-                                                  // (GSR_NO_RECT_PAYLOAD: gathered by the binning; A/B knob)
-    gsr::DevBuf<uint32_t> tpay_a, tpay_b;  // the instances' depth keys through the tile sort (per-tile sort)
-    uint32_t tds_coarse_cap = 8;           // coarse depth bits folded into the tile keys, at most
-                                           // (GSR_TDS_COARSE_BITS; TileBits takes what the passes have room for)
-    // the per-tile sort's binning counts: enqueued before the host knows D, so
-    // in a buffer of their own (radix_tmp may grow with D before the scatter reads them)
-    gsr::DevBuf<uint32_t> bin_hist;
-    gsr::DevBuf<uint2> big_runs;           // the per-tile sort's runs of > kTdsCapWave instances (start, length)
+    // depth sort of a frame alone: the top bits of its key range, the exact order restored per tile list by
+    // k_tile_ranges and k_long_runs (GSR_DEPTH_COARSE=0: every bit, depth_passes_alone)
+    uint32_t depth_coarse_alone = kDepthCoarseAlone;
+    gsr::DevBuf<uint32_t> tpay_a, tpay_b;  // the instances' depth keys through the tile sort (coarse order repair)
+    gsr::DevBuf<uint32_t> long_runs;       // starts of the runs that outgrow the repair window (k_long_runs)
+    bool rect_payload = true;              // the depth sort carries the packed tile rects (GSR_NO_RECT_PAYLOAD:
+                                           // the binning gathers them by slot; A/B and test knob)
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
     uint32_t seq = 0;                       // frame sequence number the host waits for
     uint32_t* host_counters_dev = nullptr;  // its device address
@@ -214,9 +208,10 @@ struct gsr_context {
     const uint32_t* last_tile_list = nullptr;
     int64_t last_tiles = 0;
     const uint2* last_ranges = nullptr;
-    // profiling: stage marks per frame, two frames in flight
+    // profiling: 10 events per frame, two frames in flight
     bool prof_on = false;
-    gsr::ProfMarks pm[2];
+    hipEvent_t ev[2][12] = {};
+    bool ev_pending[2] = {false, false};
     int64_t frame_idx = 0;
     double acc_ms[GSR_NUM_STAGES] = {};
     gsr::PendingFrame pend;
@@ -253,7 +248,7 @@ void each_buf(gsr_context* c, F&& f) {
     f(c->vis_mask); f(c->wave_counts); f(c->block_ranges); f(c->scan_tmp); f(c->recs);
     f(c->keys_a); f(c->keys_b); f(c->vals_a); f(c->vals_b); f(c->trect); f(c->trect_sorted);
     f(c->rect4_a); f(c->rect4_b); f(c->bin_tmp); f(c->tkeys_a); f(c->tkeys_b); f(c->tvals_a); f(c->tvals_b);
-    f(c->tpay_a); f(c->tpay_b); f(c->bin_hist); f(c->big_runs);
+    f(c->tpay_a); f(c->tpay_b); f(c->long_runs);
     f(c->radix_tmp); f(c->zero); f(c->chunk_cnt); f(c->chunk_base); f(c->chunk_desc); f(c->chunk_order);
     f(c->partial); f(c->tmax); f(c->done_ctr);
 }
@@ -341,20 +336,20 @@ int bits_for(uint32_t v) {  // bits needed to represent values < v
 // Per-frame scratch block: [0,4) counters {V, D, extra chunks, -} are
 // overwritten every frame; from `cleared` on, the depth-key range
 // {~kmin, kmax}, the radix digit totals (depth sort, tile sort), the tile
-// ranges (uint2, 16-B aligned), the saturation words (4 per tile), the
-// chunk completion counters of the tail merge (1 per tile, right after the
-// saturation words) and the per-tile depth sort's count of long runs are
+// ranges (uint2, 16-B aligned), the saturation words (4 per tile), the chunk
+// completion counters of the tail merge (1 per tile, right after the
+// saturation words) and the count of the coarse order's long runs are
 // zeroed by k_cull (or the fused preprocess, from `ranges` on).
 struct ZeroLayout {
     size_t counters = 0, cleared = 4, key_range = 4, totals_depth = 8, totals_tile = 0, ranges = 0, sat = 0,
-           big_runs = 0, total = 0;
+           long_runs = 0, total = 0;
     explicit ZeroLayout(int num_tiles) {
         const size_t tot = radix_totals_elems();
         totals_tile = totals_depth + tot;
         ranges = (totals_tile + tot + 3) & ~(size_t)3;
         sat = ranges + 2 * (size_t)num_tiles;
-        big_runs = sat + 5 * (size_t)num_tiles;
-        total = big_runs + 4;
+        long_runs = sat + 5 * (size_t)num_tiles;
+        total = long_runs + 4;
     }
 };
 
@@ -411,40 +406,38 @@ int arm_done_ctr(gsr_context* c, hipStream_t s) {
     return GSR_OK;
 }
 
-// Stage profiling: prof_start opens a frame's marks, prof_mark charges the
-// GPU time since the previous mark to `stage`.  A mark recorded after a host
-// wait measures the GPU's idle gap while the host waited (GSR_STAGE_SYNC).
-int prof_start(gsr_context* c, int slot, hipStream_t s) {
-    if (!c->prof_on) return GSR_OK;
-    ProfMarks& m = c->pm[slot];
-    m.n = 0;
-    GSR_HIP_CHECK(hipEventRecord(m.ev[0], s));
-    m.n = 1;
-    return GSR_OK;
-}
+// Event slots: 0 start | cull+scan | 1 | preprocess | 2 ~sync~ 3 | depth sort | 4 |
+// counts+scan | 5 ~sync~ 6 | instance write | 7 | tile sort | 8 | ranges | 9 | composite | 10 | merge | 11
+enum { EV_START = 0, EV_CULL, EV_PRE, EV_AFTER_SYNC1, EV_DSORT, EV_COUNTS, EV_AFTER_SYNC2, EV_DUPW, EV_TSORT,
+       EV_RANGES_END_COMPOSITE_START, EV_COMPOSITE, EV_COUNT };
 
-int prof_mark(gsr_context* c, int slot, int stage, hipStream_t s) {
+int prof_record(gsr_context* c, int slot, int ev, hipStream_t s) {
     if (!c->prof_on) return GSR_OK;
-    ProfMarks& m = c->pm[slot];
-    if (m.n == 0 || m.n >= kProfMarks) return GSR_OK;
-    GSR_HIP_CHECK(hipEventRecord(m.ev[m.n], s));
-    m.stage[m.n] = stage;
-    m.n += 1;
+    GSR_HIP_CHECK(hipEventRecord(c->ev[slot][ev], s));
     return GSR_OK;
 }
 
 void prof_accumulate(gsr_context* c, int slot, bool wait) {
-    ProfMarks& m = c->pm[slot];
-    if (!m.pending || m.n < 2) return;
-    if (wait) (void)hipEventSynchronize(m.ev[m.n - 1]);
-    else if (hipEventQuery(m.ev[m.n - 1]) != hipSuccess) return;
-    for (int i = 1; i < m.n; ++i) {
+    if (!c->ev_pending[slot]) return;
+    hipEvent_t* e = c->ev[slot];
+    if (wait) (void)hipEventSynchronize(e[EV_COUNT]);
+    else if (hipEventQuery(e[EV_COUNT]) != hipSuccess) return;
+    auto el = [&](int a, int b) {
         float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, m.ev[i - 1], m.ev[i]);
-        c->acc_ms[m.stage[i]] += ms;
-    }
+        (void)hipEventElapsedTime(&ms, e[a], e[b]);
+        return (double)ms;
+    };
+    c->acc_ms[GSR_STAGE_CULL] += el(EV_START, EV_CULL);
+    c->acc_ms[GSR_STAGE_PREPROCESS] += el(EV_CULL, EV_PRE);
+    c->acc_ms[GSR_STAGE_SYNC] += el(EV_PRE, EV_AFTER_SYNC1) + el(EV_COUNTS, EV_AFTER_SYNC2);
+    c->acc_ms[GSR_STAGE_DEPTH_SORT] += el(EV_AFTER_SYNC1, EV_DSORT);
+    c->acc_ms[GSR_STAGE_BINNING] += el(EV_DSORT, EV_COUNTS) + el(EV_AFTER_SYNC2, EV_DUPW);
+    c->acc_ms[GSR_STAGE_TILE_SORT] += el(EV_DUPW, EV_TSORT);
+    c->acc_ms[GSR_STAGE_RANGES] += el(EV_TSORT, EV_RANGES_END_COMPOSITE_START);
+    c->acc_ms[GSR_STAGE_COMPOSITE] += el(EV_RANGES_END_COMPOSITE_START, EV_COMPOSITE);
+    c->acc_ms[GSR_STAGE_MERGE] += el(EV_COMPOSITE, EV_COUNT);
     c->prof_frames += 1;
-    m.pending = false;
+    c->ev_pending[slot] = false;
 }
 
 void prof_group_accumulate(gsr_context* c, int slot) {
@@ -476,74 +469,26 @@ bool rects_packable(const gsr_context* c, const FrameUniforms& u) {
     return c->rect_payload && u.tiles_x <= kPackedRectTiles && u.tiles_y <= kPackedRectTiles;
 }
 
-// The exact form's depth sort: (depth key, slot) over the frame's key range,
-// every bit; carries the packed tile rects when the frame's tiles fit.
 int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const uint32_t* key_range, uint32_t* totals,
                hipStream_t s) {
     f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
     f.pa = c->rect4_a.p, f.pb = c->rect4_b.p;
     f.packed = rects_packable(c, f.u);
+    f.coarse = 0;
     if (f.n == 0) return GSR_OK;
-    return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32,
-                            c->depth_passes_now ? c->depth_passes_now : kDepthPasses, key_range, c->radix_tmp.p,
-                            totals, s, f.packed ? c->trect.p : nullptr, f.packed ? &f.pa : nullptr,
-                            f.packed ? &f.pb : nullptr, 0, c->fused_cull);
-}
-
-// The tile sort's digits for a frame of num_tiles tiles.
-// The tile sort of a frame: the tile id's bits, the passes of <= 11-bit digits
-// they take (the binning is pass 0), and, for the per-tile depth sort, the
-// coarse depth bits folded into the keys below the tile id (InstKey,
-// composite.hip): what room 8-bit digits leave in those passes, so they cost
-// no pass (13 tile bits at 1080p: 2 passes of 8, 3 coarse bits; 4K: 15 + 1).
-struct TileBits {
-    int bits, passes;
-    uint32_t cb = 0;
-    TileBits(int num_tiles, bool tds, uint32_t cap) : bits(bits_for((uint32_t)num_tiles)), passes(radix_passes_for(bits)) {
-        // up to 8-bit digits: the 256-digit kernels (2048 digits over 1.76 M instances cost binning + tile sort
-        // 65 -> 170 us at C2, profiles/r5_s9)
-        const int room = sort_passes() * 8 - std::max(bits, 1);
-        if (tds && room > 0) cb = std::min(cap, (uint32_t)room);
+    // (the payload only when the rects are packed: an unpacked frame gathers them)
+    const uint2* rect_in = f.packed ? c->trect.p : nullptr;
+    uint32_t** pay_io = f.packed ? &f.pa : nullptr;
+    uint32_t** pay_alt = f.packed ? &f.pb : nullptr;
+    // a frame alone with the fused binning (which carries the sorted keys to the repair): the coarse order
+    if (c->depth_passes_now && c->depth_coarse_alone && c->bin_fused) {
+        f.coarse = c->depth_coarse_alone;
+        return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, (int)f.coarse, 2, key_range,
+                                c->radix_tmp.p, totals, s, rect_in, pay_io, pay_alt, 0, c->fused_cull, f.coarse);
     }
-    int key_bits() const { return std::max(bits, 1) + (int)cb; }
-    int sort_passes() const { return std::max(passes, 1); }
-};
-
-// The per-tile depth sort's binning of a context's frame (slot order, keys carried).
-BinSortArgs tds_binning(gsr_context* c, const FrameUniforms& u, uint32_t n_slots) {
-    const TileBits tb(u.tiles_x * u.tiles_y, true, c->tds_coarse_cap);
-    const ZeroLayout zl(u.tiles_x * u.tiles_y);
-    BinSortArgs a{};
-    a.sorted_ids = nullptr;
-    a.trect = c->trect.p;
-    a.rect4_sorted = nullptr;
-    a.n_vis = n_slots;
-    a.tiles_x = u.tiles_x;
-    a.tbits = tb.bits;
-    a.passes = tb.passes;
-    a.hist = c->bin_hist.p;  // (ensure_bin_hist)
-    a.totals = c->zero.p + zl.totals_tile;
-    a.trect_sorted = nullptr;
-    a.tile_keys = c->tkeys_a.p;
-    a.tile_vals = c->tvals_a.p;
-    a.slot_keys = c->keys_a.p;
-    a.inst_keys = c->tpay_a.p;
-    a.coarse_bits = tb.cb;
-    a.key_range = c->zero.p + zl.key_range;
-    return a;
-}
-
-// Slots the binning walks: with the fused cull all n (culled ones have empty
-// rects), else the V compacted records (known once the counts are in).
-uint32_t binning_slots(const gsr_context* c, size_t n, uint32_t n_vis) {
-    return c->fused_cull ? (uint32_t)n : n_vis;
-}
-
-// The per-tile sort's binning counts of a frame (sized before they are enqueued).
-int ensure_bin_hist(gsr_context* c, size_t n_slots, int num_tiles) {
-    const TileBits tb(num_tiles, true, c->tds_coarse_cap);
-    return c->bin_hist.ensure(bin_hist_elems(std::max<size_t>(n_slots, 1), tb.key_bits(), tb.sort_passes()),
-                              "bin_hist");
+    return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32,
+                            c->depth_passes_now ? c->depth_passes_now : kDepthPasses, key_range,
+                            c->radix_tmp.p, totals, s, rect_in, pay_io, pay_alt, 0, c->fused_cull);
 }
 
 // Wait until the last preprocess block has stored this frame's (V, D, seq) to
@@ -787,8 +732,12 @@ int gsr_context_create(gsr_context** out) {
     }
     if (const char* e = std::getenv("GSR_FIRST_MAJOR")) (*out)->first_major = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_BIN_FUSED")) (*out)->bin_fused = std::strtol(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("GSR_TILE_DEPTH_SORT"))
-        (*out)->tile_depth_sort = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("GSR_DEPTH_COARSE")) {
+        // 0: exact depth sort; 8..16: coarse bits of a frame alone (2 passes of <= 8; wider needs a third pass,
+        // whose keys the fused binning would not carry)
+        const long v = std::strtol(e, nullptr, 10);
+        if (v == 0 || (v >= 8 && v <= (long)kDepthCoarseMax)) (*out)->depth_coarse_alone = (uint32_t)v;
+    }
     if (std::getenv("GSR_NO_RECT_PAYLOAD")) (*out)->rect_payload = false;
     if (const char* e = std::getenv("GSR_FUSED_CULL")) (*out)->fused_cull = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_FIRST_MAJOR_ALONE"))
@@ -801,11 +750,6 @@ int gsr_context_create(gsr_context** out) {
     if (const char* e = std::getenv("GSR_BIN_STAGE_LIMIT"))
         (*out)->bin_stage_limit = gsr::clamp_stage_limit(std::strtol(e, nullptr, 10));
     if (const char* e = std::getenv("GSR_DEBUG_HANDOFF")) (*out)->debug_handoff = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("GSR_DEBUG_TDS")) (*out)->debug_tds = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("GSR_TDS_COARSE_BITS")) {
-        const long v = std::strtol(e, nullptr, 10);
-        if (v >= 0 && v <= 8) (*out)->tds_coarse_cap = (uint32_t)v;
-    }
     if (const char* e = std::getenv("GSR_WAIT_TIMEOUT_MS")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1) (*out)->wait_timeout_ms = v;
@@ -818,14 +762,13 @@ int gsr_context_destroy(gsr_context* c) {
     (void)hipDeviceSynchronize();
     each_buf(c, [](auto& b) { b.release(); });
     if (c->host_counters) (void)hipHostFree(c->host_counters);
-    for (auto& m : c->pm)
-        for (auto& e : m.ev)
+    for (auto& row : c->ev)
+        for (auto& e : row)
             if (e) (void)hipEventDestroy(e);
     for (auto& row : c->evg)
         for (auto& e : row)
             if (e) (void)hipEventDestroy(e);
     c->stamps.release();
-    c->tds_stamps.release();
     delete c;
     return GSR_OK;
 }
@@ -852,7 +795,6 @@ int gsr_context_reserve(gsr_context* c, int64_t n, int32_t width, int32_t height
     // ensure_scene_buffers would be retired (and, in a caller's workspace, wasted)
     const int rtbits = bits_for((uint32_t)num_tiles);
     const size_t rhist = bin_hist_elems(un, rtbits > 0 ? rtbits : 1, std::max(1, radix_passes_for(rtbits)));
-    // (the binning's counts run over all n slots: bin_hist_elems(n) covers any V)
     if ((rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(d), radix_tmp_elems(un), rhist}), "radix_tmp"))) return rc;
     if ((rc = ensure_scene_buffers(c, un))) return rc;
     if ((rc = c->zero.ensure(ZeroLayout(num_tiles).total, "zero block"))) return rc;
@@ -860,9 +802,7 @@ int gsr_context_reserve(gsr_context* c, int64_t n, int32_t width, int32_t height
     if ((rc = c->tkeys_b.ensure(d, "tile_keys"))) return rc;
     if ((rc = c->tvals_a.ensure(d, "tile_vals"))) return rc;
     if ((rc = c->tvals_b.ensure(d, "tile_vals"))) return rc;
-    if (c->tile_depth_sort) {  // the instances' depth keys through the tile sort, the per-tile sort's work list
-        if ((rc = ensure_bin_hist(c, un, num_tiles))) return rc;
-        if ((rc = c->big_runs.ensure(d / (kTdsCapWave + 1) + 1, "big_runs"))) return rc;
+    if (c->depth_coarse_alone && c->bin_fused) {  // a frame alone's depth keys through the tile sort
         if ((rc = c->tpay_a.ensure(d, "tile_pay"))) return rc;
         if ((rc = c->tpay_b.ensure(d, "tile_pay"))) return rc;
     }
@@ -939,10 +879,6 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
     if ((rc = arm_done_ctr(c, s))) return rc;
     const ZeroLayout zl(num_tiles);
     if ((rc = c->zero.ensure(zl.total, "zero block"))) return rc;
-    const bool tds = c->tile_depth_sort;
-    // the per-tile sort's binning counts are enqueued here (fused cull: over all n slots)
-    const bool bin_now = tds && c->fused_cull && n > 0;
-    if (bin_now && (rc = ensure_bin_hist(c, n, num_tiles))) return rc;
     uint32_t* counters = c->zero.p + zl.counters;
     const int slot = (int)(c->frame_idx & 1);
     if (c->prof_on) prof_accumulate(c, slot, true);  // slot reuse: frame k-2 is long done
@@ -955,10 +891,11 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
     c->last_tiles = num_tiles;
     c->last_ranges = reinterpret_cast<uint2*>(c->zero.p + zl.ranges);
 
-    if ((rc = prof_start(c, slot, s))) return rc;
+    if ((rc = prof_record(c, slot, EV_START, s))) return rc;
     if (n == 0) GSR_HIP_CHECK(hipMemsetAsync(c->zero.p, 0, sizeof(uint32_t) * zl.total, s));
     if (n > 0 && c->fused_cull) {
         // one launch: cull, preprocess, V / D / key range, and the zero block's clearing
+        if ((rc = prof_record(c, slot, EV_CULL, s))) return rc;
         if ((rc = launch_preprocess_fc(sc->d, u, c->recs.p, c->keys_a.p, c->trect.p, counters, c->zero.p + zl.key_range,
                                        c->zero.p + zl.ranges, (uint32_t)(zl.total - zl.ranges), c->done_ctr.p,
                                        c->host_counters_dev, ++c->seq, radii, s)))
@@ -974,39 +911,30 @@ int gsr_render_begin(gsr_context* c, const gsr_scene* sc, const gsr_camera* cam,
         if ((rc = scan_exclusive(c->wave_counts.p, c->wave_counts.p, nw, c->scan_tmp.p, counters + 0, s,
                                  c->block_ranges.p, (n + kCullBlock - 1) / kCullBlock, c->zero.p + zl.key_range)))
             return rc;
-        if ((rc = prof_mark(c, slot, GSR_STAGE_CULL, s))) return rc;
-        if ((rc = launch_preprocess(sc->d, u, c->vis_mask.p, c->wave_counts.p, counters + 0, c->recs.p, c->keys_a.p,
-                                    c->trect.p, counters, c->done_ctr.p, c->host_counters_dev, ++c->seq, radii, s)))
-            return rc;
     }
-    if ((rc = prof_mark(c, slot, GSR_STAGE_PREPROCESS, s))) return rc;
+    if (!(n > 0 && c->fused_cull) && (rc = prof_record(c, slot, EV_CULL, s))) return rc;
+    if (n > 0 && !c->fused_cull && (rc = launch_preprocess(sc->d, u, c->vis_mask.p, c->wave_counts.p, counters + 0, c->recs.p,
+                                         c->keys_a.p, c->trect.p, counters, c->done_ctr.p, c->host_counters_dev,
+                                         ++c->seq, radii, s)))
+        return rc;
+    if ((rc = prof_record(c, slot, EV_PRE, s))) return rc;
+    if ((rc = prof_record(c, slot, EV_AFTER_SYNC1, s))) return rc;
 
+    // depth sort over the upper bound N; the device count V bounds the work
     PendingFrame& f = c->pend;
     f.n = n;
     f.u = u;
-    f.tds = tds;
-    f.binned = false;
-    if (tds) {
-        // the tile lists' depth order comes from the per-tile sort: no global order
-        f.ka = f.va = f.kb = f.vb = f.pa = f.pb = nullptr;
-        f.packed = false;
-        if (bin_now) {
-            if ((rc = launch_binning_hist(tds_binning(c, u, (uint32_t)n), s))) return rc;
-            f.binned = true;
-            if ((rc = prof_mark(c, slot, GSR_STAGE_BINNING, s))) return rc;
-        }
-    } else {
-        // depth sort over the upper bound N; the device count V bounds the work
-        if ((rc = depth_sort(c, f, counters + 0, c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s))) return rc;
-        if ((rc = prof_mark(c, slot, GSR_STAGE_DEPTH_SORT, s))) return rc;
-    }
+    if ((rc = depth_sort(c, f, counters + 0, c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s))) return rc;
+    if ((rc = prof_record(c, slot, EV_DSORT, s))) return rc;
     f.active = true;
+    f.u = u;
     f.t_min = st->t_min;
     std::memcpy(f.bg, st->bg, sizeof(f.bg));
     f.out_layout = st->out_layout;
     f.blend = st->blend;
     f.out = out;
     f.stream = s;
+    f.n = n;
     f.slot = slot;
     c->host_ms[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
     return GSR_OK;
@@ -1032,13 +960,9 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
     ViewPreArgs pre[GSR_MAX_VIEWS];
     ViewPreFcArgs pfc[GSR_MAX_VIEWS];
     const bool fc = ctxs[0]->fused_cull;
-    for (int v = 1; v < k; ++v) {
+    for (int v = 1; v < k; ++v)
         if (ctxs[v]->fused_cull != fc)
             return set_error(GSR_ERR_INVALID, "render_begin_views: contexts differ in the cull mode (GSR_FUSED_CULL)");
-        if (ctxs[v]->tile_depth_sort != ctxs[0]->tile_depth_sort)
-            return set_error(GSR_ERR_INVALID,
-                             "render_begin_views: contexts differ in the depth order form (GSR_TILE_DEPTH_SORT)");
-    }
     int rc;
     for (int v = 0; v < k; ++v) {
         gsr_context* c = ctxs[v];
@@ -1068,8 +992,6 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
                                radii ? radii[v] : nullptr, (uint32_t)(zl.total - zl.ranges), c->seq};
         PendingFrame& f = c->pend;
         f.u = u[v];
-        f.tds = c->tile_depth_sort;
-        f.binned = false;
         f.t_min = st->t_min;
         std::memcpy(f.bg, st->bg, sizeof(f.bg));
         f.out_layout = st->out_layout;
@@ -1117,83 +1039,49 @@ int gsr_render_begin_views(gsr_context* const* ctxs, int32_t k, const gsr_scene*
 
 int gsr_render_begin_sort(gsr_context* c, void* stream) {
     if (!c) return set_error(GSR_ERR_INVALID, "null argument");
-    return gsr_render_begin_sorts(&c, 1, stream);
+    PendingFrame& f = c->pend;
+    if (!f.sort_ready) return set_error(GSR_ERR_INVALID, "render_begin_sort: no gsr_render_begin_views frame");
+    hipStream_t s = (hipStream_t)stream;
+    const ZeroLayout zl(f.u.tiles_x * f.u.tiles_y);
+    uint32_t* counters = c->zero.p + zl.counters;
+    // depth sort over the upper bound N; the device count V bounds the work
+    int rc;
+    if ((rc = depth_sort(c, f, counters + 0, c->zero.p + zl.key_range, c->zero.p + zl.totals_depth, s))) return rc;
+    f.sort_ready = false;
+    f.active = true;
+    f.stream = s;
+    return GSR_OK;
 }
 
-// The second step of a group's frames: the exact form's depth sorts, or the
-// per-tile sort's binning counts (fused cull; otherwise they wait for V).
 int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream) {
     if (!ctxs) return set_error(GSR_ERR_INVALID, "null argument");
     if (k < 1 || k > GSR_MAX_VIEWS) return set_error(GSR_ERR_INVALID, "render_begin_sorts: k out of range");
     hipStream_t s = (hipStream_t)stream;
+    RadixViewArgs views[GSR_MAX_VIEWS];
     size_t n = 0;
     for (int v = 0; v < k; ++v) {
         gsr_context* c = ctxs[v];
         if (!c) return set_error(GSR_ERR_INVALID, "null argument");
-        const PendingFrame& f = c->pend;
+        PendingFrame& f = c->pend;
         if (!f.sort_ready) return set_error(GSR_ERR_INVALID, "render_begin_sorts: no gsr_render_begin_views frame");
         if (v == 0) n = f.n;
         if (f.n != n) return set_error(GSR_ERR_INVALID, "render_begin_sorts: views of different scenes");
         for (int w = 0; w < v; ++w)
             if (ctxs[w] == c) return set_error(GSR_ERR_INVALID, "render_begin_sorts: contexts must differ");
-        if (f.tds != ctxs[0]->pend.tds || c->fused_cull != ctxs[0]->fused_cull)
-            return set_error(GSR_ERR_INVALID, "render_begin_sorts: contexts differ in the depth order form");
-        if (f.u.tiles_x != ctxs[0]->pend.u.tiles_x || f.u.tiles_y != ctxs[0]->pend.u.tiles_y)
-            return set_error(GSR_ERR_INVALID, "render_begin_sorts: views differ in frame size");
+        const ZeroLayout zl(f.u.tiles_x * f.u.tiles_y);
+        f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
+        f.pa = c->rect4_a.p, f.pb = c->rect4_b.p;
+        f.packed = rects_packable(c, f.u);
+        if (f.packed != rects_packable(ctxs[0], ctxs[0]->pend.u))
+            return set_error(GSR_ERR_INVALID, "render_begin_sorts: views differ in frame size or rect payload");
+        // a group's frames: the exact sort (kDepthCoarseAlone)
+        views[v] = RadixViewArgs{&f.ka, &f.va, &f.kb, &f.vb, c->zero.p + zl.counters, c->zero.p + zl.key_range,
+                                 c->radix_tmp.p, c->zero.p + zl.totals_depth, f.packed ? c->trect.p : nullptr,
+                                 f.packed ? &f.pa : nullptr, f.packed ? &f.pb : nullptr, c->fused_cull, 0u, true};
+        f.coarse = 0;
     }
     int rc;
-    const PendingFrame& f0 = ctxs[0]->pend;
-    if (f0.tds) {
-        const bool bin_now = ctxs[0]->fused_cull && n > 0;
-        if (bin_now) {
-            const int num_tiles = f0.u.tiles_x * f0.u.tiles_y;
-            const TileBits tb(num_tiles, true, ctxs[0]->tds_coarse_cap);
-            FinishView fv[GSR_MAX_VIEWS];
-            uint32_t* hist[GSR_MAX_VIEWS];
-            uint32_t* ttot[GSR_MAX_VIEWS];
-            const uint32_t* kr[GSR_MAX_VIEWS];
-            for (int v = 0; v < k; ++v) {
-                gsr_context* c = ctxs[v];
-                if ((rc = ensure_bin_hist(c, n, num_tiles))) return rc;
-                const BinSortArgs a = tds_binning(c, c->pend.u, (uint32_t)n);
-                fv[v] = FinishView{};
-                fv[v].sorted_ids = nullptr;
-                fv[v].slot_keys = a.slot_keys;
-                fv[v].trect = a.trect;
-                fv[v].n_vis = a.n_vis;
-                fv[v].inst_keys = a.inst_keys;
-                hist[v] = a.hist;
-                ttot[v] = a.totals;
-                kr[v] = a.key_range;
-                if (c->tds_coarse_cap != ctxs[0]->tds_coarse_cap)
-                    return set_error(GSR_ERR_INVALID, "render_begin_sorts: contexts differ in GSR_TDS_COARSE_BITS");
-            }
-            if ((rc = launch_binning_hist_views(fv, hist, ttot, k, f0.u.tiles_x, tb.bits, tb.passes, s, tb.cb, kr)))
-                return rc;
-        }
-        for (int v = 0; v < k; ++v) {
-            PendingFrame& f = ctxs[v]->pend;
-            f.ka = f.va = f.kb = f.vb = f.pa = f.pb = nullptr;
-            f.packed = false;
-            f.binned = bin_now;
-        }
-    } else {
-        RadixViewArgs views[GSR_MAX_VIEWS];
-        for (int v = 0; v < k; ++v) {
-            gsr_context* c = ctxs[v];
-            PendingFrame& f = c->pend;
-            const ZeroLayout zl(f.u.tiles_x * f.u.tiles_y);
-            f.ka = c->keys_a.p, f.kb = c->keys_b.p, f.va = c->vals_a.p, f.vb = c->vals_b.p;
-            f.pa = c->rect4_a.p, f.pb = c->rect4_b.p;
-            f.packed = rects_packable(c, f.u);
-            if (f.packed != rects_packable(ctxs[0], ctxs[0]->pend.u))
-                return set_error(GSR_ERR_INVALID, "render_begin_sorts: views differ in the rect payload");
-            views[v] = RadixViewArgs{&f.ka, &f.va, &f.kb, &f.vb, c->zero.p + zl.counters, c->zero.p + zl.key_range,
-                                     c->radix_tmp.p, c->zero.p + zl.totals_depth, f.packed ? c->trect.p : nullptr,
-                                     f.packed ? &f.pa : nullptr, f.packed ? &f.pb : nullptr, c->fused_cull};
-        }
-        if (n > 0 && (rc = radix_sort_pairs_views(views, k, true, n, 32, kDepthPasses, s))) return rc;
-    }
+    if (n > 0 && (rc = radix_sort_pairs_views(views, k, true, n, 32, kDepthPasses, s))) return rc;
     for (int v = 0; v < k; ++v) {
         PendingFrame& f = ctxs[v]->pend;
         f.sort_ready = false;
@@ -1220,22 +1108,21 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     uint32_t* sat = c->zero.p + zl.sat;
     int rc;
 
-    // host: V and D (the GPU is busy with the depth sort or the binning counts meanwhile)
+    // host: V and D (the GPU is busy with the depth sort meanwhile)
     const auto h1 = std::chrono::steady_clock::now();
     if (n > 0 && (rc = wait_counts(c, s))) return rc;
     const auto h2 = std::chrono::steady_clock::now();
     const uint32_t n_vis = n > 0 ? __atomic_load_n(&c->host_counters[0], __ATOMIC_ACQUIRE) : 0u;
     const uint32_t n_dup = n > 0 ? __atomic_load_n(&c->host_counters[1], __ATOMIC_ACQUIRE) : 0u;
     if (n > 0 && (rc = check_instances(c))) return rc;
-    if (c->prof_on) {
-        prof_accumulate(c, slot ^ 1, false);
-        if ((rc = prof_mark(c, slot, GSR_STAGE_SYNC, s))) return rc;
-    }
-    if (n_vis > 0 && !f.tds) c->last_depth_order = f.va;
+    if (c->prof_on) prof_accumulate(c, slot ^ 1, false);
+    if (n_vis > 0) c->last_depth_order = f.va;
 
     uint32_t* tile_list = c->tvals_a.p;
-    const TileBits tb(num_tiles, f.tds, c->tds_coarse_cap);
-    const bool fused = f.tds || c->bin_fused;  // (the per-tile sort's binning is always the fused one)
+    const int tbits = bits_for((uint32_t)num_tiles);
+    const int tpasses = radix_passes_for(tbits);
+    const bool fused = c->bin_fused;
+    const bool carry = f.coarse && fused;  // the instances' depth keys ride along (coarse order repair)
     uint32_t *tpa = c->tpay_a.p, *tpb = c->tpay_b.p;
     if (n_dup > 0) {
         if ((rc = c->tkeys_a.ensure(n_dup, "tile_keys"))) return rc;
@@ -1243,103 +1130,72 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         if ((rc = c->tvals_a.ensure(n_dup, "tile_vals"))) return rc;
         if ((rc = c->tvals_b.ensure(n_dup, "tile_vals"))) return rc;
         if ((rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(n_dup), radix_tmp_elems(n),
-                                                bin_hist_elems(n, tb.key_bits(), tb.sort_passes())}),
+                                                bin_hist_elems(n_vis, tbits > 0 ? tbits : 1, tpasses > 0 ? tpasses : 1)}),
                                       "radix_tmp")))
             return rc;
-        if (f.tds) {
-            if ((rc = c->tpay_a.ensure(n_dup, "tile_pay"))) return rc;
-            if ((rc = c->tpay_b.ensure(n_dup, "tile_pay"))) return rc;
-            if ((rc = c->big_runs.ensure(n_dup / (kTdsCapWave + 1) + 1, "big_runs"))) return rc;
-            tpa = c->tpay_a.p, tpb = c->tpay_b.p;
-            const uint32_t slots = binning_slots(c, n, n_vis);
-            if (!f.binned && (rc = ensure_bin_hist(c, slots, num_tiles))) return rc;  // (binned: sized in begin)
-            const BinSortArgs a = tds_binning(c, u, slots);
-            if (!f.binned && (rc = launch_binning_hist(a, s))) return rc;
-            rc = launch_binning_scatter(a, s);
-        } else if (fused) {  // the tile sort's pass 0 in the binning: instances leave it ordered by digit 0
-            BinSortArgs a{};
-            a.sorted_ids = f.va;
-            a.trect = c->trect.p;
-            a.rect4_sorted = f.packed ? f.pa : nullptr;
-            a.n_vis = n_vis;
-            a.tiles_x = u.tiles_x;
-            a.tbits = tb.bits;
-            a.passes = tb.passes;
-            a.hist = c->radix_tmp.p;
-            a.totals = c->zero.p + zl.totals_tile;
-            a.trect_sorted = c->trect_sorted.p;
-            a.tile_keys = c->tkeys_a.p;
-            a.tile_vals = c->tvals_a.p;
-            if ((rc = launch_binning_hist(a, s)) == 0) rc = launch_binning_scatter(a, s);
-        } else {
+        if (carry && ((rc = c->tpay_a.ensure(n_dup, "tile_pay"))) == 0) rc = c->tpay_b.ensure(n_dup, "tile_pay");
+        if (carry && rc == 0) rc = c->long_runs.ensure(long_runs_elems(n_dup), "long_runs");
+        if (rc) return rc;
+        tpa = c->tpay_a.p, tpb = c->tpay_b.p;
+        if (fused)  // the tile sort's pass 0 in the binning: instances leave it ordered by digit 0
+            rc = launch_binning_sorted(f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, u.tiles_x, tbits, tpasses,
+                                       c->radix_tmp.p, c->zero.p + zl.totals_tile, c->trect_sorted.p, c->tkeys_a.p,
+                                       c->tvals_a.p, s, carry ? f.ka : nullptr, carry ? c->tpay_a.p : nullptr);
+        else
             rc = launch_binning(f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, u.tiles_x, c->bin_tmp.p,
                                 c->trect_sorted.p, c->tkeys_a.p, c->tvals_a.p, c->bin_stage_limit, s);
-        }
         if (rc) return rc;
     }
-    if ((rc = prof_mark(c, slot, GSR_STAGE_BINNING, s))) return rc;
+    if ((rc = prof_record(c, slot, EV_COUNTS, s))) return rc;
+    if ((rc = prof_record(c, slot, EV_AFTER_SYNC2, s))) return rc;
+    if ((rc = prof_record(c, slot, EV_DUPW, s))) return rc;
     uint32_t *tka = c->tkeys_a.p, *tkb = c->tkeys_b.p, *tva = c->tvals_a.p, *tvb = c->tvals_b.p;
     if (n_dup > 0) {
-        // (the exact form with a single tile: no key bits, nothing to sort)
-        if ((tb.bits > 0 || f.tds) &&
-            (rc = radix_sort_pairs(&tka, &tva, &tkb, &tvb, false, n_dup, nullptr, tb.key_bits(), tb.sort_passes(),
-                                   nullptr, c->radix_tmp.p, c->zero.p + zl.totals_tile, s, nullptr,
-                                   f.tds ? &tpa : nullptr, f.tds ? &tpb : nullptr, fused ? 1 : 0)))
+        if (tbits > 0 && (rc = radix_sort_pairs(&tka, &tva, &tkb, &tvb, false, n_dup, nullptr, tbits, tpasses, nullptr,
+                                                c->radix_tmp.p, c->zero.p + zl.totals_tile, s, nullptr,
+                                                carry ? &tpa : nullptr, carry ? &tpb : nullptr, fused ? 1 : 0)))
             return rc;
         tile_list = tva;
         c->last_tile_list = tva;
     }
-    if ((rc = prof_mark(c, slot, GSR_STAGE_TILE_SORT, s))) return rc;
-    uint32_t* big_count = c->zero.p + zl.big_runs;
-    if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, ranges, s, tb.cb, f.tds ? c->big_runs.p : nullptr,
-                                              big_count)))
-        return rc;
-    if ((rc = prof_mark(c, slot, GSR_STAGE_RANGES, s))) return rc;
-    if (f.tds && n_dup > 0) {  // each tile's runs of one coarse depth bucket to (depth key, slot) order
-        const TileSortView tv{tka, tpa, tva, tpb, tvb, n_dup, c->big_runs.p, big_count};
-        uint64_t* stamps = nullptr;
-        if (c->debug_tds & 8u) {
-            const size_t words = 8 * ((size_t)n_dup / kTdsSpan + 1);
-            if ((rc = c->tds_stamps.ensure(words, "tds_stamps"))) return rc;
-            GSR_HIP_CHECK(hipMemsetAsync(c->tds_stamps.p, 0, words * 8, s));
-            stamps = c->tds_stamps.p;
-        }
-        if ((rc = launch_tile_depth_sort(&tv, 1, s, c->debug_tds, stamps))) return rc;
-        if ((rc = prof_mark(c, slot, GSR_STAGE_DEPTH_SORT, s))) return rc;
-    }
+    if ((rc = prof_record(c, slot, EV_TSORT, s))) return rc;
+    // tile ranges, and (coarse order) the repair of each tile list's runs of equal coarse keys: in registers,
+    // or, for the runs that outgrow the window, k_long_runs
+    const RunFix fix{tva, c->zero.p + zl.key_range, f.coarse, tkb, tvb, carry ? tpa : nullptr,
+                     carry ? c->long_runs.p : nullptr, c->zero.p + zl.long_runs};
+    if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, ranges, fix, s))) return rc;
+    if (n_dup > 0 && f.coarse && (rc = launch_long_runs(tka, n_dup, ranges, fix, s))) return rc;
 
-    // compositing chunks: at most one per tile plus one per `chunk` instances
-    const size_t max_chunks = (size_t)num_tiles + n_dup / c->chunk + 1;
-    if (f.blend != GSR_BLEND_UNORM8) {
+    if (f.blend == GSR_BLEND_UNORM8) {  // the RGBA8 framebuffer: whole lists, back to front, no chunks
+        if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
+        if ((rc = launch_composite_unorm8(ranges, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.bg,
+                                          f.out_layout, f.out, s)))
+            return rc;
+        if ((rc = prof_record(c, slot, EV_COMPOSITE, s))) return rc;
+    } else {
+        // compositing chunks: at most one per tile plus one per `chunk` instances
+        const size_t max_chunks = (size_t)num_tiles + n_dup / c->chunk + 1;
         if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
         if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
         if ((rc = c->chunk_desc.ensure(max_chunks, "chunk_desc"))) return rc;
         if ((rc = c->chunk_order.ensure(max_chunks, "chunk_order"))) return rc;
         if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
         if ((rc = c->tmax.ensure(max_chunks, "tmax"))) return rc;
-        if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->len_classes, c->chunk_cnt.p, c->chunk_base.p,
-                                counters + 2, c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s, c->first_major_alone)))
+        if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->len_classes, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
+                                c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s, c->first_major_alone)))
             return rc;
-    }
-    if ((rc = prof_mark(c, slot, GSR_STAGE_RANGES, s))) return rc;
-
-    if (f.blend == GSR_BLEND_UNORM8) {  // the RGBA8 framebuffer: whole lists, back to front, no chunks
-        if ((rc = launch_composite_unorm8(ranges, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.bg,
-                                          f.out_layout, f.out, s)))
+        if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
+        if ((rc = launch_composite(c->chunk_desc.p, c->chunk_order.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
+                                   sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.t_min, f.bg,
+                                   f.out_layout, f.out, c->partial.p, c->tmax.p, c->tail_merge_alone, s)))
             return rc;
-        if ((rc = prof_mark(c, slot, GSR_STAGE_COMPOSITE, s))) return rc;
-    } else {
-        if ((rc = launch_composite(c->chunk_desc.p, c->chunk_order.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p,
-                                   c->chunk_base.p, sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.t_min,
-                                   f.bg, f.out_layout, f.out, c->partial.p, c->tmax.p, c->tail_merge_alone, s)))
-            return rc;
-        if ((rc = prof_mark(c, slot, GSR_STAGE_COMPOSITE, s))) return rc;
+        if ((rc = prof_record(c, slot, EV_COMPOSITE, s))) return rc;
         if ((rc = launch_merge(c->chunk_cnt.p, c->chunk_base.p, c->partial.p, sat, u, f.t_min, f.bg, f.out_layout,
                                f.out, c->tail_merge_alone, s)))
             return rc;
-        if ((rc = prof_mark(c, slot, GSR_STAGE_MERGE, s))) return rc;
     }
-    if (c->prof_on) c->pm[slot].pending = true;
+    if ((rc = prof_record(c, slot, EV_COUNT, s))) return rc;
+    if (c->prof_on) c->ev_pending[slot] = true;
     {
         const auto h3 = std::chrono::steady_clock::now();
         using ms = std::chrono::duration<double, std::milli>;
@@ -1379,23 +1235,22 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         if (c->prof_on) return set_error(GSR_ERR_INVALID, "render_finish_views: profiling is per view");
         for (int w = 0; w < v; ++w)
             if (ctxs[w] == c) return set_error(GSR_ERR_INVALID, "render_finish_views: contexts must differ");
+        if (f.coarse)
+            return set_error(GSR_ERR_INVALID, "render_finish_views: a frame begun by gsr_render_begin (coarse depth "
+                                              "order) is finished by gsr_render_finish");
         if (f.u.width != f0.u.width || f.u.height != f0.u.height || f.t_min != f0.t_min || f.bg[0] != f0.bg[0] ||
             f.bg[1] != f0.bg[1] || f.bg[2] != f0.bg[2] || f.out_layout != f0.out_layout || f.blend != f0.blend ||
             frag_class_of(f.u.render_mod) != frag_class_of(f0.u.render_mod) || c->chunk_views != c0->chunk_views ||
-            c->len_classes != c0->len_classes || c->first_major != c0->first_major || f.tds != f0.tds ||
-            f.packed != f0.packed || c->fused_cull != c0->fused_cull || c->bin_fused != c0->bin_fused)
+            c->len_classes != c0->len_classes || c->first_major != c0->first_major)
             return set_error(GSR_ERR_INVALID, "render_finish_views: views differ in frame size or settings");
     }
     const FrameUniforms& u0 = c0->pend.u;
     const int num_tiles = u0.tiles_x * u0.tiles_y;
     const ZeroLayout zl(num_tiles);
-    const bool tds = c0->pend.tds;
     FinishView fv[GSR_MAX_VIEWS];
     RadixViewArgs rv[GSR_MAX_VIEWS];
     uint32_t *tka[GSR_MAX_VIEWS], *tkb[GSR_MAX_VIEWS], *tva[GSR_MAX_VIEWS], *tvb[GSR_MAX_VIEWS];
-    uint32_t *tpa[GSR_MAX_VIEWS], *tpb[GSR_MAX_VIEWS];
-    uint32_t n_vis_max = 0, n_dup_max = 0, n_slots = 0;
-    uint32_t nv[GSR_MAX_VIEWS];
+    uint32_t n_vis_max = 0, n_dup_max = 0;
     size_t max_chunks = 0;
     int rc;
     const auto h1 = std::chrono::steady_clock::now();
@@ -1415,21 +1270,13 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         if (f.n > 0 && (rc = check_instances(c))) return rc;
         n_vis_max = std::max(n_vis_max, n_vis);
         n_dup_max = std::max(n_dup_max, n_dup);
-        nv[v] = n_vis;
-        if (n_vis > 0 && !tds) c->last_depth_order = f.va;
+        if (n_vis > 0) c->last_depth_order = f.va;
         if (n_dup > 0) {
             if ((rc = c->tkeys_a.ensure(n_dup, "tile_keys"))) return rc;
             if ((rc = c->tkeys_b.ensure(n_dup, "tile_keys"))) return rc;
             if ((rc = c->tvals_a.ensure(n_dup, "tile_vals"))) return rc;
             if ((rc = c->tvals_b.ensure(n_dup, "tile_vals"))) return rc;
         }
-        if (tds) {  // (every view's, so that each has the buffers even without instances)
-            if ((rc = c->tpay_a.ensure(std::max<uint32_t>(n_dup, 1), "tile_pay"))) return rc;
-            if ((rc = c->tpay_b.ensure(std::max<uint32_t>(n_dup, 1), "tile_pay"))) return rc;
-            if ((rc = c->big_runs.ensure(n_dup / (kTdsCapWave + 1) + 1, "big_runs"))) return rc;
-        }
-        if (tds && c->tds_coarse_cap != c0->tds_coarse_cap)
-            return set_error(GSR_ERR_INVALID, "render_finish_views: contexts differ in GSR_TDS_COARSE_BITS");
         const size_t mc = (size_t)num_tiles + n_dup / c->chunk_views + 1;
         max_chunks = std::max(max_chunks, mc);
         if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
@@ -1440,97 +1287,55 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         if ((rc = c->tmax.ensure(mc, "tmax"))) return rc;
         uint32_t* counters = c->zero.p + zl.counters;
         tka[v] = c->tkeys_a.p, tkb[v] = c->tkeys_b.p, tva[v] = c->tvals_a.p, tvb[v] = c->tvals_b.p;
-        tpa[v] = c->tpay_a.p, tpb[v] = c->tpay_b.p;
-        // binning: the per-tile sort's walks the slots in order, the exact form's the depth order
-        const uint32_t slots = tds ? binning_slots(c, f.n, n_vis) : n_vis;
-        n_slots = std::max(n_slots, slots);
-        fv[v] = FinishView{};
-        fv[v].sorted_ids = tds ? nullptr : f.va;
-        fv[v].slot_keys = tds ? c->keys_a.p : nullptr;
-        fv[v].trect = c->trect.p;
-        fv[v].rect4_sorted = f.packed ? f.pa : nullptr;
-        fv[v].n_vis = slots;
-        fv[v].n_dup = n_dup;
-        fv[v].bin_tmp = c->bin_tmp.p;
-        fv[v].trect_sorted = c->trect_sorted.p;
-        fv[v].tile_keys = tka[v];
-        fv[v].tile_vals = tva[v];
-        fv[v].inst_keys = tds ? tpa[v] : nullptr;
-        fv[v].big_runs = tds ? c->big_runs.p : nullptr;
-        fv[v].big_count = c->zero.p + zl.big_runs;
-        fv[v].ranges = reinterpret_cast<uint2*>(c->zero.p + zl.ranges);
-        fv[v].chunk_cnt = c->chunk_cnt.p;
-        fv[v].chunk_base = c->chunk_base.p;
-        fv[v].n_extra_dev = counters + 2;
-        fv[v].desc = c->chunk_desc.p;
-        fv[v].order = c->chunk_order.p;
-        fv[v].tmax = c->tmax.p;
-        fv[v].sat = c->zero.p + zl.sat;
-        fv[v].recs = c->recs.p;
-        fv[v].out = f.out;
-        fv[v].partial = c->partial.p;
+        if (f.packed != c0->pend.packed)
+            return set_error(GSR_ERR_INVALID, "render_finish_views: views differ in frame size or settings");
+        fv[v] = FinishView{f.va, c->trect.p, f.packed ? f.pa : nullptr, n_vis, n_dup, c->bin_tmp.p, c->trect_sorted.p, tka[v], tva[v], RunFix{},
+                           reinterpret_cast<uint2*>(c->zero.p + zl.ranges), c->chunk_cnt.p, c->chunk_base.p,
+                           counters + 2, c->chunk_desc.p, c->chunk_order.p, c->tmax.p, c->zero.p + zl.sat,
+                           c->recs.p, f.out, c->partial.p};
         rv[v] = RadixViewArgs{&tka[v], &tva[v], &tkb[v], &tvb[v], counters + 1, nullptr, c->radix_tmp.p,
-                              c->zero.p + zl.totals_tile, nullptr, tds ? &tpa[v] : nullptr, tds ? &tpb[v] : nullptr};
+                              c->zero.p + zl.totals_tile};
     }
     // every view's sort temporaries cover the largest view (the grids do)
-    const TileBits tb(num_tiles, tds, c0->tds_coarse_cap);
-    const bool fused = tds || c0->bin_fused;  // (the per-tile sort's binning is always the fused one)
+    const int tbits = bits_for((uint32_t)num_tiles);
+    const int tpasses = radix_passes_for(tbits);
+    const bool fused = c0->bin_fused;
     uint32_t* hist[GSR_MAX_VIEWS];
     uint32_t* ttot[GSR_MAX_VIEWS];
-    const uint32_t* krange[GSR_MAX_VIEWS];
-    for (int v = 0; v < k; ++v) {
+    for (int v = 0; v < k && n_dup_max > 0; ++v) {
         gsr_context* c = ctxs[v];
-        if (n_dup_max > 0 &&
-            (rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(n_dup_max), radix_tmp_elems(c->pend.n),
-                                                bin_hist_elems(std::max<size_t>(n_slots, c->pend.n), tb.key_bits(),
-                                                               tb.sort_passes())}),
+        if ((rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(n_dup_max), radix_tmp_elems(c->pend.n),
+                                                bin_hist_elems(n_vis_max, tbits > 0 ? tbits : 1,
+                                                               tpasses > 0 ? tpasses : 1)}),
                                       "radix_tmp")))
             return rc;
         rv[v].tmp = c->radix_tmp.p;
-        // (a group's count matrices all take the largest view's blocks)
-        if (tds && !c->pend.binned && (rc = ensure_bin_hist(c, n_slots, num_tiles))) return rc;
-        hist[v] = tds ? c->bin_hist.p : c->radix_tmp.p;  // (the per-tile form's counts: ensure_bin_hist)
+        hist[v] = c->radix_tmp.p;
         ttot[v] = c->zero.p + zl.totals_tile;
-        krange[v] = c->zero.p + zl.key_range;
     }
-    if (n_slots > 0 && n_dup_max > 0) {
-        if (fused) {
-            // the counts, unless begin_sorts enqueued them (every view or none: the same form and cull)
-            if (!(tds && c0->pend.binned) &&
-                (rc = launch_binning_hist_views(fv, hist, ttot, k, u0.tiles_x, tb.bits, tb.passes, s, tb.cb, krange)))
-                return rc;
-            rc = launch_binning_scatter_views(fv, hist, ttot, k, u0.tiles_x, tb.bits, tb.passes, s, tb.cb, krange);
-        } else {
-            rc = launch_binning_views(fv, k, u0.tiles_x, c0->bin_stage_limit, s);
-        }
+    if (n_vis_max > 0 && n_dup_max > 0) {
+        rc = fused ? launch_binning_sorted_views(fv, hist, ttot, k, u0.tiles_x, tbits, tpasses, s)
+                   : launch_binning_views(fv, k, u0.tiles_x, c0->bin_stage_limit, s);
         if (rc) return rc;
     }
-    if (n_dup_max > 0 && (tb.bits > 0 || tds) &&
-        (rc = radix_sort_pairs_views(rv, k, false, n_dup_max, tb.key_bits(), tb.sort_passes(), s, fused ? 1 : 0)))
+    if (n_dup_max > 0 && tbits > 0 &&
+        (rc = radix_sort_pairs_views(rv, k, false, n_dup_max, tbits, tpasses, s, fused ? 1 : 0)))
         return rc;
     for (int v = 0; v < k; ++v) {
         fv[v].tile_keys = tka[v];
         fv[v].tile_vals = tva[v];
-        fv[v].inst_keys = tds ? tpa[v] : nullptr;
+        fv[v].fix = RunFix{};  // (a group's frames are sorted exactly: nothing to repair)
         if (fv[v].n_dup > 0) ctxs[v]->last_tile_list = tva[v];
     }
-    if ((rc = launch_tile_ranges_views(fv, k, s, tb.cb))) return rc;
-    if (tds && n_dup_max > 0) {  // each tile's runs of one coarse depth bucket to (depth key, slot) order
-        TileSortView tv[GSR_MAX_VIEWS];
-        for (int v = 0; v < k; ++v)
-            tv[v] = TileSortView{tka[v], tpa[v], tva[v], tpb[v], tvb[v], fv[v].n_dup, fv[v].big_runs, fv[v].big_count};
-        if ((rc = launch_tile_depth_sort(tv, k, s, c0->debug_tds))) return rc;
-    }
+    if ((rc = launch_tile_ranges_views(fv, k, s))) return rc;
     const PendingFrame& f0 = c0->pend;
-    const bool unorm8 = f0.blend == GSR_BLEND_UNORM8;
-    if (!unorm8)
-        if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk_views, c0->len_classes, c0->first_major, s))) return rc;
-    if (unorm8) {  // the RGBA8 framebuffer: one launch per view, no chunks
+    if (f0.blend == GSR_BLEND_UNORM8) {  // the RGBA8 framebuffer: one launch per view, no chunks
         for (int v = 0; v < k; ++v)
             if ((rc = launch_composite_unorm8(fv[v].ranges, fv[v].tile_vals, fv[v].recs, u0,
                                               frag_class_of(u0.render_mod), f0.bg, f0.out_layout, fv[v].out, s)))
                 return rc;
     } else {
+        if ((rc = launch_chunks_views(fv, k, num_tiles, c0->chunk_views, c0->len_classes, c0->first_major, s))) return rc;
         const int gslot = c0->evg_slot;
         if (c0->prof_group) {
             prof_group_accumulate(c0, gslot);  // slot reuse: that launch is two groups back
@@ -1571,7 +1376,7 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         c->host_ms[2] += ms(h3 - h2).count() / k;
         c->host_frames += 1;
         c->frame_idx += 1;
-        c->stats.n_visible = nv[v];
+        c->stats.n_visible = fv[v].n_vis;
         c->stats.n_instances = fv[v].n_dup;
     }
     return GSR_OK;
@@ -1604,12 +1409,12 @@ int gsr_context_set_profiling(gsr_context* c, int32_t enable) {
         return GSR_OK;
     }
     c->prof_group = false;
-    if (enable && !c->pm[0].ev[0]) {
-        for (auto& m : c->pm)
-            for (auto& e : m.ev) GSR_HIP_CHECK(hipEventCreate(&e));
+    if (enable && !c->ev[0][0]) {
+        for (int a = 0; a < 2; ++a)
+            for (int b = 0; b <= EV_COUNT; ++b) GSR_HIP_CHECK(hipEventCreate(&c->ev[a][b]));
     }
     c->prof_on = enable != 0;
-    for (auto& m : c->pm) m.pending = false, m.n = 0;
+    c->ev_pending[0] = c->ev_pending[1] = false;
     for (double& v : c->acc_ms) v = 0.0;
     c->prof_frames = 0;
     return GSR_OK;
@@ -1701,14 +1506,6 @@ int64_t gsr_debug_copy(const gsr_context* c, int32_t what, void* dst, int64_t ma
         case GSR_DEBUG_DEPTH_ORDER: src = c->last_depth_order; bytes = c->stats.n_visible * 4; break;
         case GSR_DEBUG_TILE_RANGES: src = c->last_ranges; bytes = c->last_tiles * 8; break;
         case GSR_DEBUG_TILE_LIST: src = c->last_tile_list; bytes = c->stats.n_instances * 4; break;
-        case 5:  // (timing knob GSR_DEBUG_TDS & 8: the per-tile sort's block stamps, 8 words per block)
-            src = c->tds_stamps.p;
-            bytes = (int64_t)c->tds_stamps.cap * 8;
-            break;
-        case GSR_DEBUG_SLOT_KEYS:  // (the fused cull's slots are not compacted: all n)
-            src = c->keys_a.p;
-            bytes = (c->fused_cull && c->stats.n_visible > 0 ? c->stats.n_gaussians : c->stats.n_visible) * 4;
-            break;
         default: return set_error(GSR_ERR_INVALID, "unknown debug array");
     }
     if (!src || bytes == 0) return 0;

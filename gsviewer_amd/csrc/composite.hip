@@ -196,8 +196,6 @@ struct BinView {
     uint32_t* tile_keys;
     uint32_t* tile_vals;
     uint32_t n_vis;
-    const uint32_t* slot_keys;  // (fused binning with keys: see bin_scatter's kKeys)
-    uint32_t* inst_keys;
 };
 struct BinViews {
     BinView v[kMaxViews];
@@ -259,39 +257,6 @@ struct BinScatterLds {
 // almost single-lane.
 constexpr uint32_t kSerialTiles = 64;
 
-// The tile sort's key of an instance.  Plain: the tile id.  With coarse
-// depth bits (the per-tile depth sort's binning, cb > 0): (tile << cb) |
-// bucket, the bucket the top cb bits of the splat's depth key within the
-// frame's key range, so the stable tile sort leaves each tile's list in runs
-// of equal bucket (slot order inside a run) and the per-tile depth sort
-// (tile_sort.hip) sorts runs, not whole tiles.  The bits come for free: the
-// tile sort's passes are fixed by the tile id's width, their digits widen
-// to take cb more bits (TileBits, api.hip).
-struct InstKey {
-    uint32_t cb = 0;    // coarse depth bits (0: the tile id alone)
-    uint32_t kmin = 0;  // the frame's smallest visible key
-    uint32_t s0 = 0;    // bucket = (key - kmin) >> s0
-    const uint32_t* slot_keys = nullptr;
-    __device__ __forceinline__ uint32_t bucket(uint32_t r) const {
-        return cb ? min((slot_keys[r] - kmin) >> s0, (1u << cb) - 1u) : 0u;
-    }
-    __device__ __forceinline__ uint32_t of(uint32_t tile, uint32_t bk) const { return cb ? (tile << cb) | bk : tile; }
-};
-
-__device__ __forceinline__ InstKey inst_key(uint32_t cb, const uint32_t* __restrict__ key_range,
-                                            const uint32_t* __restrict__ slot_keys) {
-    InstKey ik;
-    if (!cb || !key_range || !slot_keys) return ik;
-    ik.cb = cb;
-    ik.slot_keys = slot_keys;
-    const uint32_t nk = key_range[0], kmax = key_range[1];
-    ik.kmin = ~nk;
-    const uint32_t B = kmax > ik.kmin ? 32u - (uint32_t)__clz(kmax - ik.kmin) : 0u;
-    if (kmax < ik.kmin) ik.kmin = 0u;  // nothing visible: no instances
-    ik.s0 = B > cb ? B - cb : 0u;
-    return ik;
-}
-
 // Instance idx (generation order: depth-sorted splats, each one's tiles
 // row-major) of block blk -> (tile key, record slot), given own_o: the
 // exclusive offsets of the block's threads' instances (thread t owns splats
@@ -301,7 +266,7 @@ __device__ __forceinline__ void instance_at(uint32_t idx, const uint32_t* own_o,
                                             const uint32_t* __restrict__ sorted_ids,
                                             const uint2* __restrict__ trect_sorted,
                                             const uint32_t* __restrict__ rect4_sorted, int tiles_x, uint32_t& key,
-                                            uint32_t& val, bool sorted_pos = false, const InstKey& ik = InstKey{}) {
+                                            uint32_t& val, bool sorted_pos = false) {
     uint32_t lo = 0, hi = kThreads;  // own_o[lo] <= idx < own_o[hi]
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -321,8 +286,8 @@ __device__ __forceinline__ void instance_at(uint32_t idx, const uint32_t* own_o,
             const uint32_t tx0 = tr.x & 0xffffu, tx1 = tr.x >> 16, ty0 = tr.y & 0xffffu;
             const uint32_t w = tx1 - tx0 + 1u;
             const uint32_t dy = local / w;
-            key = ik.of((ty0 + dy) * (uint32_t)tiles_x + tx0 + (local - dy * w), ik.bucket(r));
-            val = sorted_pos || !sorted_ids ? r : sorted_ids[r];
+            key = (ty0 + dy) * (uint32_t)tiles_x + tx0 + (local - dy * w);
+            val = sorted_pos ? r : sorted_ids[r];
             return;
         }
         local -= n;
@@ -340,7 +305,7 @@ __device__ __forceinline__ uint32_t block_max(uint32_t v, uint32_t* scratch) {
     return m;
 }
 
-// (sorted rect of depth-sorted splat r; sorted_ids null: slot r's)
+// (sorted rect of depth-sorted splat r)
 template <bool kPacked>
 __device__ __forceinline__ uint2 sorted_rect(const uint32_t* __restrict__ sorted_ids, const uint2* __restrict__ trect,
                                              const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis, uint32_t r,
@@ -348,7 +313,6 @@ __device__ __forceinline__ uint2 sorted_rect(const uint32_t* __restrict__ sorted
     if constexpr (kPacked) {
         return unpack_rect(rect4_sorted[r]);
     } else {
-        if (!sorted_ids) return trect[r];
         const uint2 tr = trect[sorted_ids[r]];  // (a record slot: not below n_vis with the fused cull)
         trect_sorted[r] = tr;
         return tr;
@@ -365,20 +329,18 @@ __device__ __forceinline__ void bin_hist(const uint32_t* __restrict__ sorted_ids
                                          const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis, int tiles_x,
                                          const PassArgs& pa, uint32_t* __restrict__ hist, uint32_t nbb,
                                          uint2* __restrict__ trect_sorted, uint32_t blk, uint32_t* h,
-                                         uint32_t* own, const InstKey& ik) {
+                                         uint32_t* own) {
     const Digit dg = digit_params(pa);
     const uint32_t radix = dg.mask + 1u;
     for (uint32_t d = threadIdx.x; d < radix; d += kThreads) h[d] = 0u;
     const uint32_t base = blk * kBinBlock + threadIdx.x;
     uint2 tr[kBinItems];
-    uint32_t bk[kBinItems];
     uint32_t nmax = 0;
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
         const uint32_t r = base + k * kThreads;
         tr[k] = r < n_vis ? sorted_rect<kPacked>(sorted_ids, trect, rect4_sorted, n_vis, r, trect_sorted)
                           : make_uint2(0xffffu, 0u);
-        bk[k] = ik.cb && rect_tiles(tr[k]) ? ik.bucket(r) : 0u;
         nmax = max(nmax, rect_tiles(tr[k]));
     }
     uint32_t* own_o = own;
@@ -388,7 +350,7 @@ __device__ __forceinline__ void bin_hist(const uint32_t* __restrict__ sorted_ids
             const uint32_t tx0 = tr[k].x & 0xffffu, tx1 = tr[k].x >> 16, ty0 = tr[k].y & 0xffffu, ty1 = tr[k].y >> 16;
             if (tx0 > tx1) continue;
             for (uint32_t ty = ty0; ty <= ty1; ++ty)
-                for (uint32_t tx = tx0; tx <= tx1; ++tx) atomicAdd(&h[dg.of(ik.of(ty * (uint32_t)tiles_x + tx, bk[k]))], 1u);
+                for (uint32_t tx = tx0; tx <= tx1; ++tx) atomicAdd(&h[dg.of(ty * (uint32_t)tiles_x + tx)], 1u);
         }
     } else {
         // thread t's instances in the consecutive layout: splats blk * kBinBlock + 4t .. 4t + 3
@@ -404,7 +366,7 @@ __device__ __forceinline__ void bin_hist(const uint32_t* __restrict__ sorted_ids
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < total; i += kThreads) {
             uint32_t key, val;
-            instance_at<kPacked>(i, own_o, blk, sorted_ids, trect_sorted, rect4_sorted, tiles_x, key, val, false, ik);
+            instance_at<kPacked>(i, own_o, blk, sorted_ids, trect_sorted, rect4_sorted, tiles_x, key, val);
             atomicAdd(&h[dg.of(key)], 1u);
         }
     }
@@ -417,20 +379,18 @@ __global__ __launch_bounds__(kThreads) void k_bin_hist(const uint32_t* __restric
                                                        const uint2* __restrict__ trect,
                                                        const uint32_t* __restrict__ rect4_sorted, uint32_t n_vis,
                                                        int tiles_x, PassArgs pa, uint32_t* __restrict__ hist,
-                                                       uint32_t nbb, uint2* __restrict__ trect_sorted, uint32_t cb,
-                                                       const uint32_t* __restrict__ key_range,
-                                                       const uint32_t* __restrict__ slot_keys) {
+                                                       uint32_t nbb, uint2* __restrict__ trect_sorted) {
     __shared__ uint32_t h[1 << kCB];
     __shared__ uint32_t own[kThreads + 1 + 2 * kThreads / 64];
     bin_hist<kPacked, kCB>(sorted_ids, trect, rect4_sorted, n_vis, tiles_x, pa, hist, nbb, trect_sorted, blockIdx.x,
-                           h, own, inst_key(cb, key_range, slot_keys));
+                           h, own);
 }
 
-// kKeys: each instance also carries its splat's depth key (sorted_keys, by
-// sorted position: with sorted_ids null, the slot keys) to inst_keys, for the
-// per-tile depth sort.  The window then stages each instance's sorted
-// position instead of its slot, and the writes look up both (this block's
-// 1024 splats: cache-hot).
+// kKeys: each instance also carries its splat's depth key (sorted_keys, in
+// depth order) to inst_keys, for the coarse depth order's run repair.  The
+// window then stages each instance's depth-sorted position instead of its
+// slot, and the writes look up both (this block's 1024 splats: cache-hot):
+// staging the keys as well took 16 KB more LDS (a block fewer per CU).
 template <bool kPacked, int kCB, bool kKeys = false>
 __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_ids,
                                             const uint2* __restrict__ trect_sorted,
@@ -440,7 +400,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
                                             uint32_t* __restrict__ tile_keys, uint32_t* __restrict__ tile_vals,
                                             uint32_t blk, BinScatterLds<kCB>& L,
                                             const uint32_t* __restrict__ sorted_keys = nullptr,
-                                            uint32_t* __restrict__ inst_keys = nullptr, const InstKey& ik = InstKey{}) {
+                                            uint32_t* __restrict__ inst_keys = nullptr) {
     constexpr int kCap = 1 << kCB;
     constexpr int kDpt = kCap / kThreads > 0 ? kCap / kThreads : 1;  // digits per thread
     constexpr int kWaveItems = kBinStage / (kThreads / 64);           // window items per wave
@@ -461,18 +421,17 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
     }
     // this thread's 4 consecutive depth-sorted splats
     const uint32_t base = blk * kBinBlock + threadIdx.x * kBinItems;
-    uint32_t id[kBinItems], bk[kBinItems];
+    uint32_t id[kBinItems];
     uint2 tr[kBinItems];
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < kBinItems; ++k) {
         const uint32_t r = base + k;
-        id[k] = kKeys || !sorted_ids ? r : r < n_vis ? sorted_ids[r] : 0u;  // kKeys: the sorted position
+        id[k] = kKeys ? r : r < n_vis ? sorted_ids[r] : 0u;  // kKeys: the sorted position
         if constexpr (kPacked)
             tr[k] = r < n_vis ? unpack_rect(rect4_sorted[r]) : make_uint2(0xffffu, 0u);
         else
             tr[k] = r < n_vis ? trect_sorted[r] : make_uint2(0xffffu, 0u);
-        bk[k] = ik.cb && rect_tiles(tr[k]) ? ik.bucket(r) : 0u;
         s += rect_tiles(tr[k]);
     }
     {  // global start of each digit's run of this block: digit base + the earlier blocks' counts
@@ -505,7 +464,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
             const uint32_t cnt = min((uint32_t)kBinStage, total - c0);
             for (uint32_t j = threadIdx.x; j < cnt; j += kThreads)
                 instance_at<kPacked>(c0 + j, L.own_o, blk, sorted_ids, trect_sorted, rect4_sorted, tiles_x, L.k[j],
-                                     L.v[j], kKeys, ik);
+                                     L.v[j], kKeys);
         } else if (o < c0 + (uint32_t)kBinStage && o + s > c0) {
             uint32_t idx = o;
 #pragma unroll
@@ -516,7 +475,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
                 for (uint32_t ty = ty0; ty <= ty1; ++ty)
                     for (uint32_t tx = tx0; tx <= tx1; ++tx, ++idx)
                         if (idx >= c0 && idx < c0 + (uint32_t)kBinStage) {
-                            L.k[idx - c0] = ik.of(ty * (uint32_t)tiles_x + tx, bk[k]);
+                            L.k[idx - c0] = ty * (uint32_t)tiles_x + tx;
                             L.v[idx - c0] = id[k];
                         }
             }
@@ -597,7 +556,7 @@ __device__ __forceinline__ void bin_scatter(const uint32_t* __restrict__ sorted_
             tile_keys[g] = kk;
             if constexpr (kKeys) {
                 const uint32_t r = L.v2[j];
-                tile_vals[g] = sorted_ids ? sorted_ids[r] : r;
+                tile_vals[g] = sorted_ids[r];
                 inst_keys[g] = sorted_keys[r];
             } else {
                 tile_vals[g] = L.v2[j];
@@ -623,12 +582,10 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(const uint32_t* __rest
                                                           uint32_t* __restrict__ tile_keys,
                                                           uint32_t* __restrict__ tile_vals,
                                                           const uint32_t* __restrict__ sorted_keys,
-                                                          uint32_t* __restrict__ inst_keys, uint32_t cb,
-                                                          const uint32_t* __restrict__ key_range) {
+                                                          uint32_t* __restrict__ inst_keys) {
     __shared__ BinScatterLds<kCB> L;
     bin_scatter<kPacked, kCB, kKeys>(sorted_ids, trect_sorted, rect4_sorted, n_vis, tiles_x, pa, hist_off, totals,
-                                     nbb, tile_keys, tile_vals, blockIdx.x, L, sorted_keys, inst_keys,
-                                     inst_key(cb, key_range, sorted_keys));
+                                     nbb, tile_keys, tile_vals, blockIdx.x, L, sorted_keys, inst_keys);
 }
 
 // Views of a group (blockIdx.y = view): hist / totals per view.
@@ -636,8 +593,6 @@ struct BinSortViews {
     BinView v[kMaxViews];
     uint32_t* hist[kMaxViews];
     const uint32_t* totals[kMaxViews];
-    const uint32_t* key_range[kMaxViews];  // (coarse depth bits: each view's frame key range)
-    uint32_t cb;
 };
 
 // Every view's count matrix has nbb (the largest view's blocks) columns; a
@@ -649,19 +604,17 @@ __global__ __launch_bounds__(kThreads) void k_bin_hist_views(BinSortViews vs, in
     __shared__ uint32_t own[kThreads + 1 + 2 * kThreads / 64];
     const BinView& v = vs.v[blockIdx.y];
     bin_hist<kPacked, kCB>(v.sorted_ids, v.trect, v.rect4_sorted, v.n_vis, tiles_x, pa, vs.hist[blockIdx.y], nbb,
-                           v.trect_sorted, blockIdx.x, h, own, inst_key(vs.cb, vs.key_range[blockIdx.y], v.slot_keys));
+                           v.trect_sorted, blockIdx.x, h, own);
 }
 
-template <bool kPacked, int kCB, bool kKeys>
+template <bool kPacked, int kCB>
 __global__ __launch_bounds__(kThreads) void k_bin_scatter_views(BinSortViews vs, int tiles_x, PassArgs pa,
                                                                 uint32_t nbb) {
     __shared__ BinScatterLds<kCB> L;
     const BinView& v = vs.v[blockIdx.y];
     if (blockIdx.x * kBinBlock >= v.n_vis) return;
-    bin_scatter<kPacked, kCB, kKeys>(v.sorted_ids, v.trect_sorted, v.rect4_sorted, v.n_vis, tiles_x, pa,
-                                     vs.hist[blockIdx.y], vs.totals[blockIdx.y], nbb, v.tile_keys, v.tile_vals,
-                                     blockIdx.x, L, v.slot_keys, v.inst_keys,
-                                     inst_key(vs.cb, vs.key_range[blockIdx.y], v.slot_keys));
+    bin_scatter<kPacked, kCB>(v.sorted_ids, v.trect_sorted, v.rect4_sorted, v.n_vis, tiles_x, pa, vs.hist[blockIdx.y],
+                              vs.totals[blockIdx.y], nbb, v.tile_keys, v.tile_vals, blockIdx.x, L);
 }
 
 // Tile ranges from the tile-sorted keys: kRangeItems consecutive instances per
@@ -671,18 +624,194 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter_views(BinSortViews vs,
 // compositors for CU slots.)
 constexpr int kRangeItems = 16;
 
-// (keys >> cb: the tile id of a key with coarse depth bits, InstKey.)
-// kRuns (the per-tile depth sort): every run of equal full keys longer than
-// kTdsCapWave is appended to big_runs as (start, length): the thread holding
-// its last instance finds its start by binary search (the keys ascend) and
-// takes a slot with one atomic add (a few hundred runs per frame at C2).
-template <bool kRuns, int kItems = kRangeItems>
+// The repair of one run of a coarse depth order, [i, i + L): instances of one
+// tile with equal coarse keys, in slot order (the stable coarse sort's).  The
+// exact order is (full key, slot); a run without a descent of the full key is
+// already in it.  Otherwise its (key, slot) pairs are copied to scratch and
+// each one is written at its rank.  One thread owns the run (the thread
+// holding its first instance), so its reads all precede its writes; other
+// threads read the run's slots only for their (tile, coarse key), which the
+// permutation leaves unchanged.  O(L^2), so only runs of at most kFixRunMax
+// instances: a longer one is listed for k_long_runs (tile_sort.hip), which
+// sorts it on chip in bounded time (round 4's unbounded form could spend
+// ~5e8 serial steps on one dense tile).
+__device__ __noinline__ void fix_run(const uint32_t* __restrict__ keys, uint32_t n, uint32_t* vals,
+                                     const uint32_t* __restrict__ inst_keys, uint32_t* __restrict__ scratch_keys,
+                                     uint32_t* __restrict__ scratch_vals, uint32_t* __restrict__ long_starts,
+                                     uint32_t* __restrict__ long_count, uint32_t i, uint32_t tile, uint32_t cv,
+                                     uint32_t kmin, uint32_t s0) {
+    uint32_t fprev = inst_keys[i];
+    uint32_t L = 1;
+    bool descent = false;
+    for (uint32_t q = i + 1; q < n; ++q) {
+        if (keys[q] != tile) break;
+        const uint32_t f = inst_keys[q];
+        if (((f - kmin) >> s0) != cv) break;
+        descent |= f < fprev;
+        fprev = f;
+        if (++L > kFixRunMax) {  // a long run: k_long_runs finds its end and sorts it
+            long_starts[atomicAdd(long_count, 1u)] = i;
+            return;
+        }
+    }
+    if (!descent) return;
+    for (uint32_t r = 0; r < L; ++r) {
+        scratch_vals[i + r] = vals[i + r];
+        scratch_keys[i + r] = inst_keys[i + r];
+    }
+    for (uint32_t r = 0; r < L; ++r) {
+        const uint32_t kr = scratch_keys[i + r], vr = scratch_vals[i + r];
+        uint32_t rank = 0;
+        for (uint32_t q = 0; q < L; ++q) {
+            const uint32_t kq = scratch_keys[i + q], vq = scratch_vals[i + q];
+            rank += (kq < kr || (kq == kr && vq < vr)) ? 1u : 0u;
+        }
+        vals[i + rank] = vr;
+    }
+}
+
+// The thread's kRangeItems instances: every run of equal (tile, coarse key)
+// that starts among them is repaired, in registers over a window of the
+// thread's items and the kFixExtra after them (all loads issued at once: a
+// chain of dependent loads per run cost ~200 us at C2).  Runs are short (C2,
+// 16 coarse bits: 41 % of the instances in runs, the longest 8; 22 bits: 1 %,
+// 4), so an odd-even transposition sort restricted to pairs inside one run,
+// as many rounds as the longest run, puts each in (full key, slot) order.  A
+// run that reaches the window's end is left to fix_run (global memory).
+constexpr int kFixExtra = 8;
+// instances per thread of the repairing kernel (GSR_FIX_ITEMS build knob): 8
+// (twice the waves of 16, the window's loads overlap more): 13.9 -> 10.8 us,
+// 12: 12.0 (profiles/r4_s32/c9)
+#ifndef GSR_FIX_ITEMS
+#define GSR_FIX_ITEMS 8
+#endif
+constexpr int kFixItems = GSR_FIX_ITEMS;
+static_assert(kFixItems % 4 == 0 && kFixItems + kFixExtra <= 32, "run masks are 32-bit");
+
+template <int kItems>
+__device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ keys, uint32_t n, const RunFix& fx,
+                                                uint32_t base, const uint32_t (&k)[kItems], uint32_t prev) {
+    constexpr int kFixWin = kItems + kFixExtra;
+    uint32_t kw[kFixWin], vw[kFixWin], fw[kFixWin];
+    // the window's slots: with carried keys only once a run needs sorting (most windows' runs are in order)
+    auto load_vals = [&]() {
+        if (base + kFixWin <= n) {
+            const uint4* pv = reinterpret_cast<const uint4*>(fx.vals + base);  // (base: a multiple of 16)
+#pragma unroll
+            for (int q = 0; q < kFixWin / 4; ++q) {
+                const uint4 v = pv[q];
+                vw[4 * q] = v.x; vw[4 * q + 1] = v.y; vw[4 * q + 2] = v.z; vw[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kFixWin; ++j) vw[j] = base + j < n ? fx.vals[base + j] : 0u;
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) kw[j] = k[j];
+    if (base + kFixWin <= n) {
+        const uint4* pk = reinterpret_cast<const uint4*>(keys + base + kItems);
+#pragma unroll
+        for (int q = 0; q < kFixExtra / 4; ++q) {
+            const uint4 v = pk[q];
+            kw[kItems + 4 * q] = v.x; kw[kItems + 4 * q + 1] = v.y;
+            kw[kItems + 4 * q + 2] = v.z; kw[kItems + 4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = kItems; j < kFixWin; ++j) kw[j] = base + j < n ? keys[base + j] : 0xffffffffu;
+    }
+    // the keys carried with the instances (binning + tile sort payload): coalesced
+    if (base + kFixWin <= n) {
+        const uint4* pf = reinterpret_cast<const uint4*>(fx.inst_keys + base);
+#pragma unroll
+        for (int q = 0; q < kFixWin / 4; ++q) {
+            const uint4 v = pf[q];
+            fw[4 * q] = v.x; fw[4 * q + 1] = v.y; fw[4 * q + 2] = v.z; fw[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < kFixWin; ++j) fw[j] = base + j < n ? fx.inst_keys[base + j] : 0u;
+    }
+    const uint32_t fprev = base > 0 ? fx.inst_keys[base - 1] : 0u;
+    uint32_t kmin;  // (the window's loads are in flight meanwhile)
+    const uint32_t s0 = coarse_shift(fx.key_range, fx.coarse, kmin);
+    if (s0 == 0u) return;  // the coarse sort was exact
+    // same bit j: items j and j + 1 are one run (both valid, same tile and coarse key)
+    uint32_t same = 0;
+#pragma unroll
+    for (int j = 0; j + 1 < kFixWin; ++j)
+        if (base + j + 1 < n && kw[j] == kw[j + 1] && ((fw[j] - kmin) >> s0) == ((fw[j + 1] - kmin) >> s0))
+            same |= 1u << j;
+    // own bit j: item j is in a run that starts among the thread's items
+    const bool cont0 = base > 0 && prev == kw[0] && ((fprev - kmin) >> s0) == ((fw[0] - kmin) >> s0);
+    uint32_t own = cont0 ? 0u : 1u;
+#pragma unroll
+    for (int j = 1; j < kFixWin; ++j) {
+        const bool in = ((same >> (j - 1)) & 1u) ? ((own >> (j - 1)) & 1u) != 0u : j < kItems;
+        if (in) own |= 1u << j;
+    }
+    // a run that may go on past the window: fix_run from its start, out of the register sort
+    if ((own >> (kFixWin - 1)) & 1u) {
+        int st = kFixWin - 1;
+#pragma unroll
+        for (int j = kFixWin - 2; j >= 0; --j)
+            if (st == j + 1 && ((same >> j) & 1u)) st = j;
+        own &= (1u << st) - 1u;
+        uint32_t kst = 0, fst = 0;  // items st (selected: a dynamic index would put the arrays in scratch)
+#pragma unroll
+        for (int j = 0; j < kFixWin; ++j)
+            if (j == st) kst = kw[j], fst = fw[j];
+        fix_run(keys, n, fx.vals, fx.inst_keys, fx.scratch_keys, fx.scratch_vals, fx.long_starts, fx.long_count,
+                base + (uint32_t)st, kst, (fst - kmin) >> s0, kmin, s0);
+    }
+    const uint32_t pairs = same & own;  // adjacent pairs inside one owned run
+    uint32_t descent = 0;
+#pragma unroll
+    for (int j = 0; j + 1 < kFixWin; ++j)
+        if (((pairs >> j) & 1u) && fw[j] > fw[j + 1]) descent = 1u;  // slots ascend in a run: only keys descend
+#ifdef GSR_EXP_FIX_NOSORT  // experiment build: the window's loads and tests only (timing; lists unrepaired)
+    asm volatile("" ::"v"(descent));
+    return;
+#endif
+    if (!descent) return;
+    load_vals();
+    // the longest owned run: rounds of the transposition sort
+    uint32_t len = 1, rounds = 1;
+#pragma unroll
+    for (int j = 0; j + 1 < kFixWin; ++j) {
+        len = ((pairs >> j) & 1u) ? len + 1u : 1u;
+        rounds = max(rounds, len);
+    }
+    uint32_t v0[kFixWin];
+#pragma unroll
+    for (int j = 0; j < kFixWin; ++j) v0[j] = vw[j];
+    for (uint32_t r = 0; r < rounds; ++r) {
+#pragma unroll
+        for (int j = 0; j + 1 < kFixWin; ++j) {
+            if ((j & 1) != (int)(r & 1u) || !((pairs >> j) & 1u)) continue;
+            const bool gt = fw[j] > fw[j + 1] || (fw[j] == fw[j + 1] && vw[j] > vw[j + 1]);
+            const uint32_t fa = fw[j], va = vw[j];
+            fw[j] = gt ? fw[j + 1] : fa;
+            vw[j] = gt ? vw[j + 1] : va;
+            fw[j + 1] = gt ? fa : fw[j + 1];
+            vw[j + 1] = gt ? va : vw[j + 1];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kFixWin; ++j)
+        if (((own >> j) & 1u) && vw[j] != v0[j]) fx.vals[base + j] = vw[j];
+}
+
+// kFix: the coarse depth order's run repair (a separate instantiation: its
+// registers (153 VGPRs) made the plain kernel wait for room beside the
+// compositors in flight)
+template <bool kFix, int kItems = kFix ? kFixItems : kRangeItems>
 __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, uint32_t n, uint2* __restrict__ ranges,
-                                            uint32_t t, uint32_t cb, uint2* __restrict__ big_runs,
-                                            uint32_t* __restrict__ big_count) {
+                                            uint32_t t, const RunFix& fx) {
     const uint32_t base = t * kItems;
     if (base >= n) return;
-    uint32_t k[kItems];  // full keys
+    uint32_t k[kItems];
     if (base + kItems <= n) {
         const uint4* p = reinterpret_cast<const uint4*>(keys + base);  // (base: a multiple of 16)
 #pragma unroll
@@ -696,51 +825,36 @@ __device__ __forceinline__ void tile_ranges(const uint32_t* __restrict__ keys, u
     }
     const uint32_t prev = base > 0 ? keys[base - 1] : 0xffffffffu;
     const uint32_t next = base + kItems < n ? keys[base + kItems] : 0xffffffffu;
+    // the run repair first: its window loads are issued before the range stores
+    if constexpr (kFix) fix_coarse_runs<kItems>(keys, n, fx, base, k, prev);
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
         const uint32_t i = base + j;
         if (i >= n) break;
         const uint32_t before = j == 0 ? prev : k[j - 1];
         const uint32_t after = (j + 1 < kItems) ? (i + 1 < n ? k[j + 1] : 0xffffffffu) : next;
-        const uint32_t tile = k[j] >> cb;
-        if (i == 0 || (before >> cb) != tile) ranges[tile].x = i;
-        if (i == n - 1 || (after >> cb) != tile) ranges[tile].y = i + 1;
-        if constexpr (kRuns) {
-            if ((i == n - 1 || after != k[j]) && i >= kTdsCapWave && keys[i - kTdsCapWave] == k[j]) {
-                uint32_t lo = 0, hi = i - kTdsCapWave;  // keys[hi] == k[j]: the run's start is in [0, hi]
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (keys[mid] < k[j]) lo = mid + 1;
-                    else hi = mid;
-                }
-                const uint32_t slot = atomicAdd(big_count, 1u);
-                big_runs[slot] = make_uint2(lo, i + 1 - lo);
-            }
-        }
+        if (i == 0 || before != k[j]) ranges[k[j]].x = i;
+        if (i == n - 1 || after != k[j]) ranges[k[j]].y = i + 1;
     }
 }
 
-template <bool kRuns>
+template <bool kFix>
 __global__ __launch_bounds__(kThreads) void k_tile_ranges(const uint32_t* __restrict__ keys, uint32_t n,
-                                                          uint2* __restrict__ ranges, uint32_t cb,
-                                                          uint2* __restrict__ big_runs, uint32_t* __restrict__ big_count) {
-    tile_ranges<kRuns>(keys, n, ranges, blockIdx.x * kThreads + threadIdx.x, cb, big_runs, big_count);
+                                                          uint2* __restrict__ ranges, RunFix fx) {
+    tile_ranges<kFix>(keys, n, ranges, blockIdx.x * kThreads + threadIdx.x, fx);
 }
 
 struct RangeViews {
     const uint32_t* keys[kMaxViews];
     uint2* ranges[kMaxViews];
     uint32_t n[kMaxViews];
-    uint2* big_runs[kMaxViews];
-    uint32_t* big_count[kMaxViews];
-    uint32_t cb;
+    RunFix fix[kMaxViews];
 };
 
-template <bool kRuns>
+template <bool kFix>
 __global__ __launch_bounds__(kThreads) void k_tile_ranges_views(RangeViews vs) {
     const int v = blockIdx.y;
-    tile_ranges<kRuns>(vs.keys[v], vs.n[v], vs.ranges[v], blockIdx.x * kThreads + threadIdx.x, vs.cb,
-                       vs.big_runs[v], vs.big_count[v]);
+    tile_ranges<kFix>(vs.keys[v], vs.n[v], vs.ranges[v], blockIdx.x * kThreads + threadIdx.x, vs.fix[v]);
 }
 
 struct CompositeArgs {
@@ -2049,84 +2163,58 @@ size_t bin_hist_elems(size_t n_vis, int tbits, int passes) {
     return ((n_vis + kBinBlock - 1) / kBinBlock) * ((size_t)1 << ((tbits + passes - 1) / passes));
 }
 
-// The binning's digit parameters (tile sort pass 0) and its blocks.
-static int bin_pass0(const BinSortArgs& a, PassArgs& pa, int& w, bool scatter) {
-    // (one tile: a single digit value, generation order kept)
-    const int tb = (a.tbits > 0 ? a.tbits : 1) + (int)a.coarse_bits;
-    if (a.coarse_bits && (!a.key_range || !a.slot_keys || a.sorted_ids))
-        return set_error(GSR_ERR_INVALID, "binning: coarse depth bits need slot order, the slot keys and the key range");
-    const int ps = a.passes > 0 ? a.passes : 1;
-    w = (tb + ps - 1) / ps;
+int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted,
+                          uint32_t n_vis, int tiles_x, int tbits, int passes, uint32_t* hist, uint32_t* totals,
+                          uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s,
+                          const uint32_t* sorted_keys, uint32_t* inst_keys) {
+    if (n_vis == 0) return GSR_OK;
+    const int tb = tbits > 0 ? tbits : 1;  // one tile: a single digit value, generation order kept
+    const int ps = passes > 0 ? passes : 1;
+    const int w = (tb + ps - 1) / ps;
     if (w > 11) return set_error(GSR_ERR_INVALID, "binning: tile digit wider than 11 bits");
-    if (!a.sorted_ids && (a.rect4_sorted || (scatter && (!a.slot_keys || !a.inst_keys))))
-        return set_error(GSR_ERR_INVALID, "binning: slot order takes the plain rects and carries the keys");
-    pa = PassArgs{nullptr, (uint32_t)tb, (uint32_t)ps, 0u};
-    return GSR_OK;
-}
-
-int launch_binning_hist(const BinSortArgs& a, hipStream_t s) {
-    if (a.n_vis == 0) return GSR_OK;
-    PassArgs pa;
-    int w, rc;
-    if ((rc = bin_pass0(a, pa, w, false))) return rc;
-    const uint32_t nbb = (a.n_vis + kBinBlock - 1) / kBinBlock;
-    const bool packed = a.rect4_sorted != nullptr;
-    // slot order: the rects are read where they lie (trect_sorted aliases trect, nothing is written to it)
-    uint2* tsorted = a.sorted_ids ? a.trect_sorted : const_cast<uint2*>(a.trect);
-#define GSR_BIN_HIST(P, CB)                                                                                  \
-    k_bin_hist<P, CB><<<nbb, kThreads, 0, s>>>(a.sorted_ids, a.trect, a.rect4_sorted, a.n_vis, a.tiles_x, pa, \
-                                               a.hist, nbb, tsorted, a.coarse_bits, a.key_range, a.slot_keys)
+    const uint32_t nbb = (n_vis + kBinBlock - 1) / kBinBlock;
+    const PassArgs pa{nullptr, (uint32_t)tb, (uint32_t)ps, 0u};
+    const bool packed = rect4_sorted != nullptr;
+#define GSR_BIN_HIST(P, CB)                                                                                 \
+    k_bin_hist<P, CB><<<nbb, kThreads, 0, s>>>(sorted_ids, trect, rect4_sorted, n_vis, tiles_x, pa, hist, nbb, \
+                                               trect_sorted)
+#define GSR_BIN_SCATTER(P, CB)                                                                                  \
+    do {                                                                                                        \
+        if (inst_keys)                                                                                          \
+            k_bin_scatter<P, CB, true><<<nbb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis,     \
+                                                                tiles_x, pa, hist, totals, nbb, tile_keys,         \
+                                                                tile_vals, sorted_keys, inst_keys);                \
+        else                                                                                                    \
+            k_bin_scatter<P, CB, false><<<nbb, kThreads, 0, s>>>(sorted_ids, trect_sorted, rect4_sorted, n_vis,    \
+                                                                 tiles_x, pa, hist, totals, nbb, tile_keys,        \
+                                                                 tile_vals, nullptr, nullptr);                     \
+    } while (0)
     if (w <= 8) {
         if (packed) GSR_BIN_HIST(true, 8); else GSR_BIN_HIST(false, 8);
     } else {
         if (packed) GSR_BIN_HIST(true, 11); else GSR_BIN_HIST(false, 11);
     }
-#undef GSR_BIN_HIST
     GSR_LAUNCH_CHECK("bin_hist");
-    return radix_offsets(a.hist, nbb, (int)pa.bits, (int)pa.passes, 0, a.totals, s);
-}
-
-int launch_binning_scatter(const BinSortArgs& a, hipStream_t s) {
-    if (a.n_vis == 0) return GSR_OK;
-    PassArgs pa;
-    int w, rc;
-    if ((rc = bin_pass0(a, pa, w, true))) return rc;
-    const uint32_t nbb = (a.n_vis + kBinBlock - 1) / kBinBlock;
-    const bool packed = a.rect4_sorted != nullptr;
-    const uint2* tsorted = a.sorted_ids ? a.trect_sorted : a.trect;
-#define GSR_BIN_SCATTER(P, CB)                                                                                      \
-    do {                                                                                                            \
-        if (a.inst_keys)                                                                                            \
-            k_bin_scatter<P, CB, true><<<nbb, kThreads, 0, s>>>(a.sorted_ids, tsorted, a.rect4_sorted, a.n_vis,     \
-                                                                a.tiles_x, pa, a.hist, a.totals, nbb, a.tile_keys,  \
-                                                                a.tile_vals, a.slot_keys, a.inst_keys,              \
-                                                                a.coarse_bits, a.key_range);                        \
-        else                                                                                                        \
-            k_bin_scatter<P, CB, false><<<nbb, kThreads, 0, s>>>(a.sorted_ids, tsorted, a.rect4_sorted, a.n_vis,    \
-                                                                 a.tiles_x, pa, a.hist, a.totals, nbb, a.tile_keys, \
-                                                                 a.tile_vals, nullptr, nullptr, 0u, nullptr);       \
-    } while (0)
+    int rc;
+    if ((rc = radix_offsets(hist, nbb, tb, ps, 0, totals, s))) return rc;
     if (w <= 8) {
         if (packed) GSR_BIN_SCATTER(true, 8); else GSR_BIN_SCATTER(false, 8);
     } else {
         if (packed) GSR_BIN_SCATTER(true, 11); else GSR_BIN_SCATTER(false, 11);
     }
-#undef GSR_BIN_SCATTER
     GSR_LAUNCH_CHECK("bin_scatter");
+#undef GSR_BIN_HIST
+#undef GSR_BIN_SCATTER
     return GSR_OK;
 }
 
-int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, hipStream_t s, uint32_t cb,
-                       uint2* big_runs, uint32_t* big_count) {
+int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, const RunFix& fix, hipStream_t s) {
     if (n_dup == 0) return GSR_OK;
-    if (big_runs && !big_count) return set_error(GSR_ERR_INVALID, "tile ranges: long runs need their counter");
-    const uint32_t per_block = kThreads * kRangeItems;
-    if (big_runs)
-        k_tile_ranges<true><<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, cb,
-                                                                                   big_runs, big_count);
+    const uint32_t per_block = kThreads * (fix.coarse ? kFixItems : kRangeItems);
+    if (fix.coarse)
+        k_tile_ranges<true><<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, fix);
     else
-        k_tile_ranges<false><<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, cb,
-                                                                                    nullptr, nullptr);
+        k_tile_ranges<false><<<(n_dup + per_block - 1) / per_block, kThreads, 0, s>>>(tile_keys, n_dup, ranges, fix);
     GSR_LAUNCH_CHECK("tile_ranges");
     return GSR_OK;
 }
@@ -2273,49 +2361,26 @@ int launch_binning_views(FinishView* views, int k, int tiles_x, uint32_t stage_l
     return GSR_OK;
 }
 
-// A group's fused binning (views of one frame size), in the same two halves.
-static int bin_views_args(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tbits,
-                          int passes, BinSortViews& bv, uint32_t& nbb, PassArgs& pa, int& w, bool scatter,
-                          uint32_t coarse_bits, const uint32_t* const* key_range) {
-    bv = BinSortViews{};
-    bv.cb = coarse_bits;
-    nbb = 0;
+int launch_binning_sorted_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
+                                int tbits, int passes, hipStream_t s) {
+    BinSortViews bv{};
+    uint32_t nbb = 0;
     for (int i = 0; i < k; ++i) {
         const FinishView& f = views[i];
-        // slot order: the rects are read where they lie
-        uint2* tsorted = f.sorted_ids ? f.trect_sorted : const_cast<uint2*>(f.trect);
-        bv.v[i] = BinView{f.sorted_ids, f.trect, f.rect4_sorted, tsorted, f.bin_tmp, f.tile_keys, f.tile_vals,
-                          f.n_vis, f.slot_keys, f.inst_keys};
+        bv.v[i] = BinView{f.sorted_ids, f.trect, f.rect4_sorted, f.trect_sorted, f.bin_tmp, f.tile_keys, f.tile_vals,
+                          f.n_vis};
         bv.hist[i] = hist[i];
         bv.totals[i] = totals[i];
-        bv.key_range[i] = key_range ? key_range[i] : nullptr;
-        if (coarse_bits && (!bv.key_range[i] || !f.slot_keys || f.sorted_ids))
-            return set_error(GSR_ERR_INVALID, "binning: coarse depth bits need slot order, the slot keys and the key range");
-        if ((f.rect4_sorted != nullptr) != (views[0].rect4_sorted != nullptr) ||
-            (scatter && (f.inst_keys != nullptr) != (views[0].inst_keys != nullptr)))
-            return set_error(GSR_ERR_INVALID, "binning: packed rectangles or carried keys on some views only");
-        if (!f.sorted_ids && (f.rect4_sorted || (scatter && (!f.slot_keys || !f.inst_keys))))
-            return set_error(GSR_ERR_INVALID, "binning: slot order takes the plain rects and carries the keys");
+        if ((f.rect4_sorted != nullptr) != (views[0].rect4_sorted != nullptr))
+            return set_error(GSR_ERR_INVALID, "binning: packed rectangles on some views only");
         nbb = std::max(nbb, (f.n_vis + kBinBlock - 1) / kBinBlock);
     }
-    const int tb = (tbits > 0 ? tbits : 1) + (int)coarse_bits;
-    const int ps = passes > 0 ? passes : 1;
-    w = (tb + ps - 1) / ps;
-    if (w > 11) return set_error(GSR_ERR_INVALID, "binning: tile digit wider than 11 bits");
-    pa = PassArgs{nullptr, (uint32_t)tb, (uint32_t)ps, 0u};
-    return GSR_OK;
-}
-
-int launch_binning_hist_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
-                              int tbits, int passes, hipStream_t s, uint32_t coarse_bits,
-                              const uint32_t* const* key_range) {
-    BinSortViews bv;
-    uint32_t nbb;
-    PassArgs pa;
-    int w, rc;
-    if ((rc = bin_views_args(views, hist, totals, k, tbits, passes, bv, nbb, pa, w, false, coarse_bits, key_range)))
-        return rc;
     if (nbb == 0) return GSR_OK;
+    const int tb = tbits > 0 ? tbits : 1;
+    const int ps = passes > 0 ? passes : 1;
+    const int w = (tb + ps - 1) / ps;
+    if (w > 11) return set_error(GSR_ERR_INVALID, "binning: tile digit wider than 11 bits");
+    const PassArgs pa{nullptr, (uint32_t)tb, (uint32_t)ps, 0u};
     const bool packed = views[0].rect4_sorted != nullptr;
     const dim3 grid(nbb, (unsigned)k);
     if (w <= 8) {
@@ -2326,55 +2391,34 @@ int launch_binning_hist_views(FinishView* views, uint32_t* const* hist, uint32_t
         else k_bin_hist_views<false, 11><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
     }
     GSR_LAUNCH_CHECK("bin_hist_views");
-    return radix_offsets_views(hist, totals, k, nbb, (int)pa.bits, (int)pa.passes, 0, s);
-}
-
-int launch_binning_scatter_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k,
-                                 int tiles_x, int tbits, int passes, hipStream_t s, uint32_t coarse_bits,
-                                 const uint32_t* const* key_range) {
-    BinSortViews bv;
-    uint32_t nbb;
-    PassArgs pa;
-    int w, rc;
-    if ((rc = bin_views_args(views, hist, totals, k, tbits, passes, bv, nbb, pa, w, true, coarse_bits, key_range)))
-        return rc;
-    if (nbb == 0) return GSR_OK;
-    const bool packed = views[0].rect4_sorted != nullptr;
-    const bool keys = views[0].inst_keys != nullptr;
-    const dim3 grid(nbb, (unsigned)k);
-#define GSR_BIN_SCATTER_V(P, CB)                                                                   \
-    do {                                                                                           \
-        if (keys) k_bin_scatter_views<P, CB, true><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);  \
-        else k_bin_scatter_views<P, CB, false><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);      \
-    } while (0)
+    int rc;
+    if ((rc = radix_offsets_views(hist, totals, k, nbb, tb, ps, 0, s))) return rc;
     if (w <= 8) {
-        if (packed) GSR_BIN_SCATTER_V(true, 8); else GSR_BIN_SCATTER_V(false, 8);
+        if (packed) k_bin_scatter_views<true, 8><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+        else k_bin_scatter_views<false, 8><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
     } else {
-        if (packed) GSR_BIN_SCATTER_V(true, 11); else GSR_BIN_SCATTER_V(false, 11);
+        if (packed) k_bin_scatter_views<true, 11><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
+        else k_bin_scatter_views<false, 11><<<grid, kThreads, 0, s>>>(bv, tiles_x, pa, nbb);
     }
-#undef GSR_BIN_SCATTER_V
     GSR_LAUNCH_CHECK("bin_scatter_views");
     return GSR_OK;
 }
 
-int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s, uint32_t cb) {
+int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s) {
     RangeViews rv{};
-    rv.cb = cb;
     uint32_t n_max = 0;
-    const bool runs = views[0].big_runs != nullptr;
+    bool fix = false;
     for (int i = 0; i < k; ++i) {
         rv.keys[i] = views[i].tile_keys;
         rv.ranges[i] = views[i].ranges;
         rv.n[i] = views[i].n_dup;
-        rv.big_runs[i] = views[i].big_runs;
-        rv.big_count[i] = views[i].big_count;
-        if ((views[i].big_runs != nullptr) != runs || (runs && !views[i].big_count))
-            return set_error(GSR_ERR_INVALID, "tile ranges: long runs on some views only");
+        rv.fix[i] = views[i].fix;
+        fix |= views[i].fix.coarse != 0;
         n_max = std::max(n_max, views[i].n_dup);
     }
     if (n_max == 0) return GSR_OK;
-    const uint32_t per_block = kThreads * kRangeItems;
-    if (runs)
+    const uint32_t per_block = kThreads * (fix ? kFixItems : kRangeItems);
+    if (fix)
         k_tile_ranges_views<true><<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);
     else
         k_tile_ranges_views<false><<<dim3((n_max + per_block - 1) / per_block, (unsigned)k), kThreads, 0, s>>>(rv);

@@ -197,6 +197,11 @@ struct PassArgs {
     // keys are read (not the device count) and keys outside {kmin, kmax}
     // (culled slots, key 0xffffffff) are dropped; later passes see only V
     uint32_t drop = 0;
+    // Coarse depth order (the frame's depth sort): only the top `coarse` bits
+    // of the B-bit key range are sorted (0: all B).  Equal coarse keys keep
+    // their input (slot) order; tile_ranges restores the exact order inside
+    // each tile's list (RunFix).
+    uint32_t coarse = 0;
 };
 
 struct Digit {
@@ -208,7 +213,7 @@ struct Digit {
 
 __device__ __forceinline__ Digit digit_params(const PassArgs& p) {
     Digit d;
-    uint32_t B;
+    uint32_t B, s0 = 0;
     if (p.key_range) {
         d.kmin = ~p.key_range[0];
         const uint32_t kmax = p.key_range[1];
@@ -216,15 +221,29 @@ __device__ __forceinline__ Digit digit_params(const PassArgs& p) {
         // an empty range ({0, 0}: nothing visible) keeps no key: every slot is then culled (0xffffffff)
         d.lim = kmax >= d.kmin ? kmax - d.kmin : 0xfffffffeu;
         if (kmax < d.kmin) d.kmin = 0u;
+        if (p.coarse && B > p.coarse) {
+            s0 = B - p.coarse;
+            B = p.coarse;
+        }
     } else {
         d.kmin = 0u;
         d.lim = 0xffffffffu;
         B = p.bits;
     }
     d.w = max(1u, (B + p.passes - 1u) / p.passes);
-    d.shift = p.pass * d.w;
+    d.shift = s0 + p.pass * d.w;
     d.mask = (1u << d.w) - 1u;
     return d;
+}
+
+// kmin and the coarse shift of the frame's depth sort (digit_params, PassArgs::coarse)
+// (0 also for an exact sort, coarse == 0: nothing to repair)
+__device__ __forceinline__ uint32_t coarse_shift(const uint32_t* key_range, uint32_t coarse, uint32_t& kmin) {
+    kmin = ~key_range[0];
+    const uint32_t kmax = key_range[1];
+    const uint32_t B = kmax > kmin ? 32u - (uint32_t)__clz(kmax - kmin) : 0u;
+    if (kmax < kmin) kmin = 0u;
+    return coarse && B > coarse ? B - coarse : 0u;
 }
 
 // Lanes of the wave holding the same w-bit digit (only `valid` lanes).
@@ -283,6 +302,8 @@ struct RadixViewArgs {
     uint32_t** pay_io = nullptr;
     uint32_t** pay_alt = nullptr;
     bool drop_first = false;  // see radix_sort_pairs
+    uint32_t coarse = 0;      // see PassArgs::coarse
+    bool keys_last = true;    // the last pass writes the sorted keys (else keys_io keeps its input)
 };
 int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size_t n, int bits, int passes,
                            hipStream_t s, int first_pass = 0);
@@ -302,14 +323,13 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
                      int bits, int passes, const uint32_t* key_range, uint32_t* tmp,
                      uint32_t* totals, hipStream_t s, const uint2* rect_in = nullptr,
                      uint32_t** pay_io = nullptr, uint32_t** pay_alt = nullptr, int first_pass = 0,
-                     bool drop_first = false);
+                     bool drop_first = false, uint32_t coarse = 0, bool keys_last = true);
 // drop_first (needs key_range): the keys are the fused cull's n slots; the
 // first pass reads all n and drops the culled ones (PassArgs::drop), later
 // passes run over the device count n_dev = V.
-// Payload (pay_io non-null): a 32-bit word travels with each pair, read from
-// *pay_io (or, with rect_in non-null, the first pass packs the tile rectangles
-// rect_in[n] (uint2, in the input order) to 32 bits: pack_rect, frames of at
-// most 256 x 256 tiles); the sorted payload ends in *pay_io.
+// Payload (rect_in non-null): the tile rectangles rect_in[n] (uint2, in the
+// input order) travel with the pairs packed to 32 bits (pack_rect: frames of
+// at most 256 x 256 tiles); the sorted packed rectangles end in *pay_io.
 constexpr int kPackedRectTiles = 256;
 
 // scene.hip
@@ -412,69 +432,48 @@ uint32_t clamp_stage_limit(long v);
 int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted, uint32_t n_vis,
                    int tiles_x, uint32_t* tmp, uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals,
                    uint32_t stage_limit, hipStream_t s);
-// cb: the keys' coarse depth bits (InstKey; the tile id is key >> cb).  big_runs
-// (nullable): every run of equal keys longer than kTdsCapWave is appended as
-// (start, length), *big_count (zeroed per frame) counting them, for the per-tile depth sort.
-int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, hipStream_t s, uint32_t cb = 0,
-                       uint2* big_runs = nullptr, uint32_t* big_count = nullptr);
+// Repair of a coarse depth order inside the tile lists (k_tile_ranges): runs of
+// one tile's instances with equal coarse depth keys are put in (full key, slot)
+// order, in place.  coarse == 0 (an exact depth sort): nothing to repair.
+// Runs longer than kFixRunMax that reach past a thread's register window are
+// not repaired there: their starts go to long_starts (*long_count, zeroed per
+// frame) and launch_long_runs sorts them (tile_sort.hip).
+struct RunFix {
+    uint32_t* vals;             // the tile list (slots), repaired in place
+    const uint32_t* key_range;  // the frame's {~kmin, kmax}
+    uint32_t coarse;
+    uint32_t* scratch_keys;     // n_dup words each, free at this point (the tile sort's alternates)
+    uint32_t* scratch_vals;
+    uint32_t* inst_keys = nullptr;     // each list position's depth key (binning + tile sort payload)
+    uint32_t* long_starts = nullptr;   // long_runs_elems(n_dup) words: long_run_cap starts, then their lengths
+    uint32_t* long_count = nullptr;
+};
+// runs repaired by one thread (O(L^2) steps, L + 1 serial scan loads) at most this long
+constexpr uint32_t kFixRunMax = 16;
+inline size_t long_run_cap(size_t n_dup) { return n_dup / (kFixRunMax + 1) + 1; }
+inline size_t long_runs_elems(size_t n_dup) { return 2 * long_run_cap(n_dup); }
+int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, const RunFix& fix,
+                       hipStream_t s);
+// tile_sort.hip: the coarse order's long runs (RunFix::long_starts), each
+// bounded by a 64-way search from its start (runs are stretches of one tile's
+// list with equal coarse key, ranges[tile] bounds them) and sorted by (full
+// key, slot) on chip: up to 1024 instances by one wave, up to 24576 by a
+// 1024-thread block in registers, longer ones by a block through the scratch
+// buffers.  A fixed grid takes the listed runs in turn and exits at once when
+// there are none.
+int launch_long_runs(const uint32_t* tile_keys, uint32_t n_dup, const uint2* ranges, const RunFix& fix,
+                     hipStream_t s);
 // The binning with the tile sort's first radix pass fused in (composite.hip,
 // k_bin_hist / k_bin_scatter): the instances end in (tile_keys, tile_vals)
 // ordered by digit 0 of the tile sort (tbits bits in `passes` passes); the
 // sort then continues from pass 1 (radix_sort_pairs first_pass = 1).  hist
 // holds bin_hist_elems(n_vis, tbits, passes) uint32, totals
 // radix_totals_elems().  tbits = 0 (one tile): generation order.
-// sorted_ids null: the splats in slot order (the per-tile depth sort's
-// binning: slot r is splat r, its rect trect[r]; trect_sorted unused); then
-// slot_keys (the preprocess's depth key per slot) ride along to inst_keys.
-// In two halves: the counts and their offsets (launch_binning_hist, which needs
-// no instance buffer), then the scatter (launch_binning_scatter).
 size_t bin_hist_elems(size_t n_vis, int tbits, int passes);
-struct BinSortArgs {
-    const uint32_t* sorted_ids;  // null: slot order
-    const uint2* trect;
-    const uint32_t* rect4_sorted;
-    uint32_t n_vis;
-    int tiles_x, tbits, passes;
-    uint32_t* hist;
-    uint32_t* totals;
-    uint2* trect_sorted;
-    uint32_t* tile_keys;
-    uint32_t* tile_vals;
-    const uint32_t* slot_keys = nullptr;
-    uint32_t* inst_keys = nullptr;
-    // coarse depth bits of the instance keys (slot order only): (tile << coarse_bits) | bucket of the
-    // splat's key in the frame's key_range (device {~kmin, kmax}); the digits span tbits + coarse_bits
-    uint32_t coarse_bits = 0;
-    const uint32_t* key_range = nullptr;
-};
-int launch_binning_hist(const BinSortArgs& a, hipStream_t s);
-int launch_binning_scatter(const BinSortArgs& a, hipStream_t s);
-// tile_sort.hip: the per-tile depth sort (see there).  The tile-sorted
-// instances come in runs of equal (tile, coarse depth bucket) (InstKey,
-// composite.hip), each in slot order; every run is put in (depth key, slot)
-// order in place.  A block takes the runs that start in its kTdsSpan
-// instances: runs of 2 .. kTdsCapWave one wave each, up to kTdsCapBlock the
-// block in registers, longer ones the block through global scratch.
-constexpr uint32_t kTdsCapWave = 1024;
-constexpr uint32_t kTdsCapBlock = 24576;
-constexpr uint32_t kTdsSpan = 8192;
-struct TileSortView {
-    const uint32_t* tile_keys;  // the tile sort's keys ((tile << cb) | bucket): runs are their equal stretches
-    uint32_t* keys;             // each list position's depth key (the tile sort's payload); permuted
-    uint32_t* vals;             // the tile lists (slots): sorted in place
-    uint32_t* keys_alt;         // n_dup words each of scratch (the tile sort's alternate buffers)
-    uint32_t* vals_alt;
-    uint32_t n_dup;
-    const uint2* big_runs;      // the runs of > kTdsCapWave instances (k_tile_ranges), in no order
-    const uint32_t* big_count;
-};
-// debug (GSR_DEBUG_TDS, timing experiments only; 0 in production): 1 skips the
-// runs a block sorts, 2 the runs waves sort, 4 sorts one digit pass only;
-// stamps (8: the knob's stamp buffer): per block of view 0, 8 words of clock
-// stamps (start, after the long runs, after finding its runs, end) and counts
-int launch_tile_depth_sort(const TileSortView* views, int k, hipStream_t s, uint32_t debug = 0,
-                           uint64_t* stamps = nullptr);
-
+int launch_binning_sorted(const uint32_t* sorted_ids, const uint2* trect, const uint32_t* rect4_sorted,
+                          uint32_t n_vis, int tiles_x, int tbits, int passes, uint32_t* hist, uint32_t* totals,
+                          uint2* trect_sorted, uint32_t* tile_keys, uint32_t* tile_vals, hipStream_t s,
+                          const uint32_t* sorted_keys = nullptr, uint32_t* inst_keys = nullptr);
 // chunk_cnt must hold chunk_cnt_elems(num_tiles) entries (block totals after the tiles);
 // order: one entry per chunk (dispatch position -> chunk slot)
 size_t chunk_cnt_elems(int num_tiles);
@@ -506,8 +505,7 @@ int launch_merge(const uint32_t* chunk_cnt, const uint32_t* chunk_base, const fl
 // the frame size, t_min, background, output layout and chunk length.
 struct FinishView {
     // binning (n_vis, n_dup: this view's exact counts)
-    const uint32_t* sorted_ids;  // null: slot order (the per-tile depth sort), slot_keys ride along
-    const uint32_t* slot_keys;
+    const uint32_t* sorted_ids;
     const uint2* trect;
     const uint32_t* rect4_sorted;  // nullable, on every view or none (launch_binning)
     uint32_t n_vis, n_dup;
@@ -515,9 +513,7 @@ struct FinishView {
     uint2* trect_sorted;
     uint32_t* tile_keys;  // tile-sorted (keys, vals) after the tile sort
     uint32_t* tile_vals;
-    uint32_t* inst_keys;  // per-tile depth sort: the instances' depth keys (binning + tile sort payload), else null
-    uint2* big_runs;      // ... its runs of > kTdsCapWave instances (k_tile_ranges_views), else null
-    uint32_t* big_count;
+    RunFix fix;           // coarse depth order repair (vals, scratch set after the tile sort)
     // chunks, composite, merge
     uint2* ranges;
     uint32_t* chunk_cnt;
@@ -533,15 +529,10 @@ struct FinishView {
 };
 // binning: bin_tmp of each view holds its per-block instance counts
 int launch_binning_views(FinishView* views, int k, int tiles_x, uint32_t stage_limit, hipStream_t s);
-// ... and with the tile sort's pass 0 fused in (hist[v], totals[v] per view), in
-// the two halves of launch_binning_hist / launch_binning_scatter
-int launch_binning_hist_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
-                              int tbits, int passes, hipStream_t s, uint32_t coarse_bits = 0,
-                              const uint32_t* const* key_range = nullptr);
-int launch_binning_scatter_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k,
-                                 int tiles_x, int tbits, int passes, hipStream_t s, uint32_t coarse_bits = 0,
-                                 const uint32_t* const* key_range = nullptr);
-int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s, uint32_t cb = 0);
+// ... and with the tile sort's pass 0 fused in (hist[v], totals[v] per view)
+int launch_binning_sorted_views(FinishView* views, uint32_t* const* hist, uint32_t* const* totals, int k, int tiles_x,
+                                int tbits, int passes, hipStream_t s);
+int launch_tile_ranges_views(FinishView* views, int k, hipStream_t s);
 // first_major: every tile's first chunk dispatched before any later chunk
 int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk, uint32_t classes, bool first_major,
                         hipStream_t s);

@@ -384,35 +384,39 @@ static int sort_passes(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_a
                        bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
                        const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s,
                        const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt, int first_pass,
-                       bool drop_first) {
+                       bool drop_first, uint32_t coarse, bool keys_last) {
     constexpr int kTileItems = kThreads * kR;
     const uint32_t nt = (uint32_t)((n + kTileItems - 1) / kTileItems);
     // upper bound of the radix over the passes (device-chosen widths never exceed it)
     const uint32_t radix_max = 1u << ((bits + passes - 1) / passes);
     bool ident = identity_vals;
-    // a payload: the packed rects (rect_in, read by the first pass), or the words in *pay_io (the tile sort
-    // carrying the instances' depth keys)
-    const bool pay = pay_io != nullptr;
+    // a payload: the packed rects (rect_in, read by the first pass), or pay_io alone (the tile sort carrying
+    // the instances' depth keys)
+    const bool pay = rect_in != nullptr || pay_io != nullptr;
     for (int p = first_pass; p < passes; ++p) {
         const PassArgs pa{key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p,
-                          drop_first && p == first_pass ? 1u : 0u};
+                          drop_first && p == first_pass ? 1u : 0u, coarse};
+        // keys_last false: the last pass writes no keys, so *keys_io keeps its input
+        uint32_t* kout = (keys_last || p + 1 < passes) ? *keys_alt : nullptr;
         k_rs_upsweep<kR, kCB><<<nt, kThreads, 0, s>>>(*keys_io, n_dev, (uint32_t)n, pa, tmp, nt);
         GSR_LAUNCH_CHECK("rs_upsweep");
         k_rs_offsets<<<(radix_max + kOffWaves - 1) / kOffWaves, 64 * kOffWaves, 0, s>>>(tmp, nt, pa, totals);
         GSR_LAUNCH_CHECK("rs_offsets");
         if (pay) {
-            k_rs_scatter<kR, true, kCB><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev,
-                                                                (uint32_t)n, pa, tmp, totals, nt,
-                                                                p == first_pass ? rect_in : nullptr, *pay_io, *pay_alt);
+            k_rs_scatter<kR, true, kCB><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, kout, *vals_alt, n_dev,
+                                                           (uint32_t)n, pa, tmp, totals, nt, p == first_pass ? rect_in : nullptr,
+                                                           *pay_io, *pay_alt);
         } else {
-            k_rs_scatter<kR, false, kCB><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, *keys_alt, *vals_alt, n_dev,
-                                                                 (uint32_t)n, pa, tmp, totals, nt, nullptr, nullptr,
-                                                                 nullptr);
+            k_rs_scatter<kR, false, kCB><<<nt, kThreads, 0, s>>>(*keys_io, *vals_io, ident, kout, *vals_alt, n_dev,
+                                                            (uint32_t)n, pa, tmp, totals, nt, nullptr, nullptr,
+                                                            nullptr);
         }
         GSR_LAUNCH_CHECK("rs_scatter");
         ident = false;
         uint32_t* t;
-        t = *keys_io; *keys_io = *keys_alt; *keys_alt = t;
+        if (kout) {
+            t = *keys_io; *keys_io = *keys_alt; *keys_alt = t;
+        }
         t = *vals_io; *vals_io = *vals_alt; *vals_alt = t;
         if (pay) {
             t = *pay_io; *pay_io = *pay_alt; *pay_alt = t;
@@ -428,17 +432,18 @@ static int sort_passes_views(RadixViewArgs* views, int k, bool identity_vals, si
     const uint32_t nt = (uint32_t)((n + kTileItems - 1) / kTileItems);
     const uint32_t radix_max = 1u << ((bits + passes - 1) / passes);
     bool ident = identity_vals;
-    const bool pay = views[0].pay_io != nullptr;  // all views or none (radix_sort_pairs_views)
     for (int p = first_pass; p < passes; ++p) {
         SortViews sv{};
         for (int v = 0; v < k; ++v) {
             RadixViewArgs& a = views[v];
-            sv.v[v] = SortView{*a.keys_io, *a.vals_io, *a.keys_alt, *a.vals_alt, a.n_dev, a.tmp, a.totals,
+            sv.v[v] = SortView{*a.keys_io, *a.vals_io, (a.keys_last || p + 1 < passes) ? *a.keys_alt : nullptr,
+                               *a.vals_alt, a.n_dev, a.tmp, a.totals,
                                PassArgs{a.key_range, (uint32_t)bits, (uint32_t)passes, (uint32_t)p,
-                                        a.drop_first && p == first_pass ? 1u : 0u},
-                               p == first_pass ? a.rect_in : nullptr, pay ? *a.pay_io : nullptr,
-                               pay ? *a.pay_alt : nullptr};
+                                        a.drop_first && p == first_pass ? 1u : 0u, a.coarse},
+                               p == first_pass ? a.rect_in : nullptr, a.rect_in ? *a.pay_io : nullptr,
+                               a.rect_in ? *a.pay_alt : nullptr};
         }
+        const bool pay = views[0].rect_in != nullptr;  // all views or none (radix_sort_pairs_views)
         k_rs_upsweep_views<kR, kCB><<<dim3(nt, k), kThreads, 0, s>>>(sv, (uint32_t)n, nt);
         GSR_LAUNCH_CHECK("rs_upsweep_views");
         k_rs_offsets_views<<<dim3((radix_max + kOffWaves - 1) / kOffWaves, k), 64 * kOffWaves, 0, s>>>(sv, nt);
@@ -452,9 +457,11 @@ static int sort_passes_views(RadixViewArgs* views, int k, bool identity_vals, si
         for (int v = 0; v < k; ++v) {
             RadixViewArgs& a = views[v];
             uint32_t* t;
-            t = *a.keys_io; *a.keys_io = *a.keys_alt; *a.keys_alt = t;
+            if (a.keys_last || p + 1 < passes) {
+                t = *a.keys_io; *a.keys_io = *a.keys_alt; *a.keys_alt = t;
+            }
             t = *a.vals_io; *a.vals_io = *a.vals_alt; *a.vals_alt = t;
-            if (pay) {
+            if (a.rect_in) {
                 t = *a.pay_io; *a.pay_io = *a.pay_alt; *a.pay_alt = t;
             }
         }
@@ -500,12 +507,8 @@ int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size
     if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
         return set_error(GSR_ERR_INVALID, "radix sort: digit width out of range");
     for (int v = 1; v < k; ++v)
-        if ((views[v].rect_in != nullptr) != (views[0].rect_in != nullptr) ||
-            (views[v].pay_io != nullptr) != (views[0].pay_io != nullptr))
+        if ((views[v].rect_in != nullptr) != (views[0].rect_in != nullptr))
             return set_error(GSR_ERR_INVALID, "radix sort: payload on some views only");
-    for (int v = 0; v < k; ++v)
-        if (views[v].rect_in && !views[v].pay_io)
-            return set_error(GSR_ERR_INVALID, "radix sort: packed rectangles need the payload buffers");
     if ((bits + passes - 1) / passes <= 8)
         return views[0].key_range
                    ? sort_passes_views<kRDepth, 8>(views, k, identity_vals, n, bits, passes, s, first_pass)
@@ -517,9 +520,9 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
                      bool identity_vals, size_t n, const uint32_t* n_dev, int bits, int passes,
                      const uint32_t* key_range, uint32_t* tmp, uint32_t* totals, hipStream_t s,
                      const uint2* rect_in, uint32_t** pay_io, uint32_t** pay_alt, int first_pass,
-                     bool drop_first) {
+                     bool drop_first, uint32_t coarse, bool keys_last) {
     if (n == 0 || passes == 0 || first_pass >= passes) return GSR_OK;
-    if (rect_in && !pay_io) return set_error(GSR_ERR_INVALID, "radix sort: packed rectangles need the payload buffers");
+    if (coarse && !key_range) return set_error(GSR_ERR_INVALID, "radix sort: a coarse order needs the key range");
     if (drop_first && !key_range) return set_error(GSR_ERR_INVALID, "radix sort: dropping needs the key range");
     if (n > 0xffffffffull - 4 * kMinTileItems) return set_error(GSR_ERR_OVERFLOW, "radix sort: n too large");
     if (bits < 1 || bits > 32 || passes < 1 || (bits + passes - 1) / passes > kMaxBits)
@@ -530,12 +533,15 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
     if ((bits + passes - 1) / passes <= 8) {
         if (key_range)
             return sort_passes<kRDepth, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
-                                     key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first);
+                                     key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first, coarse,
+                                     keys_last);
         return sort_passes<kRTile, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
-                                  key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first);
+                                  key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first, coarse,
+                                     keys_last);
     }
     return sort_passes<kRWide, kMaxBits>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
-                                         key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first);
+                                         key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first, coarse,
+                                     keys_last);
 }
 
 }  // namespace gsr

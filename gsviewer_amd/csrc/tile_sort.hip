@@ -1,51 +1,50 @@
-// Per-tile depth sort (round 5): every tile's instance list put in the GL draw
-// order restricted to the tile, (depth key, slot), in place.
+// The coarse depth order's long runs (round 5): the stretches of one tile's
+// list whose instances share the coarse depth key and that are too long for
+// k_tile_ranges' in-thread repair (RunFix, composite.hip), put in the GL draw
+// order restricted to the tile, (full depth key, slot), in place.
 //
-// The frame's instances are binned in slot order (no global depth sort) under
-// the key (tile << cb) | bucket, the bucket the top cb bits of the splat's
-// depth key in the frame's key range (InstKey, composite.hip), and sorted by
-// that key with the stable tile radix sort: each tile's list leaves it in
-// runs of equal bucket, buckets ascending, each run in ascending slot order,
-// with its instances' depth keys beside it (the binning and the tile sort
-// carry them).  A stable LSD radix sort of every run by depth key then gives
-// exactly (key, slot): the order the global depth sort + stable binning
-// produced (renderer_ogl.py:16-26: GL draws back to front in _sort_gaussian's
-// order; the compositor walks it front to back; ties in slot order, slot
-// n-1-i for Gaussian i, see preprocess.hip).  The cb bits cost no tile-sort
-// pass: the passes are fixed by the tile id's width and their 8-bit digits
-// have room for them (api.hip TileBits: 3 bits at 1080p, 1 at 4K; 11-bit
-// digits for 9 bits cost the binning and the tile sort 105 us, profiles/r5_s9).
+// The frame alone sorts depth by the top bits of its key range only (two
+// 8-bit passes, api.hip depth_sort); the binning and the tile sort are stable
+// and carry each instance's full key, so every tile's list leaves them in runs
+// of equal coarse key, ascending, each run in slot order.  A stable sort of a
+// run by full key gives exactly (key, slot): the order an exact depth sort and
+// the stable binning produce (renderer_ogl.py:16-26: GL draws back to front in
+// _sort_gaussian's order; the compositor walks it front to back; ties in slot
+// order, slot n-1-i for Gaussian i, see preprocess.hip).  Runs of up to
+// kFixRunMax are repaired in k_tile_ranges; the longer ones, listed there, are
+// rare in a scene of spread depths (none at C2) and unbounded in a degenerate
+// one (a fronto-parallel plane: a deep tile's whole list is one run), so they
+// get on-chip sorts of bounded cost, not round 4's single-thread O(L^2).
 //
-// Why runs: a deep tile (22 K instances at C2) sorted by one workgroup keeps
-// one CU busy for ~40 us (the ranking is VALU issue: ~50 instructions per
-// instance and pass at 4 cycles each, profiles/r5_s8), while the depth
-// buckets cut it into runs (at C2 the longest 9.4 K) that spread over the
-// chip, and the runs' narrower key ranges take fewer passes.  Why no global sort:
-// the work is each run's own instances, kept on chip (one read and one
-// write each), one launch instead of a chain of global passes.
+// Per-run or per-tile sorting as the DEFAULT order was measured and dropped:
+// it is latency-bound (one wave ~5 us per run, a workgroup 20-25 us,
+// profiles/r5_s13); here it only covers what the coarse order leaves.
 //
-// One launch, one 1024-thread block per kTdsSpan instances:
-//   * runs of more than 1024 instances (k_tile_ranges lists them; a few
-//     hundred at C2) are dealt to the blocks in turn, each sorted by one whole
-//     block: up to 24576 the run in registers (24 per thread), per
-//     pass a stable ranking (ballot digit matching, per-wave digit counts in
-//     LDS) and one LDS exchange; the last pass writes the slots coalesced
-//     through LDS;
-//   * longer (a run that fills a deep tile: a depth range too narrow for the
-//     frame's buckets, the deepest tiles of C3): the whole block, sub-blocks
-//     of 12288 ranked as above and written as contiguous digit runs through
-//     global scratch (the tile sort's alternate buffers), an even number of
-//     passes so the result lands in place;
-//   * then each block finds the runs that start in its span (the last one may
-//     end past it) and sorts those of 2 .. 1024 instances, one wave per run,
-//     16 items per lane, wave-local ranking and exchange, no workgroup
-//     barriers.
+// One launch, a fixed grid of 1024-thread blocks; block b takes the listed
+// runs b, b + G, ...:
+//   * each wave finds one run's end (a 64-way search between its start and
+//     its tile's end: tile key and coarse key are nondecreasing along the
+//     list, so "still in the run" is a prefix) and, up to 1024 instances,
+//     sorts it (16 items per lane, wave-local ranking by ballot digit
+//     matching and an LDS exchange, no workgroup barriers);
+//   * then the block sorts its longer runs one at a time: up to 24576 in
+//     registers (24 per thread), per pass a stable ranking with per-wave digit
+//     counts in LDS and one LDS exchange, the last pass writing the slots
+//     coalesced; longer ones through global scratch (the tile sort's
+//     alternate buffers), an even number of passes so the result lands in place.
+// Concurrent blocks read other runs only while searching: the tile keys are
+// never written and a run's permutation keeps its coarse key, so the search's
+// answer does not depend on it.
+
 #include "gsr_internal.h"
 
 namespace gsr {
 namespace {
 
+constexpr uint32_t kTdsCapWave = 1024;    // runs sorted by one wave (16 items per lane)
+constexpr uint32_t kTdsCapBlock = 24576;  // runs sorted by one workgroup in registers (24 per thread)
 constexpr int kTdsThreads = 1024;
+constexpr int kLongGrid = 256;  // blocks of the long-run launch (one per CU: 108 KB of LDS each)
 constexpr int kTdsWaves = kTdsThreads / 64;
 constexpr int kTdsItems = kTdsCapBlock / kTdsThreads;  // per thread, workgroup path
 static_assert(kTdsItems * kTdsThreads == (int)kTdsCapBlock, "capacity");
@@ -89,7 +88,7 @@ __device__ __forceinline__ uint32_t tds_passes(uint32_t B, bool even) {
 // ---------------------------------------------------------------- wave path
 // One wave sorts the list [b, b + L), 2 <= L <= kTdsCapWave.
 __device__ void tds_wave(const uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t b, uint32_t L,
-                         TdsWaveLds& W, uint32_t dbg) {
+                         TdsWaveLds& W) {
     const uint32_t lane = __lane_id();
     const uint32_t nr = (L + 63u) / 64u;
     uint32_t k[kTdsLaneItems], v[kTdsLaneItems], rank[kTdsLaneItems];
@@ -112,11 +111,10 @@ __device__ void tds_wave(const uint32_t* __restrict__ keys, uint32_t* __restrict
     const uint32_t kmin = wave_min(lo), kmax = wave_reduce_max(hi);
     if (kmax == kmin) return;  // equal keys: the slot order is the order
     const uint32_t B = 32u - (uint32_t)__clz(kmax - kmin);
-    uint32_t P = tds_passes(B, false);
+    const uint32_t P = tds_passes(B, false);
     TdsPass dg;
     dg.kmin = kmin;
     dg.w = (B + P - 1u) / P;
-    if (dbg & 4u) P = 1u;  // (timing knob: the first digit only, <= 8 bits)
     dg.mask = (1u << dg.w) - 1u;
     uint16_t* c16 = reinterpret_cast<uint16_t*>(W.cnt);
     for (uint32_t p = 0; p < P; ++p) {
@@ -262,7 +260,7 @@ __device__ __forceinline__ void tds_rank_block(const uint32_t (&k)[kI], uint32_t
 
 // One workgroup sorts [b, b + L), kTdsCapWave < L <= kTdsCapBlock, in registers.
 __device__ void tds_block(const uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t b, uint32_t L,
-                          TdsLds& S, uint32_t dbg) {
+                          TdsLds& S) {
     const uint32_t t = threadIdx.x, w = t >> 6, lane = __lane_id();
     // wave w's span: items [w * span, (w + 1) * span), rounds of 64
     const uint32_t span = (L + kTdsThreads - 1u) / kTdsThreads * 64u;
@@ -285,11 +283,10 @@ __device__ void tds_block(const uint32_t* __restrict__ keys, uint32_t* __restric
     block_minmax(lo, hi, S);
     if (hi == lo) return;
     const uint32_t B = 32u - (uint32_t)__clz(hi - lo);
-    uint32_t P = tds_passes(B, false);
+    const uint32_t P = tds_passes(B, false);
     TdsPass dg;
     dg.kmin = lo;
     dg.w = (B + P - 1u) / P;
-    if (dbg & 4u) P = 1u;  // (timing knob: the first digit only, <= 8 bits)
     dg.mask = (1u << dg.w) - 1u;
     for (uint32_t p = 0; p < P; ++p) {
         dg.shift = p * dg.w;
@@ -426,151 +423,88 @@ __device__ void tds_global(uint32_t* __restrict__ keys, uint32_t* __restrict__ v
     }
 }
 
-struct TdsView {
-    const uint32_t* tkeys;  // the tile sort's keys: a run is a stretch of equal ones
-    uint32_t* keys;         // the instances' depth keys; the global path permutes them
-    uint32_t* vals;         // the tile lists (slots), sorted in place
-    uint32_t* keys_alt;     // scratch for the global path (n words each)
+struct LongRunArgs {
+    const uint32_t* tile_keys;  // the sorted tile keys (never written)
+    const uint2* ranges;        // each tile's [begin, end) in the list
+    uint32_t* inst_keys;        // each position's full depth key (the global path permutes them with the slots)
+    uint32_t* vals;             // the tile lists (slots), sorted in place
+    uint32_t* keys_alt;         // scratch for the global path (n words each)
     uint32_t* vals_alt;
-    uint32_t n;
-    const uint2* big_runs;  // the runs of > kTdsCapWave (k_tile_ranges)
-    const uint32_t* big_count;
-};
-struct TdsViews {
-    TdsView v[kMaxViews];
-    uint64_t* stamps;  // (timing knob GSR_DEBUG_TDS & 8: per block 4 clock stamps + 4 counts; else null)
+    const uint32_t* key_range;  // the frame's {~kmin, kmax}
+    uint32_t coarse;
+    const uint32_t* starts;     // the runs' first positions (k_tile_ranges), *count of them
+    const uint32_t* count;
+    uint32_t* lens;             // each run's length, for the block pass
 };
 
-constexpr int kSpanItems = (int)kTdsSpan / kTdsThreads;  // instances per thread when finding the runs
+// The end of the run starting at b (tile `tile`, coarse key cv), at most hi:
+// 64 probes a round, the first failing one narrows the bracket 64-fold.
+__device__ uint32_t run_end(const LongRunArgs& a, uint32_t b, uint32_t hi, uint32_t tile, uint32_t cv, uint32_t kmin,
+                            uint32_t s0) {
+    const uint32_t lane = __lane_id();
+    uint32_t lo = b, up = hi;  // p(lo) holds; every position >= up fails (or is past the tile)
+    while (up - lo > 1u) {
+        const uint32_t step = (up - lo + 63u) / 64u;
+        const uint32_t pos = lo + (lane + 1u) * step;
+        bool in = false;
+        if (pos < up) {
+            const uint32_t tk = a.tile_keys[pos], f = a.inst_keys[pos];
+            in = tk == tile && ((f - kmin) >> s0) == cv;
+        }
+        const uint32_t c = (uint32_t)__popcll(__ballot(in));  // a prefix of the lanes
+        up = min(up, lo + (c + 1u) * step);
+        lo += c * step;
+    }
+    return up;
+}
 
-// Runs of a span, outside the sort's LDS (TdsLds): their starts (offsets from
-// the span's first instance) and the last one's end.
-struct TdsRunLds {
-    uint16_t start[kTdsSpan];
-    uint32_t n_runs, last_end;
-    uint32_t scan[kTdsWaves];
-};
-
-__global__ __launch_bounds__(kTdsThreads) void k_tile_depth_sort(TdsViews vs, uint32_t dbg) {
+__global__ __launch_bounds__(kTdsThreads) void k_long_runs(LongRunArgs a) {
     __shared__ TdsLds S;
-    __shared__ TdsRunLds R;
-    const TdsView& V = vs.v[blockIdx.y];
-    if (blockIdx.x * kTdsSpan >= V.n) return;  // (a view smaller than the grid's largest)
-    const uint32_t t = threadIdx.x, w = t >> 6, lane = __lane_id();
-    uint64_t* st = vs.stamps && blockIdx.y == 0 ? vs.stamps + 8 * (size_t)blockIdx.x : nullptr;
-    if (st && t == 0) st[0] = __builtin_amdgcn_s_memrealtime();
-    // A. the long runs, one workgroup each, dealt to the view's blocks in turn
-    const uint32_t n_big = *V.big_count;
-    const uint32_t blocks = (V.n + kTdsSpan - 1) / kTdsSpan;
-    uint32_t big_done = 0, big_items = 0;
-    for (uint32_t i = blockIdx.x; i < n_big; i += blocks) {
-        const uint2 br = V.big_runs[i];
-        ++big_done;
-        big_items += br.y;
-        if (!(dbg & 1u)) {
-            if (br.y > kTdsCapBlock)
-                tds_global(V.keys, V.vals, V.keys_alt, V.vals_alt, br.x, br.y, S);
-            else
-                tds_block(V.keys, V.vals, br.x, br.y, S, dbg);
-        }
+    const uint32_t n_long = *a.count;
+    if (blockIdx.x >= n_long) return;
+    const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
+    uint32_t kmin;
+    const uint32_t s0 = coarse_shift(a.key_range, a.coarse, kmin);  // > 0: a long run was listed
+    const uint32_t G = gridDim.x;
+    const uint32_t mine = (n_long - blockIdx.x + G - 1u) / G;  // this block's runs: blockIdx.x + j G, j < mine
+    // 1. one wave per run: its end, and the sort of a run of <= kTdsCapWave
+    for (uint32_t j = w; j < mine; j += kTdsWaves) {
+        const uint32_t r = blockIdx.x + j * G;
+        const uint32_t b = a.starts[r];
+        const uint32_t tile = a.tile_keys[b];
+        const uint32_t cv = (a.inst_keys[b] - kmin) >> s0;
+        const uint32_t L = run_end(a, b, a.ranges[tile].y, tile, cv, kmin, s0) - b;
+        if (L <= kTdsCapWave) tds_wave(a.inst_keys, a.vals, b, L, S.wave[w]);
+        if (lane == 0) a.lens[r] = L;
+    }
+    __syncthreads();  // (the lengths are this block's own writes)
+    // 2. the whole block per longer run
+    for (uint32_t j = 0; j < mine; ++j) {
+        const uint32_t r = blockIdx.x + j * G;
+        const uint32_t L = a.lens[r];
+        if (L <= kTdsCapWave) continue;
+        const uint32_t b = a.starts[r];
+        if (L > kTdsCapBlock)
+            tds_global(a.inst_keys, a.vals, a.keys_alt, a.vals_alt, b, L, S);
+        else
+            tds_block(a.inst_keys, a.vals, b, L, S);
         __syncthreads();  // (the next run reuses the LDS)
-    }
-    if (st && t == 0) st[1] = __builtin_amdgcn_s_memrealtime();
-    // B. the runs of 2 .. kTdsCapWave that start in this block's span, one wave each
-    const uint32_t p0 = blockIdx.x * kTdsSpan;
-    const uint32_t p1 = min(p0 + kTdsSpan, V.n);
-    {
-        const uint32_t q0 = p0 + t * kSpanItems;
-        uint32_t flags = 0, cnt = 0;
-        if (q0 < p1) {
-            uint32_t kk[kSpanItems];  // (every load issued before any is used)
-#pragma unroll
-            for (int j = 0; j < kSpanItems; ++j) kk[j] = q0 + (uint32_t)j < p1 ? V.tkeys[q0 + j] : 0u;
-            uint32_t prev = q0 > 0 ? V.tkeys[q0 - 1] : ~kk[0];
-#pragma unroll
-            for (int j = 0; j < kSpanItems; ++j) {
-                if (q0 + (uint32_t)j < p1 && kk[j] != prev) flags |= 1u << j;
-                prev = kk[j];
-            }
-            cnt = (uint32_t)__popc(flags);
-        }
-        uint32_t total;
-        uint32_t o = block_exclusive<kTdsThreads>(cnt, R.scan, total);
-#pragma unroll
-        for (int j = 0; j < kSpanItems; ++j)
-            if (flags & (1u << j)) R.start[o++] = (uint16_t)(t * kSpanItems + (uint32_t)j);
-        if (t == 0) R.n_runs = total;
-    }
-    __syncthreads();
-    const uint32_t n_runs = R.n_runs;  // (0: the whole span continues a run begun before it)
-    // where the span's last run ends (it may go on past p1; a long one is not this block's): wave 0 looks
-    // at most kTdsCapWave + 1 instances past p1, 64 at a time
-    if (w == 0) {
-        uint32_t e = p1;
-        if (n_runs > 0 && p1 < V.n) {
-            const uint32_t key = V.tkeys[p0 + R.start[n_runs - 1]];
-            constexpr int kLook = (int)(kTdsCapWave + 64) / 64;  // 17 loads per lane, all in flight
-            uint32_t kk[kLook];
-#pragma unroll
-            for (int c = 0; c < kLook; ++c) {
-                const uint32_t i = p1 + (uint32_t)c * 64u + lane;
-                kk[c] = i < V.n ? V.tkeys[i] : ~key;
-            }
-            e = 0xffffffffu;
-#pragma unroll
-            for (int c = kLook - 1; c >= 0; --c) {  // the first mismatch: the lowest chunk that has one
-                const uint64_t m = __ballot(kk[c] != key);
-                if (m) e = p1 + (uint32_t)c * 64u + (uint32_t)__builtin_ctzll(m);
-            }
-            if (e == 0xffffffffu) e = V.n;  // longer than kTdsCapWave: a long run (part A)
-        }
-        if (lane == 0) R.last_end = min(e, V.n);
-    }
-    __syncthreads();
-    if (st && t == 0) st[2] = __builtin_amdgcn_s_memrealtime();
-    uint32_t small_items = 0;
-    if (!(dbg & 2u)) {
-        for (uint32_t r = w; r < n_runs; r += kTdsWaves) {
-            const uint32_t b = p0 + R.start[r];
-            const uint32_t e = r + 1 < n_runs ? p0 + R.start[r + 1] : R.last_end;
-            const uint32_t L = e - b;
-            if (L >= 2u && L <= kTdsCapWave) {
-                tds_wave(V.keys, V.vals, b, L, S.wave[w], dbg);
-                small_items += L;
-            }
-        }
-    }
-    if (st) {
-        __syncthreads();
-        if (t == 0) {
-            st[3] = __builtin_amdgcn_s_memrealtime();
-            st[4] = big_done;
-            st[5] = big_items;
-            st[6] = n_runs;
-        }
-        if (lane == 0) atomicAdd(reinterpret_cast<unsigned long long*>(st + 7), (unsigned long long)small_items);
     }
 }
 
 }  // namespace
 
-int launch_tile_depth_sort(const TileSortView* views, int k, hipStream_t s, uint32_t debug, uint64_t* stamps) {
-    if (k < 1 || k > kMaxViews) return set_error(GSR_ERR_INVALID, "tile depth sort: view count out of range");
-    TdsViews tv{};
-    tv.stamps = stamps;
-    uint32_t n_max = 0;
-    for (int i = 0; i < k; ++i) {
-        const TileSortView& a = views[i];
-        if (a.n_dup && (!a.tile_keys || !a.keys || !a.vals || !a.keys_alt || !a.vals_alt || !a.big_runs ||
-                        !a.big_count))
-            return set_error(GSR_ERR_INVALID, "tile depth sort: null buffer");
-        tv.v[i] = TdsView{a.tile_keys, a.keys, a.vals, a.keys_alt, a.vals_alt, a.n_dup, a.big_runs, a.big_count};
-        n_max = std::max(n_max, a.n_dup);
-    }
-    if (n_max == 0) return GSR_OK;
-    const uint32_t grid = (n_max + kTdsSpan - 1) / kTdsSpan;
-    k_tile_depth_sort<<<dim3(grid, (unsigned)k), kTdsThreads, 0, s>>>(tv, debug);
-    GSR_LAUNCH_CHECK("tile_depth_sort");
+int launch_long_runs(const uint32_t* tile_keys, uint32_t n_dup, const uint2* ranges, const RunFix& fix,
+                     hipStream_t s) {
+    if (n_dup == 0 || fix.coarse == 0) return GSR_OK;
+    if (!tile_keys || !ranges || !fix.inst_keys || !fix.vals || !fix.scratch_keys || !fix.scratch_vals ||
+        !fix.long_starts || !fix.long_count || !fix.key_range)
+        return set_error(GSR_ERR_INVALID, "long runs: null buffer");
+    const LongRunArgs a{tile_keys, ranges, fix.inst_keys, fix.vals, fix.scratch_keys, fix.scratch_vals,
+                        fix.key_range, fix.coarse, fix.long_starts, fix.long_count,
+                        fix.long_starts + long_run_cap(n_dup)};
+    k_long_runs<<<kLongGrid, kTdsThreads, 0, s>>>(a);
+    GSR_LAUNCH_CHECK("long_runs");
     return GSR_OK;
 }
 

@@ -310,17 +310,14 @@ int gsr_debug_stall(void* stream, uint32_t microseconds);
  *                          Gaussian, slot n-1-id, N records (culled slots hold
  *                          no record).  Separate cull: compacted, slot s = the
  *                          s-th visible Gaussian in DESCENDING id order, V records.
- *   GSR_DEBUG_DEPTH_ORDER  uint32 record slots, front-to-back: the global depth
- *                          order of a frame in the exact form (GSR_TILE_DEPTH_SORT=0
- *                          at context creation).  The default per-tile depth sort
- *                          orders each tile's list only: nothing is copied (0).
+ *   GSR_DEBUG_DEPTH_ORDER  uint32 record slots, front-to-back.  A frame alone
+ *                          (gsr_render) sorts only the top 16 bits of its depth
+ *                          key range (GSR_DEPTH_COARSE, 0 = exact): equal coarse
+ *                          keys in slot order; the tile lists are exact.  A
+ *                          group's frames sort exactly.
  *   GSR_DEBUG_TILE_RANGES  uint32 pairs [begin, end) per 16x16 tile (row-major tiles)
- *   GSR_DEBUG_TILE_LIST    uint32 record slots of all (tile, splat) instances, by tile then depth
- *   GSR_DEBUG_SLOT_KEYS    uint32 depth key per record slot (order-preserving bits of -z; the
- *                          fused cull's culled slots hold 0xffffffff).  The default form
- *                          only: the exact form's depth sort reuses the array. */
-enum { GSR_DEBUG_RECORDS = 0, GSR_DEBUG_DEPTH_ORDER = 1, GSR_DEBUG_TILE_RANGES = 2, GSR_DEBUG_TILE_LIST = 3,
-       GSR_DEBUG_SLOT_KEYS = 4 };
+ *   GSR_DEBUG_TILE_LIST    uint32 record slots of all (tile, splat) instances, by tile then depth */
+enum { GSR_DEBUG_RECORDS = 0, GSR_DEBUG_DEPTH_ORDER = 1, GSR_DEBUG_TILE_RANGES = 2, GSR_DEBUG_TILE_LIST = 3 };
 int64_t gsr_debug_copy(const gsr_context* ctx, int32_t what, void* dst_dev, int64_t max_bytes, void* stream);
 
 #ifdef __cplusplus

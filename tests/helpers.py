@@ -19,21 +19,49 @@ TOL_MAX = 8e-3             # any pixel-channel: a fragment whose alpha sits on t
 TOL_TMIN = 1e-4            # extra error allowed by early termination at t_min = 1e-4
 
 
-def frame_depth_order(vs):
-    """The global depth order a frame in the exact form leaves
-    (GSR_TILE_DEPTH_SORT=0: GSR_DEBUG_DEPTH_ORDER), as Gaussian ids front to
-    back: the reverse of the GL draw order (ties: descending id).  The default
-    per-tile depth sort has no global order (res["depth_order"] is empty); its
-    tile lists are this order restricted to each tile."""
-    return O.sort_back_to_front(vs["view_z"], vs["visible"])[::-1]
+def depth_coarse_bits(path="alone") -> int:
+    """A frame depth sort's coarse bits: api.hip kDepthCoarseAlone for a frame
+    alone (gsr_render; GSR_DEPTH_COARSE=0 exact, 8..16 otherwise), 0 for a
+    group's frames (always exact)."""
+    import os
+    if path != "alone":
+        return 0
+    bits = 16
+    v = os.environ.get("GSR_DEPTH_COARSE")
+    if v is not None and (int(v) == 0 or 8 <= int(v) <= 16):
+        bits = int(v)
+    return bits
+
+
+def frame_depth_order(vs, coarse=None):
+    """The order a frame's depth sort leaves (GSR_DEBUG_DEPTH_ORDER), as Gaussian
+    ids front to back.  Exact: the reverse of the GL draw order (ties: descending
+    id).  Coarse (the default, api.hip kDepthCoarse): only the top `coarse` bits
+    of the frame's key range (key = order-preserving bits of -z, minus the
+    smallest visible key) are ordered, equal coarse keys by descending id; the
+    tile lists are still exact (k_tile_ranges restores each run)."""
+    vis = vs["visible"]
+    f2b = O.sort_back_to_front(vs["view_z"], vis)[::-1]
+    coarse = depth_coarse_bits("alone") if coarse is None else coarse
+    if coarse == 0:
+        return f2b
+    gid = np.nonzero(vis)[0]
+    if gid.size == 0:
+        return f2b
+    b = (-vs["view_z"][gid].astype(np.float32)).view(np.uint32).astype(np.uint64)
+    key = np.where(b & 0x80000000, ~b & 0xFFFFFFFF, b | 0x80000000)
+    kmin, kmax = int(key.min()), int(key.max())
+    B = (kmax - kmin).bit_length()
+    s0 = max(0, B - coarse)
+    ck = (key - kmin) >> np.uint64(s0)
+    return gid[np.lexsort((-gid, ck))]
 
 
 def check_depth_order(res, vs):
-    """A frame's GSR_DEBUG_DEPTH_ORDER against frame_depth_order, when the frame has one."""
-    if res["depth_order"].size == 0:
-        return False
+    """A frame's GSR_DEBUG_DEPTH_ORDER against frame_depth_order with the
+    frame's coarse bits (res["depth_coarse"], 0 when absent)."""
     vis_desc = np.nonzero(vs["visible"])[0][::-1]
-    np.testing.assert_array_equal(vis_desc[res["depth_order"]], frame_depth_order(vs))
+    np.testing.assert_array_equal(vis_desc[res["depth_order"]], frame_depth_order(vs, res.get("depth_coarse", 0)))
     return True
 
 
@@ -77,7 +105,7 @@ def gpu_frame(g, cam, settings, with_debug=False, radii=False):
     settings.out_layout = 1
     render_into(ctx, scene, camera_from(cam), settings, out, rad)
     torch.cuda.synchronize()
-    res = {"image": out.cpu().numpy(), "stats": ctx.stats()}
+    res = {"image": out.cpu().numpy(), "stats": ctx.stats(), "depth_coarse": depth_coarse_bits("alone")}
     if radii:
         res["radii"] = rad.cpu().numpy()
     if with_debug:
@@ -112,17 +140,9 @@ def grab_debug(ctx, st):
         # culling fused into the preprocess (GSR_FUSED_CULL, the default):
         # Gaussian i owns slot n-1-i.  The compacted slots of the separate
         # cull keep the same order, so the visible slots map to them by rank.
-        # The visible slots: the exact form's depth order, or the slots whose
-        # depth key is not the culled mark (the default form).
-        if depth_order.size == nv:
-            vis_slots = np.sort(depth_order)
-        else:
-            keys = grab(_lib.GSR_DEBUG_SLOT_KEYS, n_all * 4, np.uint32)
-            vis_slots = np.nonzero(keys != 0xFFFFFFFF)[0].astype(np.uint32)
-            assert vis_slots.size == nv, (vis_slots.size, nv)
+        vis_slots = np.sort(depth_order)
         records = records.reshape(n_all, 48)[vis_slots]
-        if depth_order.size:
-            depth_order = np.searchsorted(vis_slots, depth_order).astype(np.uint32)
+        depth_order = np.searchsorted(vis_slots, depth_order).astype(np.uint32)
         tile_list = np.searchsorted(vis_slots, tile_list).astype(np.uint32)
     return dict(records=records.reshape(nv, 48), depth_order=depth_order,
                 ranges=grab(_lib.GSR_DEBUG_TILE_RANGES, nt * 8, np.uint32).reshape(nt, 2),
@@ -154,7 +174,8 @@ def batched_frames(scene, cams, settings, group=4, debug_views=()):
     torch.cuda.synchronize()
     res = []
     for v, (ctx, out) in enumerate(zip(ctxs, outs)):
-        r = {"image": out.permute(1, 2, 0).contiguous().cpu().numpy(), "stats": ctx.stats()}
+        r = {"image": out.permute(1, 2, 0).contiguous().cpu().numpy(), "stats": ctx.stats(),
+             "depth_coarse": depth_coarse_bits("views")}
         if v in debug_views:
             r.update(grab_debug(ctx, r["stats"]))
         res.append(r)

@@ -1,29 +1,26 @@
-"""The per-tile depth sort (gsviewer_amd/csrc/tile_sort.hip, the default form).
+"""The coarse depth order's long runs (gsviewer_amd/csrc/tile_sort.hip k_long_runs).
 
-The instances are binned in slot order under the key (tile, coarse depth
-bucket) (composite.hip InstKey: the top cb bits of the splat's depth key in
-the frame's key range; cb fills the tile sort's 11-bit digits: 0 for frames of
-<= 2048 tiles, 9 at 1080p), and every run of equal key is sorted by its
-instances' depth keys.  The order it must produce is the GL draw order
-restricted to the tile, the one /root/reference/render/renderer_ogl.py:16-26
-draws back to front (read front to back; ties in descending Gaussian id).
-Checked here, against the exact form (GSR_TILE_DEPTH_SORT=0: the global radix
-depth sort, then a stable binning in depth order; tests/test_gpu_parity.py
-checks that form's global order and tile lists against the oracle), bit for
-bit (tile lists, ranges, records, images):
+A frame alone sorts depth by the top GSR_DEPTH_COARSE bits of its key range
+(default 16); the stable binning and tile sort leave each tile's list in runs
+of equal coarse key, in slot order, which must end in (full key, slot) order:
+the GL draw order restricted to the tile, the one
+/root/reference/render/renderer_ogl.py:16-26 draws back to front (read front
+to back; ties in descending Gaussian id).  Runs of up to 16 are repaired in
+k_tile_ranges; longer ones are listed and sorted by k_long_runs (one wave up
+to 1024 instances, a workgroup in registers up to 24576, a workgroup through
+global scratch beyond).  Checked bit for bit (tile lists, ranges, records,
+images) against the exact sort (GSR_DEPTH_COARSE=0; tests/test_gpu_parity.py
+checks that form's global order and tile lists against the oracle):
 
-* every run path: one wave per run of 2..1024, one workgroup per run up to
-  24576 in registers, one workgroup through global scratch beyond (several
-  12288-instance sub-blocks per pass) -- at 540x960 (2040 tiles, cb = 0) the
-  runs are whole tile lists of every length;
-* a single run of ~60k instances: a dense fronto-parallel plane in one tile,
-  one far splat stretching the frame's key range so that the plane's depths
-  share one coarse bucket;
+* every run path: a fronto-parallel plane whose density falls off to the
+  right, one far splat stretching the key range (so that, with 8 coarse bits,
+  each tile's list is one run) -- runs of every length class;
+* a single run of ~60k instances in one tile;
 * lists whose keys are all equal, or take two values (ties by slot only);
-* round 4's adversarial case for the coarse order: a dense plane plus one far
-  splat at 1080p (runs as long as the tile lists), whose frame must also stay
-  within 1.5x the exact form's time;
-* a group of views (gsr_render_finish_views), deep lists included.
+* round 4's adversarial case: a dense plane plus one far splat at 1080p (runs
+  as long as the tile lists; round 4 spent ~5e8 serial steps there), whose
+  frame must stay within 1.5x the exact form's time;
+* a group of views (exact sort) against the same views alone (coarse).
 """
 import time
 
@@ -39,15 +36,15 @@ from oracle import gl_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-CAP_WAVE, CAP_BLOCK = 1024, 24576  # gsr_internal.h kTdsCapWave / kTdsCapBlock
+CAP_WAVE, CAP_BLOCK, FIX_MAX = 1024, 24576, 16  # tile_sort.hip kTdsCapWave / kTdsCapBlock, kFixRunMax
 
 
-def tds_class(lens):
-    """Run classes by length (a run is a whole tile list when cb = 0): 0 global
-    path, 1-3 workgroup, 4-6 wave, 7 nothing to sort."""
+def run_class(lens):
+    """Run classes by length: 0 global path, 1-3 workgroup, 4-6 wave, 7 the
+    in-thread repair, 8 nothing to sort."""
     lens = np.asarray(lens, np.int64)
-    return np.select([lens > CAP_BLOCK, lens > 8192, lens > 2048, lens > CAP_WAVE, lens > 256, lens > 64, lens >= 2],
-                     [0, 1, 2, 3, 4, 5, 6], 7)
+    return np.select([lens > CAP_BLOCK, lens > 8192, lens > 2048, lens > CAP_WAVE, lens > 256, lens > 64,
+                      lens > FIX_MAX, lens >= 2], [0, 1, 2, 3, 4, 5, 6, 7], 8)
 
 
 def _settings(**kw):
@@ -65,15 +62,21 @@ def _scene(xyz, scale, seed, opacity=(0.05, 0.6)):
                         rng.normal(0, 0.5, (n, 3)).astype(np.float32))
 
 
-def graded_scene(n=400_000, seed=11):
-    """Density falling off exponentially to the right of the frame: tile lists
-    from a few instances to > 24576 (every work-list class)."""
+def graded_plane(n=400_000, seed=11, far=True):
+    """A fronto-parallel plane (depth jitter 1e-4) whose density falls off
+    exponentially to the right of the frame: tile lists from a few instances
+    to > 24576; with the far splat and 8 coarse bits each list is one run."""
     rng = np.random.default_rng(seed)
     x = -1.6 + rng.exponential(0.35, n)
     y = rng.uniform(-1.0, 1.0, n)
-    z = rng.uniform(-1.0, 1.0, n)
+    z = rng.uniform(-1e-4, 1e-4, n)
     scale = np.exp(rng.uniform(np.log(0.004), np.log(0.03), (n, 3)))
-    return _scene(np.stack([x, y, z], 1), scale, seed)
+    scale[:, 2] = 1e-4
+    xyz = np.stack([x, y, z], 1)
+    if far:
+        xyz = np.concatenate([xyz, [[0.0, 0.0, -400.0]]])
+        scale = np.concatenate([scale, [[2.0, 2.0, 2.0]]])
+    return _scene(xyz, scale, seed, opacity=(0.02, 0.2))
 
 
 def plane_scene(n=250_000, seed=12, far=True, levels=0):
@@ -94,8 +97,12 @@ def plane_scene(n=250_000, seed=12, far=True, levels=0):
     return _scene(xyz, scale, seed, opacity=(0.02, 0.2))
 
 
+def _coarse(monkeypatch, form):
+    monkeypatch.setenv("GSR_DEPTH_COARSE", {"exact": "0", "coarse": "16", "coarse8": "8"}[form])
+
+
 def _frames(monkeypatch, g, cam, st, form):
-    monkeypatch.setenv("GSR_TILE_DEPTH_SORT", "1" if form == "tile" else "0")
+    _coarse(monkeypatch, form)
     return gpu_frame(g, cam, st, with_debug=True)
 
 
@@ -105,27 +112,28 @@ def _same(a, b, what=""):
     assert a["stats"] == b["stats"], what
 
 
-def test_every_class_matches_exact_form(gpu, monkeypatch):
-    g = graded_scene()
+@pytest.mark.parametrize("form", ["coarse8", "coarse"])
+def test_every_class_matches_exact_form(gpu, monkeypatch, form):
+    g = graded_plane()
     cam = Camera(540, 960)
     st = _settings(t_min=0.0)
-    tile = _frames(monkeypatch, g, cam, st, "tile")
+    got = _frames(monkeypatch, g, cam, st, form)
     exact = _frames(monkeypatch, g, cam, st, "exact")
-    _same(tile, exact)
+    _same(got, exact)
     assert check_depth_order(exact, O.vertex_stage(g.flat(), g.sh_dim, uniforms_for(cam)))
-    lens = (tile["ranges"][:, 1] - tile["ranges"][:, 0]).astype(np.int64)
-    classes = set(tds_class(lens).tolist())
-    assert {0, 1, 2, 3, 4, 5, 6} <= classes, sorted(classes)
+    lens = (got["ranges"][:, 1] - got["ranges"][:, 0]).astype(np.int64)
+    classes = set(run_class(lens).tolist())
+    assert {0, 1, 2, 3, 4, 5, 6, 7} <= classes, sorted(classes)
     assert lens.max() > 2 * 12288, lens.max()  # several sub-blocks per pass on the global path
 
 
 def test_deep_lists_image_against_oracle(gpu, monkeypatch):
     """The global path's frame against the C oracle at the stated tolerances
     (small frame: every tile deep)."""
-    g = graded_scene(n=120_000, seed=5)
+    g = graded_plane(n=120_000, seed=5)
     cam = Camera(96, 160)
     st = _settings(t_min=0.0)
-    res = _frames(monkeypatch, g, cam, st, "tile")
+    res = _frames(monkeypatch, g, cam, st, "coarse8")
     lens = res["ranges"][:, 1].astype(np.int64) - res["ranges"][:, 0]
     assert lens.max() > CAP_BLOCK, lens.max()
     ref = C.render(g.flat(), g.sh_dim, uniforms_for(cam), mode="float")
@@ -147,7 +155,7 @@ def test_single_long_run(gpu, monkeypatch):
     g = _scene(xyz, scale, 21, opacity=(0.01, 0.05))
     cam = Camera(96, 160)
     st = _settings(t_min=0.0)
-    tile = _frames(monkeypatch, g, cam, st, "tile")
+    tile = _frames(monkeypatch, g, cam, st, "coarse")
     exact = _frames(monkeypatch, g, cam, st, "exact")
     _same(tile, exact)
     lens = tile["ranges"][:, 1].astype(np.int64) - tile["ranges"][:, 0]
@@ -163,7 +171,7 @@ def test_equal_depths(gpu, monkeypatch, levels):
     g = plane_scene(n=60_000, far=False, levels=levels)
     cam = Camera(270, 480)
     st = _settings(t_min=1e-4)
-    tile = _frames(monkeypatch, g, cam, st, "tile")
+    tile = _frames(monkeypatch, g, cam, st, "coarse")
     exact = _frames(monkeypatch, g, cam, st, "exact")
     _same(tile, exact, f"levels {levels}")
     assert tile["stats"]["n_instances"] > 50_000
@@ -171,7 +179,7 @@ def test_equal_depths(gpu, monkeypatch, levels):
 
 def _frame_ms(monkeypatch, g, cam, st, form, reps=10):
     from gsviewer_amd.rasterizer import HipContext, HipScene, camera_from, render_into
-    monkeypatch.setenv("GSR_TILE_DEPTH_SORT", "1" if form == "tile" else "0")
+    _coarse(monkeypatch, form)
     scene = HipScene.from_gaussian_data(g)
     ctx = HipContext()
     out = torch.empty((cam.h, cam.w, 3), dtype=torch.float32, device="cuda")
@@ -197,29 +205,33 @@ def test_plane_with_far_splat(gpu, monkeypatch):
     g = plane_scene()
     cam = Camera(1080, 1920)
     st = _settings(t_min=1e-4)
-    tile = _frames(monkeypatch, g, cam, st, "tile")
+    got = _frames(monkeypatch, g, cam, st, "coarse")
     exact = _frames(monkeypatch, g, cam, st, "exact")
-    _same(tile, exact)
-    lens = tile["ranges"][:, 1].astype(np.int64) - tile["ranges"][:, 0]
+    _same(got, exact)
+    lens = got["ranges"][:, 1].astype(np.int64) - got["ranges"][:, 0]
     assert lens.max() > 1000, lens.max()
-    ms_tile = _frame_ms(monkeypatch, g, cam, _settings(t_min=1e-4), "tile")
+    ms_coarse = _frame_ms(monkeypatch, g, cam, _settings(t_min=1e-4), "coarse")
     ms_exact = _frame_ms(monkeypatch, g, cam, _settings(t_min=1e-4), "exact")
-    print(f"plane + far splat, 1080p: per-tile {ms_tile:.3f} ms, exact {ms_exact:.3f} ms")
-    assert ms_tile <= 1.5 * ms_exact, (ms_tile, ms_exact)
+    print(f"plane + far splat, 1080p: coarse {ms_coarse:.3f} ms, exact {ms_exact:.3f} ms")
+    assert ms_coarse <= 1.5 * ms_exact, (ms_coarse, ms_exact)
 
 
 @pytest.mark.parametrize("scene_kind", ["graded", "plane"])
-def test_group_matches_exact_form(gpu, monkeypatch, scene_kind):
+def test_group_matches_frames_alone(gpu, monkeypatch, scene_kind):
+    """A group's frames (exact sort, gsr_render_finish_views) against the same
+    views rendered alone (coarse order + long runs), deep lists included.
+    (One chunk length for both: with t_min > 0 it decides where a pixel
+    stops, tests/test_gpu_multiview.py.)"""
     from gsviewer_amd.rasterizer import HipScene
-    g = graded_scene(n=200_000) if scene_kind == "graded" else plane_scene(n=100_000)
+    monkeypatch.setenv("GSR_CHUNK", "256")
+    monkeypatch.setenv("GSR_CHUNK_VIEWS", "256")
+    g = graded_plane(n=200_000) if scene_kind == "graded" else plane_scene(n=100_000)
     cams = [Camera(270, 480).yaw(v * 20.0) for v in range(3)]
-    res = {}
-    for form in ("tile", "exact"):
-        monkeypatch.setenv("GSR_TILE_DEPTH_SORT", "1" if form == "tile" else "0")
-        scene = HipScene.from_gaussian_data(g)
-        res[form] = batched_frames(scene, cams, _settings(t_min=1e-4), group=3, debug_views=(0, 1, 2))
-        scene.close()
+    st = _settings(t_min=1e-4)
+    scene = HipScene.from_gaussian_data(g)
+    group = batched_frames(scene, cams, st, group=3, debug_views=(0, 1, 2))
+    scene.close()
     for v in range(3):
-        a, b = res["tile"][v], res["exact"][v]
+        alone = _frames(monkeypatch, g, cams[v], st, "coarse8")
         for key in ("tile_list", "ranges", "records", "image"):
-            np.testing.assert_array_equal(a[key], b[key], err_msg=f"view {v} {key}")
+            np.testing.assert_array_equal(alone[key], group[v][key], err_msg=f"view {v} {key}")

@@ -119,15 +119,15 @@ def test_contexts_share_one_scene_concurrently(gpu):
 def test_shared_scene_pass_matches_serial_renders(gpu, monkeypatch, batched_sorts, batched_finish, mode):
     """gsr_render_begin_views (one cull + preprocess pass over the scene for a
     group of views) through ViewBatchPipeline with two groups: images, radii
-    and counts identical to each view rendered alone; with the group's sort
-    step and finish batched or per view in every combination (the sort step
-    leaves what the finish reads: the binning counts of the per-tile form, the
-    depth order of the exact form); also with one group finished a step after
-    it began (lookahead 1), with one host thread per group
-    (ThreadedViewBatchPipeline), and in the exact form (GSR_TILE_DEPTH_SORT=0)."""
+    and counts identical to each view rendered alone (a frame alone sorts
+    depth coarsely and repairs the tile lists' runs; a group's frames sort
+    exactly); with the group's sort step and finish batched or per view in
+    every combination; also with one group finished a step after it began
+    (lookahead 1), with one host thread per group (ThreadedViewBatchPipeline),
+    and against frames alone sorted exactly too (GSR_DEPTH_COARSE=0)."""
     import torch
 
-    monkeypatch.setenv("GSR_TILE_DEPTH_SORT", "0" if mode == "exact" else "1")
+    monkeypatch.setenv("GSR_DEPTH_COARSE", "0" if mode == "exact" else "16")
 
     from gsviewer_amd.multiview import ThreadedViewBatchPipeline, ViewBatchPipeline
     from gsviewer_amd.rasterizer import HipContext, render_into

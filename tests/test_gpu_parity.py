@@ -6,7 +6,7 @@ import pytest
 from gsviewer_amd.camera import Camera, euler_to_rotation_matrix
 from gsviewer_amd.gaussian_data import garden_standin, naive_gaussian, random_scene
 from oracle import gl_oracle as O
-from helpers import (TOL_TMIN, alpha_box_rects, check_depth_order, compare_images, decode_records, kept_fragments,
+from helpers import (TOL_TMIN, alpha_box_rects, compare_images, decode_records, frame_depth_order, kept_fragments,
                      narrowed_rects,
                      tile_lists_for, expected_interval_form, expected_quadratic, gpu_frame,
                      uniforms_for)
@@ -91,19 +91,16 @@ def test_preprocess_records_plain_for_other_fragment_classes(gpu, mode):
     assert np.all(rec["mid"] == 0)
 
 
-@pytest.mark.parametrize("form", ["tile", "exact"])
-def test_depth_order_and_tile_lists_exact(gpu, monkeypatch, form):
-    """Both depth-order forms: the per-tile sort (default) and the exact
-    global sort (GSR_TILE_DEPTH_SORT=0), whose global order is also checked."""
-    monkeypatch.setenv("GSR_TILE_DEPTH_SORT", "1" if form == "tile" else "0")
+def test_depth_order_and_tile_lists_exact(gpu):
     g = random_scene(4000, sh_degree=0, seed=5)
     cam = Camera(80, 112).yaw(-35)
     res = gpu_frame(g, cam, _settings(t_min=0.0), with_debug=True)
     U = uniforms_for(cam)
     vs = O.vertex_stage(g.flat(), 3, U)
     vis_desc = np.nonzero(vs["visible"])[0][::-1]
-    # the exact form's global order: the reverse of the GL draw order
-    assert check_depth_order(res, vs) == (form == "exact")
+    # the frame's global order: the coarse depth order (helpers.frame_depth_order),
+    # or, with GSR_DEPTH_COARSE=0, the reverse of the GL draw order
+    np.testing.assert_array_equal(vis_desc[res["depth_order"]], frame_depth_order(vs, res["depth_coarse"]))
     # per-tile instance lists == GL order restricted to the tile, reversed, over
     # the quads narrowed by the alpha box
     rects = narrowed_rects(res, vs, U)

@@ -12,7 +12,7 @@ import pytest
 from gsviewer_amd.camera import Camera
 from gsviewer_amd.gaussian_data import GaussianData, garden_standin, random_scene
 from oracle import gl_oracle as O
-from helpers import check_depth_order, gpu_frame, narrowed_rects, uniforms_for
+from helpers import frame_depth_order, gpu_frame, narrowed_rects, uniforms_for
 
 pytestmark = pytest.mark.gpu
 
@@ -47,7 +47,7 @@ def check_frame_order(res, vs, U):
     assert res["stats"]["n_visible"] == nv
     # global front-to-back order == reverse of the GL draw order (ties: descending id)
     f2b = O.sort_back_to_front(vs["view_z"], vis)[::-1]
-    check_depth_order(res, vs)  # (the exact form's global order; the default form has none)
+    np.testing.assert_array_equal(vis_desc[res["depth_order"]], frame_depth_order(vs, res["depth_coarse"]))
     # every tile list == the global order restricted to the tile
     rank = np.empty(len(vis), np.int64)
     rank[f2b] = np.arange(nv)

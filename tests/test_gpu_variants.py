@@ -1,15 +1,9 @@
 """The pipeline's alternative stage forms give identical frames:
 
-* GSR_TILE_DEPTH_SORT (default 1): the per-tile depth sort (binning in slot
-  order, each tile's list sorted by depth key, tile_sort.hip) against the
-  exact global depth sort before a binning in depth order: the same tile
-  lists by two independent constructions;
-* GSR_BIN_FUSED (default 1; the exact form's knob, the per-tile form always
-  fuses): the binning with the tile sort's first radix pass fused in
-  (k_bin_hist + k_bin_scatter) against the separate binning and full tile
-  sort (k_bin_reduce + k_bin_write, then every radix pass): integer index work;
-* GSR_NO_RECT_PAYLOAD (exact form): the binning gathers the tile rects by
-  slot instead of taking them from the depth sort's payload;
+* GSR_BIN_FUSED (default 1): the binning with the tile sort's first radix
+  pass fused in (k_bin_hist + k_bin_scatter) against the separate binning and
+  full tile sort (k_bin_reduce + k_bin_write, then every radix pass): integer
+  index work;
 * GSR_TAIL_MERGE (groups, default 1) / GSR_TAIL_MERGE_ALONE (a frame alone,
   default 0): a multi-chunk tile folded by its last chunk to finish, inside
   the compositing launch, against the k_merge launch: the same fold in the
@@ -19,10 +13,9 @@
   the compaction scan + k_preprocess (tests/helpers.grab_debug maps the
   uncompacted slots to the compacted ones by rank).
 
-Images, records, tile lists and tile ranges (and the exact forms' global
-depth orders) must be bit-identical, on a frame rendered alone (gsr_render)
-and on a group of views (gsr_render_finish_views), for frame sizes whose tile
-ids take one radix pass (<= 2048 tiles) and two, plus the full-size C2 frame."""
+Images, records, depth order, tile lists and tile ranges must be bit-identical, on a frame rendered alone (gsr_render) and on a group of
+views (gsr_render_finish_views), for frame sizes whose tile ids take one
+radix pass (<= 2048 tiles) and two, plus the full-size C2 frame."""
 import numpy as np
 import pytest
 
@@ -32,9 +25,8 @@ from helpers import batched_frames, gpu_frame
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [{}, {"GSR_TILE_DEPTH_SORT": "0"}, {"GSR_TILE_DEPTH_SORT": "0", "GSR_BIN_FUSED": "0"},
-            {"GSR_TAIL_MERGE": "0", "GSR_TAIL_MERGE_ALONE": "1"}, {"GSR_FUSED_CULL": "0"},
-            {"GSR_TILE_DEPTH_SORT": "0", "GSR_NO_RECT_PAYLOAD": "1"}]
+VARIANTS = [{}, {"GSR_BIN_FUSED": "0"}, {"GSR_TAIL_MERGE": "0", "GSR_TAIL_MERGE_ALONE": "1"},
+            {"GSR_FUSED_CULL": "0"}]
 
 
 def _settings(**kw):
@@ -43,8 +35,7 @@ def _settings(**kw):
 
 
 def _frames(monkeypatch, env, g, scene, cams):
-    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE", "GSR_FUSED_CULL", "GSR_TILE_DEPTH_SORT",
-              "GSR_NO_RECT_PAYLOAD"):
+    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE", "GSR_FUSED_CULL", "GSR_DEPTH_COARSE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -68,10 +59,8 @@ def test_stage_variants_identical(gpu, monkeypatch, h, w, n):
             assert alone["stats"]["n_instances"] > 0
             continue
         for a, b in ((ref[0], alone), (ref[1][0], group[0])):
-            for key in ("tile_list", "ranges", "records"):
+            for key in ("tile_list", "ranges", "depth_order", "records"):
                 np.testing.assert_array_equal(a[key], b[key], err_msg=f"{env} {key}")
-            if a["depth_order"].size and b["depth_order"].size:  # (only the exact form has a global order)
-                np.testing.assert_array_equal(a["depth_order"], b["depth_order"], err_msg=f"{env} depth_order")
             np.testing.assert_array_equal(a["image"], b["image"], err_msg=f"{env} image")
         for v in range(1, len(cams)):
             np.testing.assert_array_equal(ref[1][v]["image"], group[v]["image"], err_msg=f"{env} view {v}")

@@ -1,8 +1,8 @@
 #!/bin/bash
 # GPU check of the current tree on one MI355X (run through gpurun):
-# build, parity tests, smoke, bench, rocprofv3 kernel stats, HBM PMC passes.
+# load, parity tests, smoke, bench, rocprofv3 kernel stats, HBM PMC passes.
 # usage: gpurun --timeout 1100 -- bash tools/gpu_round.sh TAG [quick|full]
-#   quick: build, parity tests, smoke, bench (no CPU baseline), kernel stats
+#   quick: load, parity tests, smoke, bench (no CPU baseline), kernel stats
 #   full: + the CPU baseline and the PMC traffic passes (tools/pmc.sh TAG traffic)
 # Every step has its own time limit; the first failing step ends the script.
 TAG=${1:-run}
@@ -24,7 +24,8 @@ step() {  # step NAME SECONDS CMD...
     fi
 }
 
-step build 300 bash -c "python -c 'import __graft_entry__ as g; g.build()' > $O/build.log 2>&1"
+# (the library is built here, in-tree, and travels with the tree: the driver runs without building)
+step load 120 bash -c "python -c 'from gsviewer_amd import _lib; _lib.load()' > $O/load.log 2>&1"
 step pytest_gpu 600 bash -c "python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1"
 step smoke 120 bash -c "python -c 'import __graft_entry__ as g; g.smoke()' > $O/smoke.log 2>&1"
 if [ "$MODE" = quick ]; then
