@@ -805,6 +805,7 @@ int gsr_context_reserve(gsr_context* c, int64_t n, int32_t width, int32_t height
     if (c->depth_coarse_alone && c->bin_fused) {  // a frame alone's depth keys through the tile sort
         if ((rc = c->tpay_a.ensure(d, "tile_pay"))) return rc;
         if ((rc = c->tpay_b.ensure(d, "tile_pay"))) return rc;
+        if ((rc = c->long_runs.ensure(long_runs_elems(d), "long_runs"))) return rc;
     }
     if ((rc = c->radix_tmp.ensure(std::max({radix_tmp_elems(d), radix_tmp_elems(un), rhist}), "radix_tmp"))) return rc;
     const size_t mc = (size_t)num_tiles + d / std::min(c->chunk, c->chunk_views) + 1;

@@ -24,7 +24,7 @@ def depth_coarse_bits(path="alone") -> int:
     alone (gsr_render; GSR_DEPTH_COARSE=0 exact, 8..16 otherwise), 0 for a
     group's frames (always exact)."""
     import os
-    if path != "alone":
+    if path != "alone" or os.environ.get("GSR_BIN_FUSED") == "0":  # (the repair needs the fused binning's keys)
         return 0
     bits = 16
     v = os.environ.get("GSR_DEPTH_COARSE")

@@ -60,6 +60,8 @@ def test_stage_variants_identical(gpu, monkeypatch, h, w, n):
             continue
         for a, b in ((ref[0], alone), (ref[1][0], group[0])):
             for key in ("tile_list", "ranges", "depth_order", "records"):
+                if key == "depth_order" and a["depth_coarse"] != b["depth_coarse"]:
+                    continue  # (GSR_BIN_FUSED=0 sorts exactly: the repair needs the fused binning's keys)
                 np.testing.assert_array_equal(a[key], b[key], err_msg=f"{env} {key}")
             np.testing.assert_array_equal(a["image"], b["image"], err_msg=f"{env} image")
         for v in range(1, len(cams)):

@@ -26,7 +26,7 @@ step() {  # step NAME SECONDS CMD...
 
 # (the library is built here, in-tree, and travels with the tree: the driver runs without building)
 step load 120 bash -c "python -c 'from gsviewer_amd import _lib; _lib.load()' > $O/load.log 2>&1"
-step pytest_gpu 600 bash -c "python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1"
+step pytest_gpu 600 bash -c "python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1"
 step smoke 120 bash -c "python -c 'import __graft_entry__ as g; g.smoke()' > $O/smoke.log 2>&1"
 if [ "$MODE" = quick ]; then
     step bench 300 bash -c "python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err"
