@@ -21,7 +21,7 @@ BUILD = os.path.join(ROOT, "build", "gsr")
 LIB = os.path.join(PKG, "libgsr.so")
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["api.hip", "scene.hip", "scan.hip", "radix_sort.hip", "preprocess.hip", "composite.hip", "tile_sort.hip",
+SOURCES = ["api.hip", "scene.hip", "scan.hip", "radix_sort.hip", "preprocess.hip", "composite.hip",
            "export.hip",
            "ply.cpp"]
 # The per-Gaussian stage must evaluate exactly like the oracle: no contraction.

@@ -140,7 +140,7 @@ constexpr int kDepthPassesAlone = 3;
 // order.  Only each tile's list needs the exact (key, slot) order: the
 // binning and the tile sort carry each instance's full depth key, and
 // k_tile_ranges restores the order run by run (RunFix; runs that outgrow its
-// register window go to k_long_runs, tile_sort.hip).  Needs the fused binning
+// register window go to k_long_runs, long_runs.h).  Needs the fused binning
 // (which carries the keys; GSR_BIN_FUSED=0 sorts exactly).  A group's frames
 // (gsr_render_begin_views / _sorts / _finish_views) keep the exact sort (4
 // passes of <= 8 bits): in flight the sort's VALU work is the same in 3 or 4
@@ -1165,7 +1165,10 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     const RunFix fix{tva, c->zero.p + zl.key_range, f.coarse, tkb, tvb, carry ? tpa : nullptr,
                      carry ? c->long_runs.p : nullptr, c->zero.p + zl.long_runs};
     if (n_dup > 0 && (rc = launch_tile_ranges(tka, n_dup, ranges, fix, s))) return rc;
-    if (n_dup > 0 && f.coarse && (rc = launch_long_runs(tka, n_dup, ranges, fix, s))) return rc;
+    // the runs longer than the repair's: by the chunk-count launch, or alone (no chunks: RGBA8)
+    const LongRuns long_runs{tka, n_dup, fix};
+    const bool runs_apart = n_dup > 0 && f.coarse && f.blend == GSR_BLEND_UNORM8;
+    if (runs_apart && (rc = launch_long_runs(tka, n_dup, ranges, fix, s))) return rc;
 
     if (f.blend == GSR_BLEND_UNORM8) {  // the RGBA8 framebuffer: whole lists, back to front, no chunks
         if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
@@ -1183,7 +1186,8 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
         if ((rc = c->tmax.ensure(max_chunks, "tmax"))) return rc;
         if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->len_classes, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
-                                c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s, c->first_major_alone)))
+                                c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s, c->first_major_alone,
+                                f.coarse ? &long_runs : nullptr)))
             return rc;
         if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
         if ((rc = launch_composite(c->chunk_desc.p, c->chunk_order.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,

@@ -18,6 +18,7 @@
 #include <cstdlib>
 
 #include "gsr_internal.h"
+#include "long_runs.h"
 
 namespace gsr {
 namespace {
@@ -632,7 +633,7 @@ constexpr int kRangeItems = 16;
 // holding its first instance), so its reads all precede its writes; other
 // threads read the run's slots only for their (tile, coarse key), which the
 // permutation leaves unchanged.  O(L^2), so only runs of at most kFixRunMax
-// instances: a longer one is listed for k_long_runs (tile_sort.hip), which
+// instances: a longer one is listed for k_long_runs (long_runs.h), which
 // sorts it on chip in bounded time (round 4's unbounded form could spend
 // ~5e8 serial steps on one dense tile).
 __device__ __noinline__ void fix_run(const uint32_t* __restrict__ keys, uint32_t n, uint32_t* vals,
@@ -949,16 +950,19 @@ __device__ __forceinline__ uint32_t first_class_of(uint2 r, uint32_t chunk, uint
     return first_major && (r.y - r.x) >= chunk ? 0u : partial_class_of(r, chunk, classes);
 }
 
+// Tiles [grp * kThreads, (grp + 1) * kThreads) of ngrp such groups, thread lt
+// of the group's kThreads (every thread of the launch's blocks calls it: one
+// workgroup barrier)
 __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
                                             uint32_t classes, bool first_major, uint32_t* __restrict__ tot,
-                                            uint32_t (*lds)[kThreads / 64]) {
-    const int t = blockIdx.x * kThreads + threadIdx.x;
+                                            uint32_t (*lds)[kThreads / 64], uint32_t grp, uint32_t ngrp, uint32_t lt) {
+    const int t = (int)(grp * kThreads + lt);
     const bool valid = t < num_tiles;
     const uint2 r = valid ? ranges[t] : make_uint2(0u, 0u);
     const uint32_t e = wave_reduce_sum(valid ? chunks_of(r, chunk) - 1u : 0u);
     const uint32_t f = wave_reduce_sum(first_full_of(r, chunk, first_major));
     const uint32_t pc = valid ? first_class_of(r, chunk, classes, first_major) : 0u;
-    const int w = threadIdx.x >> 6;
+    const int w = (int)(lt >> 6);
     if (__lane_id() == 0) {
         lds[0][w] = e;
         lds[1][w] = f;
@@ -968,16 +972,35 @@ __device__ __forceinline__ void chunk_count(const uint2* __restrict__ ranges, in
         if (__lane_id() == 0) lds[1 + k][w] = n;
     }
     __syncthreads();
-    if (threadIdx.x <= classes)
-        tot[threadIdx.x * gridDim.x + blockIdx.x] =
-            lds[threadIdx.x][0] + lds[threadIdx.x][1] + lds[threadIdx.x][2] + lds[threadIdx.x][3];
+    if (lt <= classes && grp < ngrp) tot[lt * ngrp + grp] = lds[lt][0] + lds[lt][1] + lds[lt][2] + lds[lt][3];
 }
 
 __global__ __launch_bounds__(kThreads) void k_chunk_count(const uint2* __restrict__ ranges, int num_tiles,
                                                           uint32_t chunk, uint32_t classes,
                                                           uint32_t* __restrict__ tot, uint32_t first_major) {
     __shared__ uint32_t lds[1 + kMaxLenClasses][kThreads / 64];
-    chunk_count(ranges, num_tiles, chunk, classes, first_major != 0, tot, lds);
+    chunk_count(ranges, num_tiles, chunk, classes, first_major != 0, tot, lds, blockIdx.x, gridDim.x, threadIdx.x);
+}
+
+// The chunk counts with the coarse depth order's long runs (long_runs.h) in
+// the same launch: blocks [0, n_cc) count (four tile groups of kThreads each,
+// k_chunk_count's blocks), the rest sort the listed runs.  Saves the runs'
+// own launch (4.7 us when there are none, profiles/r5_s14).
+constexpr int kCountGroups = kTdsThreads / kThreads;
+__global__ __launch_bounds__(kTdsThreads) void k_chunk_count_long(const uint2* __restrict__ ranges, int num_tiles,
+                                                                  uint32_t chunk, uint32_t classes,
+                                                                  uint32_t* __restrict__ tot, uint32_t first_major,
+                                                                  uint32_t n_cc, LongRunArgs la) {
+    __shared__ TdsLds S;
+    __shared__ uint32_t lds[kCountGroups][1 + kMaxLenClasses][kThreads / 64];
+    if (blockIdx.x < n_cc) {
+        const uint32_t g = threadIdx.x / kThreads;
+        const uint32_t ngrp = (uint32_t)((num_tiles + kThreads - 1) / kThreads);
+        chunk_count(ranges, num_tiles, chunk, classes, first_major != 0, tot, lds[g], blockIdx.x * kCountGroups + g,
+                    ngrp, threadIdx.x % kThreads);
+        return;
+    }
+    long_runs_block(la, S, blockIdx.x - n_cc, gridDim.x - n_cc);
 }
 
 struct ChunkWriteLds {
@@ -1118,7 +1141,8 @@ __global__ __launch_bounds__(kThreads) void k_chunk_count_views(ChunkViews vs, i
                                                                 uint32_t classes, uint32_t first_major) {
     __shared__ uint32_t lds[1 + kMaxLenClasses][kThreads / 64];
     const ChunkView& v = vs.v[blockIdx.y];
-    chunk_count(v.ranges, num_tiles, chunk, classes, first_major != 0, v.chunk_cnt + num_tiles, lds);
+    chunk_count(v.ranges, num_tiles, chunk, classes, first_major != 0, v.chunk_cnt + num_tiles, lds, blockIdx.x,
+                gridDim.x, threadIdx.x);
 }
 
 __global__ __launch_bounds__(kThreads) void k_chunk_write_views(ChunkViews vs, int num_tiles, uint32_t chunk,
@@ -2256,7 +2280,7 @@ const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uin
 
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
-                  hipStream_t s, bool first_major) {
+                  hipStream_t s, bool first_major, const LongRuns* long_runs) {
 #ifndef GSR_COMP_BOUND
     tmax = nullptr;  // the published maxima are only read by the bound variant
 #endif
@@ -2264,11 +2288,30 @@ int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t c
     const unsigned g = (unsigned)((num_tiles + kThreads - 1) / kThreads);
     // the per-block totals live in chunk_cnt past its num_tiles entries
     uint32_t* tot = chunk_cnt + num_tiles;
-    k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot, first_major ? 1u : 0u);
-    GSR_LAUNCH_CHECK("chunk_count");
+    if (long_runs && long_runs->n_dup > 0 && long_runs->fix.coarse) {
+        LongRunArgs la;
+        if (int rc = long_run_args(long_runs->tile_keys, long_runs->n_dup, ranges, long_runs->fix, la)) return rc;
+        const unsigned n_cc = (g + kCountGroups - 1) / kCountGroups;
+        k_chunk_count_long<<<n_cc + kLongGrid, kTdsThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot,
+                                                                    first_major ? 1u : 0u, n_cc, la);
+        GSR_LAUNCH_CHECK("chunk_count_long");
+    } else {
+        k_chunk_count<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot, first_major ? 1u : 0u);
+        GSR_LAUNCH_CHECK("chunk_count");
+    }
     k_chunk_write<<<g, kThreads, 0, s>>>(ranges, num_tiles, chunk, classes, tot, chunk_cnt, chunk_base, n_extra_dev,
                                          desc, order, tmax, first_major ? 1u : 0u);
     GSR_LAUNCH_CHECK("chunk_write");
+    return GSR_OK;
+}
+
+int launch_long_runs(const uint32_t* tile_keys, uint32_t n_dup, const uint2* ranges, const RunFix& fix,
+                     hipStream_t s) {
+    if (n_dup == 0 || fix.coarse == 0) return GSR_OK;
+    LongRunArgs a;
+    if (int rc = long_run_args(tile_keys, n_dup, ranges, fix, a)) return rc;
+    k_long_runs<<<kLongGrid, kTdsThreads, 0, s>>>(a);
+    GSR_LAUNCH_CHECK("long_runs");
     return GSR_OK;
 }
 

@@ -437,7 +437,7 @@ int launch_binning(const uint32_t* sorted_ids, const uint2* trect, const uint32_
 // order, in place.  coarse == 0 (an exact depth sort): nothing to repair.
 // Runs longer than kFixRunMax that reach past a thread's register window are
 // not repaired there: their starts go to long_starts (*long_count, zeroed per
-// frame) and launch_long_runs sorts them (tile_sort.hip).
+// frame) and launch_long_runs sorts them (long_runs.h).
 struct RunFix {
     uint32_t* vals;             // the tile list (slots), repaired in place
     const uint32_t* key_range;  // the frame's {~kmin, kmax}
@@ -454,13 +454,13 @@ inline size_t long_run_cap(size_t n_dup) { return n_dup / (kFixRunMax + 1) + 1; 
 inline size_t long_runs_elems(size_t n_dup) { return 2 * long_run_cap(n_dup); }
 int launch_tile_ranges(const uint32_t* tile_keys, uint32_t n_dup, uint2* ranges, const RunFix& fix,
                        hipStream_t s);
-// tile_sort.hip: the coarse order's long runs (RunFix::long_starts), each
+// long_runs.h: the coarse order's long runs (RunFix::long_starts), each
 // bounded by a 64-way search from its start (runs are stretches of one tile's
 // list with equal coarse key, ranges[tile] bounds them) and sorted by (full
 // key, slot) on chip: up to 1024 instances by one wave, up to 24576 by a
 // 1024-thread block in registers, longer ones by a block through the scratch
 // buffers.  A fixed grid takes the listed runs in turn and exits at once when
-// there are none.
+// there are none (a launch of its own; launch_chunks takes them as extra blocks).
 int launch_long_runs(const uint32_t* tile_keys, uint32_t n_dup, const uint2* ranges, const RunFix& fix,
                      hipStream_t s);
 // The binning with the tile sort's first radix pass fused in (composite.hip,
@@ -480,9 +480,16 @@ size_t chunk_cnt_elems(int num_tiles);
 // classes (2 .. kMaxLenClasses): dispatch order = full chunks, then the partial
 // ones in classes - 1 length classes, longest first; the frame's chunk count
 // of each class lands at chunk_class_totals(chunk_cnt, num_tiles, classes)
+// long_runs (nullable): the frame's coarse-order long runs, sorted by extra
+// blocks of the chunk-count launch (in place of launch_long_runs)
+struct LongRuns {
+    const uint32_t* tile_keys;
+    uint32_t n_dup;
+    RunFix fix;
+};
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
-                  hipStream_t s, bool first_major = false);
+                  hipStream_t s, bool first_major = false, const LongRuns* long_runs = nullptr);
 const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes);
 int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n_chunks_dev, uint32_t max_chunks,
                      const uint32_t* chunk_cnt, const uint32_t* chunk_base, uint32_t* sat,

@@ -20,8 +20,11 @@
 // it is latency-bound (one wave ~5 us per run, a workgroup 20-25 us,
 // profiles/r5_s13); here it only covers what the coarse order leaves.
 //
-// One launch, a fixed grid of 1024-thread blocks; block b takes the listed
-// runs b, b + G, ...:
+// Device code only, included by composite.hip: the runs are sorted by extra
+// blocks of the chunk-count launch (k_chunk_count_long), or by a launch of
+// their own (k_long_runs) where no chunks are built (the RGBA8 framebuffer).
+// A fixed set of G 1024-thread blocks; block b takes the listed runs
+// b, b + G, ...:
 //   * each wave finds one run's end (a 64-way search between its start and
 //     its tile's end: tile key and coarse key are nondecreasing along the
 //     list, so "still in the run" is a prefix) and, up to 1024 instances,
@@ -36,6 +39,7 @@
 // never written and a run's permutation keeps its coarse key, so the search's
 // answer does not depend on it.
 
+#pragma once
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -458,18 +462,17 @@ __device__ uint32_t run_end(const LongRunArgs& a, uint32_t b, uint32_t hi, uint3
     return up;
 }
 
-__global__ __launch_bounds__(kTdsThreads) void k_long_runs(LongRunArgs a) {
-    __shared__ TdsLds S;
+// The runs of block `bid` of G (S: the block's LDS; every thread of the block calls it).
+__device__ void long_runs_block(const LongRunArgs& a, TdsLds& S, uint32_t bid, uint32_t G) {
     const uint32_t n_long = *a.count;
-    if (blockIdx.x >= n_long) return;
+    if (bid >= n_long) return;
     const uint32_t w = threadIdx.x >> 6, lane = __lane_id();
     uint32_t kmin;
     const uint32_t s0 = coarse_shift(a.key_range, a.coarse, kmin);  // > 0: a long run was listed
-    const uint32_t G = gridDim.x;
-    const uint32_t mine = (n_long - blockIdx.x + G - 1u) / G;  // this block's runs: blockIdx.x + j G, j < mine
+    const uint32_t mine = (n_long - bid + G - 1u) / G;  // this block's runs: bid + j G, j < mine
     // 1. one wave per run: its end, and the sort of a run of <= kTdsCapWave
     for (uint32_t j = w; j < mine; j += kTdsWaves) {
-        const uint32_t r = blockIdx.x + j * G;
+        const uint32_t r = bid + j * G;
         const uint32_t b = a.starts[r];
         const uint32_t tile = a.tile_keys[b];
         const uint32_t cv = (a.inst_keys[b] - kmin) >> s0;
@@ -480,7 +483,7 @@ __global__ __launch_bounds__(kTdsThreads) void k_long_runs(LongRunArgs a) {
     __syncthreads();  // (the lengths are this block's own writes)
     // 2. the whole block per longer run
     for (uint32_t j = 0; j < mine; ++j) {
-        const uint32_t r = blockIdx.x + j * G;
+        const uint32_t r = bid + j * G;
         const uint32_t L = a.lens[r];
         if (L <= kTdsCapWave) continue;
         const uint32_t b = a.starts[r];
@@ -492,20 +495,22 @@ __global__ __launch_bounds__(kTdsThreads) void k_long_runs(LongRunArgs a) {
     }
 }
 
-}  // namespace
+__global__ __launch_bounds__(kTdsThreads) void k_long_runs(LongRunArgs a) {
+    __shared__ TdsLds S;
+    long_runs_block(a, S, blockIdx.x, gridDim.x);
+}
 
-int launch_long_runs(const uint32_t* tile_keys, uint32_t n_dup, const uint2* ranges, const RunFix& fix,
-                     hipStream_t s) {
-    if (n_dup == 0 || fix.coarse == 0) return GSR_OK;
+// The launch arguments of the runs of a frame (null-checked).
+inline int long_run_args(const uint32_t* tile_keys, uint32_t n_dup, const uint2* ranges, const RunFix& fix,
+                         LongRunArgs& a) {
     if (!tile_keys || !ranges || !fix.inst_keys || !fix.vals || !fix.scratch_keys || !fix.scratch_vals ||
         !fix.long_starts || !fix.long_count || !fix.key_range)
         return set_error(GSR_ERR_INVALID, "long runs: null buffer");
-    const LongRunArgs a{tile_keys, ranges, fix.inst_keys, fix.vals, fix.scratch_keys, fix.scratch_vals,
-                        fix.key_range, fix.coarse, fix.long_starts, fix.long_count,
-                        fix.long_starts + long_run_cap(n_dup)};
-    k_long_runs<<<kLongGrid, kTdsThreads, 0, s>>>(a);
-    GSR_LAUNCH_CHECK("long_runs");
+    a = LongRunArgs{tile_keys, ranges, fix.inst_keys, fix.vals, fix.scratch_keys, fix.scratch_vals,
+                    fix.key_range, fix.coarse, fix.long_starts, fix.long_count,
+                    fix.long_starts + long_run_cap(n_dup)};
     return GSR_OK;
 }
 
+}  // namespace
 }  // namespace gsr

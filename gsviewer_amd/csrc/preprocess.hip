@@ -955,12 +955,7 @@ static unsigned preprocess_grid(int64_t n, bool alone = false) {
             c = 256;
         return c;
     }();
-    static const long knob = [] {  // experiment knob (read once per process): blocks per CU for both
-        const char* e = std::getenv("GSR_PRE_BLOCKS_PER_CU");
-        const long v = e ? std::strtol(e, nullptr, 10) : 0;
-        return (v >= 1 && v <= 32) ? v : 0L;
-    }();
-    const unsigned per_cu = knob ? (unsigned)knob : (alone ? 3u : 4u);
+    const unsigned per_cu = alone ? 3u : 4u;  // (measured: profiles/r4_s8, r4_s27)
     return std::max(1u, std::min((unsigned)((n + kThreads - 1) / kThreads), per_cu * (unsigned)cus));
 }
 

@@ -4,7 +4,7 @@ A frame's depth sort orders only the top bits of its key range (2 radix
 passes) and keeps equal coarse keys in slot order; k_tile_ranges then puts
 every run of one tile's instances with equal coarse keys into the exact
 (key, slot) order (composite.hip fix_run; runs longer than 16 in
-tile_sort.hip k_long_runs, tests/test_gpu_long_runs.py).  What the compositor reads -- the
+long_runs.h k_long_runs, tests/test_gpu_long_runs.py).  What the compositor reads -- the
 tile lists, their ranges, the records -- and so the image must be exactly the
 exact sort's:
 

@@ -8,7 +8,12 @@ the batched finish: binning, tile lists, compositing, merge) with planar
 
 * C2: 1M garden stand-in, SH 3, 1920x1080, t_min 1e-4 (the bench) and 0;
 * C3: 6M synthetic, SH 3, 1920x1080;
-* C5: 1M, SH 3, 3840x2160, no box / AABB / OBB (SURVEY.md 8d C5 settings).
+* C5: 1M, SH 3, 3840x2160, no box / AABB / OBB (SURVEY.md 8d C5 settings);
+* the bench's exact shape at C2: groups of 5 views, two groups in flight on
+  their own streams, stepped round the ring as bench.py's timed region does
+  (each context renders its view again), t_min 1e-4;
+* the C2 frame alone through gsr_render (the drop-in render() path: coarse
+  depth order + run repair), t_min 1e-4.
 
 Per view: the image against the oracle with the stated tolerances (helpers.py)
 plus an absolute census of the channels above 2e-5 (+ t_min), bounded at what
@@ -28,7 +33,8 @@ from gsviewer_amd.camera import Camera, euler_to_rotation_matrix
 from gsviewer_amd.gaussian_data import garden_standin
 from oracle import c_oracle as C
 from oracle import gl_oracle as O
-from helpers import TOL_EXACT, TOL_TMIN, batched_frames, compare_images, error_census, uniforms_for
+from helpers import (TOL_EXACT, TOL_TMIN, batched_frames, compare_images, error_census, gpu_frame, grab_debug,
+                     uniforms_for)
 from test_gpu_scale import check_frame_order
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
@@ -72,16 +78,16 @@ def _box(g, kind):
     return {}
 
 
-def _run(case, n, seed, W, H, t_min, box="none", order_check=True):
-    g, scene = _scene(n, seed)
-    st = _settings(t_min=t_min, **_box(g, box))
-    cams = [Camera(H, W).yaw(45.0 * v) for v in range(4)]
-    res = batched_frames(scene, cams, st, group=4, debug_views=(0,) if order_check else ())
+def _check(case, g, st, cams, res, n, W, H, t_min, box="none", order_check=True):
     flat = g.flat()
     tol = TOL_EXACT + (TOL_TMIN if t_min > 0 else 0.0)
+    refs = {}
     for v, (cam, r) in enumerate(zip(cams, res)):
         U = uniforms_for(cam, st)
-        ref = C.render(flat, g.sh_dim, U, threads=THREADS)
+        key = np.asarray(cam.get_view_matrix(), np.float32).tobytes()  # (views yawed by 360 share one render)
+        if key not in refs:
+            refs[key] = C.render(flat, g.sh_dim, U, threads=THREADS)
+        ref = refs[key]
         cen = error_census(r["image"], ref, tol)
         cen.update(case=case, view=v, t_min=t_min, n=n, width=W, height=H, box=box,
                    n_visible=r["stats"]["n_visible"], n_instances=r["stats"]["n_instances"])
@@ -96,6 +102,14 @@ def _run(case, n, seed, W, H, t_min, box="none", order_check=True):
             assert r["stats"]["n_visible"] == int(vs["visible"].sum())
             check_frame_order(r, vs, U)
     return res
+
+
+def _run(case, n, seed, W, H, t_min, box="none", order_check=True):
+    g, scene = _scene(n, seed)
+    st = _settings(t_min=t_min, **_box(g, box))
+    cams = [Camera(H, W).yaw(45.0 * v) for v in range(4)]
+    res = batched_frames(scene, cams, st, group=4, debug_views=(0,) if order_check else ())
+    return _check(case, g, st, cams, res, n, W, H, t_min, box, order_check)
 
 
 def test_c2_bench_path_tmin(gpu):
@@ -122,3 +136,47 @@ def test_c5_4k_obb(gpu):
 
 def test_c3_6m(gpu):
     _run("C3", 6_000_000, 2, 1920, 1080, 1e-4)
+
+
+def test_c2_bench_shape_groups_of_5(gpu):
+    """bench.py's timed shape (bench.py --inflight 20: groups of 5 views, one
+    stream per group, ViewBatchPipeline stepped round the ring), here two
+    groups of 5 stepped 5 times (every context renders its view again)."""
+    import torch
+
+    from gsviewer_amd.multiview import ViewBatchPipeline
+    from gsviewer_amd.rasterizer import HipContext, camera_from
+    n, W, H, K, G = 1_000_000, 1920, 1080, 5, 2
+    g, scene = _scene(n, 1)
+    st = _settings(t_min=1e-4)
+    st.out_layout = 0
+    cams = [Camera(H, W).yaw(45.0 * v) for v in range(K * G)]
+    ctxs = [HipContext() for _ in cams]
+    outs = [torch.full((3, H, W), -1.0, dtype=torch.float32, device="cuda") for _ in cams]
+    streams = [torch.cuda.Stream() for _ in range(G)]
+    camcs = [camera_from(c) for c in cams]
+    groups = [(ctxs[i:i + K], camcs[i:i + K], outs[i:i + K], streams[i // K]) for i in range(0, K * G, K)]
+    pipe = ViewBatchPipeline(groups, scene, st)
+    for _ in range(2 * G + 1):
+        pipe.step()
+    pipe.drain()
+    torch.cuda.synchronize()
+    res = []
+    for v, (ctx, out) in enumerate(zip(ctxs, outs)):
+        r = {"image": out.permute(1, 2, 0).contiguous().cpu().numpy(), "stats": ctx.stats(), "depth_coarse": 0}
+        if v == 0:
+            r.update(grab_debug(ctx, r["stats"]))
+        res.append(r)
+    for c in ctxs:
+        c.close()
+    _check("C2 groups of 5", g, st, cams, res, n, W, H, 1e-4)
+
+
+def test_c2_frame_alone(gpu):
+    """The drop-in render() path at C2: gsr_render (coarse depth order, run
+    repair, per-frame chunking)."""
+    g, _ = _scene(1_000_000, 1)
+    st = _settings(t_min=1e-4)
+    cam = Camera(1080, 1920)
+    r = gpu_frame(g, cam, st, with_debug=True)
+    _check("C2 alone", g, st, [cam], [r], 1_000_000, 1920, 1080, 1e-4)

@@ -1,4 +1,4 @@
-"""The coarse depth order's long runs (gsviewer_amd/csrc/tile_sort.hip k_long_runs).
+"""The coarse depth order's long runs (gsviewer_amd/csrc/long_runs.h k_long_runs).
 
 A frame alone sorts depth by the top GSR_DEPTH_COARSE bits of its key range
 (default 16); the stable binning and tile sort leave each tile's list in runs
@@ -36,7 +36,7 @@ from oracle import gl_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-CAP_WAVE, CAP_BLOCK, FIX_MAX = 1024, 24576, 16  # tile_sort.hip kTdsCapWave / kTdsCapBlock, kFixRunMax
+CAP_WAVE, CAP_BLOCK, FIX_MAX = 1024, 24576, 16  # long_runs.h kTdsCapWave / kTdsCapBlock, kFixRunMax
 
 
 def run_class(lens):
@@ -235,3 +235,18 @@ def test_group_matches_frames_alone(gpu, monkeypatch, scene_kind):
         alone = _frames(monkeypatch, g, cams[v], st, "coarse8")
         for key in ("tile_list", "ranges", "records", "image"):
             np.testing.assert_array_equal(alone[key], group[v][key], err_msg=f"view {v} {key}")
+
+
+def test_unorm8_long_runs(gpu, monkeypatch):
+    """The RGBA8 framebuffer (GSR_BLEND_UNORM8: whole lists back to front, no
+    chunks) sorts the long runs in a launch of its own: tile lists and image
+    bit-identical to the exact sort's."""
+    g = graded_plane(n=120_000, seed=6)
+    cam = Camera(270, 480)
+    st = _settings(blend=1)
+    got = _frames(monkeypatch, g, cam, st, "coarse8")
+    exact = _frames(monkeypatch, g, cam, _settings(blend=1), "exact")
+    for key in ("tile_list", "ranges", "image"):
+        np.testing.assert_array_equal(got[key], exact[key], err_msg=key)
+    lens = got["ranges"][:, 1].astype(np.int64) - got["ranges"][:, 0]
+    assert lens.max() > CAP_BLOCK, lens.max()
