@@ -173,6 +173,9 @@ struct gsr_context {
     gsr::DevBuf<float4> tmax;                     // per chunk: published slice maxima of local T
     uint32_t chunk = 192;                         // instances per compositing chunk of a frame finished alone
                                                   // (gsr_render / gsr_render_finish): latency (r2_s17 sweep)
+    uint32_t chunk_target = 0;                    // a frame alone with many instances: chunks of at least
+                                                  // n_dup / chunk_target (rounded up to 64; at most
+                                                  // chunk_views), 0: `chunk` always (frame_chunk)
     uint32_t chunk_views = 3072;                  // ... of a group's frames (gsr_render_finish_views): with
                                                   // views in flight the other views fill the chip while a
                                                   // deep tile's long chunk runs, so few chunks (fewer partials,
@@ -455,6 +458,16 @@ void prof_group_accumulate(gsr_context* c, int slot) {
 // The frame's depth sort (pairs (depth key, slot), over the upper bound n; the
 // device count V bounds the work); carries the packed tile rects as payload
 // when the frame's tiles fit 8 bits per coordinate.
+// A frame alone's compositing chunk: `chunk`, or longer when the frame has
+// more instances than chunk_target chunks of it would hold (fewer partials and
+// merges, and chunks long enough to saturate slices themselves)
+uint32_t frame_chunk(const gsr_context* c, uint32_t n_dup) {
+    if (!c->chunk_target) return c->chunk;
+    const uint64_t want = ((uint64_t)n_dup + c->chunk_target - 1) / c->chunk_target;
+    const uint32_t r = (uint32_t)std::min<uint64_t>((want + 63u) & ~63ull, 1u << 20);
+    return std::max(c->chunk, std::min(r, std::max(c->chunk, c->chunk_views)));
+}
+
 int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const uint32_t* key_range, uint32_t* totals,
                hipStream_t s);
 
@@ -717,6 +730,10 @@ int gsr_context_create(gsr_context** out) {
     if (const char* e = std::getenv("GSR_CHUNK")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 16 && v <= (1 << 20)) (*out)->chunk = (uint32_t)v;
+    }
+    if (const char* e = std::getenv("GSR_CHUNK_TARGET")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 0 && v <= (1 << 24)) (*out)->chunk_target = (uint32_t)v;
     }
     if (const char* e = std::getenv("GSR_CHUNK_VIEWS")) {
         const long v = std::strtol(e, nullptr, 10);
@@ -1178,21 +1195,26 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         if ((rc = prof_record(c, slot, EV_COMPOSITE, s))) return rc;
     } else {
         // compositing chunks: at most one per tile plus one per `chunk` instances
-        const size_t max_chunks = (size_t)num_tiles + n_dup / c->chunk + 1;
+        // a frame of many instances (frame_chunk longer than `chunk`): longer chunks, first chunks
+        // dispatched first, and later chunks stopped by the earlier ones' transmittance bound
+        const uint32_t chunk = frame_chunk(c, n_dup);
+        const bool deep = chunk > c->chunk;
+        const size_t max_chunks = (size_t)num_tiles + n_dup / chunk + 1;
         if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
         if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
         if ((rc = c->chunk_desc.ensure(max_chunks, "chunk_desc"))) return rc;
         if ((rc = c->chunk_order.ensure(max_chunks, "chunk_order"))) return rc;
         if ((rc = c->partial.ensure(max_chunks * 256, "partial"))) return rc;
         if ((rc = c->tmax.ensure(max_chunks, "tmax"))) return rc;
-        if ((rc = launch_chunks(ranges, num_tiles, c->chunk, c->len_classes, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
-                                c->chunk_desc.p, c->chunk_order.p, c->tmax.p, s, c->first_major_alone,
+        float4* const tmax = deep ? c->tmax.p : nullptr;  // (after its ensure: it may have moved)
+        if ((rc = launch_chunks(ranges, num_tiles, chunk, c->len_classes, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
+                                c->chunk_desc.p, c->chunk_order.p, tmax, s, c->first_major_alone || deep,
                                 f.coarse ? &long_runs : nullptr)))
             return rc;
         if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
         if ((rc = launch_composite(c->chunk_desc.p, c->chunk_order.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,
                                    sat, tile_list, c->recs.p, u, frag_class_of(u.render_mod), f.t_min, f.bg,
-                                   f.out_layout, f.out, c->partial.p, c->tmax.p, c->tail_merge_alone, s)))
+                                   f.out_layout, f.out, c->partial.p, tmax, c->tail_merge_alone, s)))
             return rc;
         if ((rc = prof_record(c, slot, EV_COMPOSITE, s))) return rc;
         if ((rc = launch_merge(c->chunk_cnt.p, c->chunk_base.p, c->partial.p, sat, u, f.t_min, f.bg, f.out_layout,

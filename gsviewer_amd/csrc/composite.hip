@@ -628,46 +628,51 @@ constexpr int kRangeItems = 16;
 // The repair of one run of a coarse depth order, [i, i + L): instances of one
 // tile with equal coarse keys, in slot order (the stable coarse sort's).  The
 // exact order is (full key, slot); a run without a descent of the full key is
-// already in it.  Otherwise its (key, slot) pairs are copied to scratch and
-// each one is written at its rank.  One thread owns the run (the thread
-// holding its first instance), so its reads all precede its writes; other
+// already in it.  Otherwise each slot is written at its rank (the count of
+// smaller keys, and of equal keys earlier in the run: slots ascend along it).
+// One thread owns the run (the thread holding its first instance); other
 // threads read the run's slots only for their (tile, coarse key), which the
-// permutation leaves unchanged.  O(L^2), so only runs of at most kFixRunMax
-// instances: a longer one is listed for k_long_runs (long_runs.h), which
-// sorts it on chip in bounded time (round 4's unbounded form could spend
-// ~5e8 serial steps on one dense tile).
+// permutation leaves unchanged.  The kFixRunMax + 1 instances from the start
+// are loaded at once and ranked in registers (round 4 scanned the run load by
+// load, ~1 us per instance, and ranked it in global memory: C3's k_tile_ranges
+// took 166 us, profiles/r5_s16).  A longer run is listed for the long-run
+// sorts (long_runs.h), which sort it on chip in bounded time (round 4's
+// unbounded form could spend ~5e8 serial steps on one dense tile).
 __device__ __noinline__ void fix_run(const uint32_t* __restrict__ keys, uint32_t n, uint32_t* vals,
-                                     const uint32_t* __restrict__ inst_keys, uint32_t* __restrict__ scratch_keys,
-                                     uint32_t* __restrict__ scratch_vals, uint32_t* __restrict__ long_starts,
+                                     const uint32_t* __restrict__ inst_keys, uint32_t* __restrict__ long_starts,
                                      uint32_t* __restrict__ long_count, uint32_t i, uint32_t tile, uint32_t cv,
                                      uint32_t kmin, uint32_t s0) {
-    uint32_t fprev = inst_keys[i];
+    constexpr int M = (int)kFixRunMax + 1;
+    uint32_t kk[M], ff[M], vv[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+        const bool ok = i + (uint32_t)j < n;
+        kk[j] = ok ? keys[i + j] : ~tile;
+        ff[j] = ok ? inst_keys[i + j] : 0u;
+        vv[j] = ok ? vals[i + j] : 0u;
+    }
     uint32_t L = 1;
-    bool descent = false;
-    for (uint32_t q = i + 1; q < n; ++q) {
-        if (keys[q] != tile) break;
-        const uint32_t f = inst_keys[q];
-        if (((f - kmin) >> s0) != cv) break;
-        descent |= f < fprev;
-        fprev = f;
-        if (++L > kFixRunMax) {  // a long run: k_long_runs finds its end and sorts it
-            long_starts[atomicAdd(long_count, 1u)] = i;
-            return;
+    bool open = true, descent = false;
+#pragma unroll
+    for (int j = 1; j < M; ++j) {
+        open = open && kk[j] == tile && ((ff[j] - kmin) >> s0) == cv;
+        if (open) {
+            ++L;
+            descent |= ff[j] < ff[j - 1];
         }
+    }
+    if (L > kFixRunMax) {  // a long run: the long-run sorts find its end and sort it
+        long_starts[atomicAdd(long_count, 1u)] = i;
+        return;
     }
     if (!descent) return;
-    for (uint32_t r = 0; r < L; ++r) {
-        scratch_vals[i + r] = vals[i + r];
-        scratch_keys[i + r] = inst_keys[i + r];
-    }
-    for (uint32_t r = 0; r < L; ++r) {
-        const uint32_t kr = scratch_keys[i + r], vr = scratch_vals[i + r];
+#pragma unroll
+    for (int r = 0; r < M - 1; ++r) {
         uint32_t rank = 0;
-        for (uint32_t q = 0; q < L; ++q) {
-            const uint32_t kq = scratch_keys[i + q], vq = scratch_vals[i + q];
-            rank += (kq < kr || (kq == kr && vq < vr)) ? 1u : 0u;
-        }
-        vals[i + rank] = vr;
+#pragma unroll
+        for (int q = 0; q < M - 1; ++q)
+            rank += ((uint32_t)q < L && (ff[q] < ff[r] || (ff[q] == ff[r] && q < r))) ? 1u : 0u;
+        if ((uint32_t)r < L) vals[i + rank] = vv[r];
     }
 }
 
@@ -763,8 +768,8 @@ __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ key
 #pragma unroll
         for (int j = 0; j < kFixWin; ++j)
             if (j == st) kst = kw[j], fst = fw[j];
-        fix_run(keys, n, fx.vals, fx.inst_keys, fx.scratch_keys, fx.scratch_vals, fx.long_starts, fx.long_count,
-                base + (uint32_t)st, kst, (fst - kmin) >> s0, kmin, s0);
+        fix_run(keys, n, fx.vals, fx.inst_keys, fx.long_starts, fx.long_count, base + (uint32_t)st, kst,
+                (fst - kmin) >> s0, kmin, s0);
     }
     const uint32_t pairs = same & own;  // adjacent pairs inside one owned run
     uint32_t descent = 0;
@@ -1198,6 +1203,15 @@ __device__ __forceinline__ const uint32_t* chunk_tmax(const float4* tmax, uint32
 
 // Issue (no wait) the loads of the published slice maxima of chunks
 // 0..min(kk,64)-1, one chunk per lane; other lanes hold 1.0.
+// The cross-chunk bound for a group's frames: an experiment build only
+// (-DGSR_COMP_BOUND, profiles/r2_s53: slower in flight).  A frame alone takes
+// it per frame (launch_composite's tmax, api.hip frame_chunk).
+#ifdef GSR_COMP_BOUND
+constexpr bool kBoundViews = true;
+#else
+constexpr bool kBoundViews = false;
+#endif
+
 __device__ __forceinline__ void load_prior(const float4* tmax, uint32_t tile, uint32_t base, uint32_t kk,
                                            uint32_t prior[4]) {
     const uint32_t j = __lane_id();
@@ -1252,7 +1266,7 @@ __device__ unsigned long long g_comp_stats[5];
 // (atomicMax of the complement; zero = none): k_merge folds each slice only up
 // to that chunk.  All words are accessed relaxed at agent scope; a stale read
 // only costs work, never accuracy.
-template <int FRAG>
+template <int FRAG, bool kBound>
 __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t slot, float4* __restrict__ my,
                                                 const uint32_t* __restrict__ list,
                                                 const SplatRec* __restrict__ recs, const CompositeArgs& a,
@@ -1295,10 +1309,10 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
     const bool poll = track && kk > 0;
     // live slices (bit k): not yet stopped
     uint32_t live = 0xfu;
-#ifdef GSR_COMP_BOUND
-    uint32_t prior[4];  // lane i < min(kk, 64): chunk i's published slice maxima (async)
-    if (poll) load_prior(tmax, (uint32_t)tile, base, kk, prior);
-#endif
+    [[maybe_unused]] uint32_t prior[4];  // (kBound) lane i < min(kk, 64): chunk i's published slice maxima (async)
+    if constexpr (kBound) {
+        if (poll) load_prior(tmax, (uint32_t)tile, base, kk, prior);
+    }
 
     // Two-stage prefetch: the records of batch b+1 and the list indices of
     // batch b+2 are in flight while batch b is composited, so neither the
@@ -1314,8 +1328,7 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         const uint32_t i2 = begin + kBatch + lane;
         if (i2 < end) idx_next = list[i2];
     }
-#ifdef GSR_COMP_BOUND
-    if (poll) {  // a chunk that starts behind saturated ones computes nothing
+    if (kBound && poll) {  // a chunk that starts behind saturated ones computes nothing
         float B[4];
         prior_bound(tmax, (uint32_t)tile, base, kk, prior, B);
         uint32_t dead = 0;
@@ -1330,15 +1343,13 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         }
         live &= ~dead;
     }
-#else
-    if (poll) {  // slices an earlier chunk already saturated
+    if (!kBound && poll) {  // slices an earlier chunk already saturated
         uint32_t dead = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (0xffffffffu - ld_relaxed(my_sat + k) < kk) dead |= 1u << k;
         live &= ~__builtin_amdgcn_readfirstlane(dead);
     }
-#endif
     if (a.debug_handoff && nchunks > 1 && kk == 0) {
         // Test knob (tests/test_gpu_handoff.py), chunk 0 of a multi-chunk tile,
         // before any other chunk can have finished: bit 1 polls the tile's
@@ -1385,17 +1396,14 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                 sb[k] = ((live >> k) & 1u) ? (uint64_t)__ballot(((covy >> (4 * k)) & 0xfu) != 0u) : 0ull;
         }
         __builtin_amdgcn_wave_barrier();
-#ifdef GSR_COMP_BOUND
-        // earlier chunks' published maxima, consumed after this batch
-        if (poll) load_prior(tmax, (uint32_t)tile, base, kk, prior);
-#else
-        // saturation words of the other chunks, consumed after this batch
-        uint32_t satw[4];
-        if (poll) {
+        // earlier chunks' published maxima (kBound), or the saturation words of
+        // the other chunks, consumed after this batch
+        [[maybe_unused]] uint32_t satw[4];
+        if (kBound && poll) load_prior(tmax, (uint32_t)tile, base, kk, prior);
+        if (!kBound && poll) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) satw[k] = ld_relaxed(my_sat + k);
         }
-#endif
         {  // prefetch: records of batch b+1, list indices of batch b+2
             const uint32_t i = b + kBatch + lane;
             if (i < end) {
@@ -1550,8 +1558,7 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         }
         if (t_min > 0.f) {
             uint32_t still = 0;
-#ifdef GSR_COMP_BOUND
-            if (track) {
+            if (kBound && track) {
                 // publish this chunk's slice maxima, then test bound * max against t_min
                 float m[4], B[4] = {1.f, 1.f, 1.f, 1.f};
 #pragma unroll
@@ -1565,9 +1572,7 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     if (B[k] * m[k] >= t_min) still |= 1u << k;
-            } else
-#endif
-            {
+            } else {
                 // stop a slice when every pixel's chunk-local T is below t_min
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
@@ -1580,15 +1585,13 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                     if (newly & (1u << k)) atomicMax(my_sat + k, 0xffffffffu - kk);
             }
             live &= still;
-#ifndef GSR_COMP_BOUND
-            if (poll && live) {
+            if (!kBound && poll && live) {
                 uint32_t dead = 0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     if (0xffffffffu - satw[k] < kk) dead |= 1u << k;
                 live &= ~__builtin_amdgcn_readfirstlane(dead);
             }
-#endif
         }
     }
 
@@ -1762,7 +1765,7 @@ __device__ __forceinline__ uint32_t comp_block() {
     return w * W + (r & 7u) * R + (r >> 3);
 }
 
-template <int FRAG>
+template <int FRAG, bool kBound>
 __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const uint4* __restrict__ desc,
                                                         const uint32_t* __restrict__ order,
                                                         const uint32_t* __restrict__ n_chunks_dev,
@@ -1780,7 +1783,7 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const uint4 d = desc[slot];
-    composite_chunk<FRAG>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax, chunk_base);
+    composite_chunk<FRAG, kBound>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax, chunk_base);
 #ifdef GSR_COMP_TRACE
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if (__lane_id() == 0 && slot < kTraceMax) {
@@ -1864,7 +1867,7 @@ __device__ __forceinline__ void composite_views_wave(const CompViews& vs, const 
     if (pos >= (uint32_t)a.num_tiles + v.n_chunks_dev[0]) return;
     const uint32_t slot = v.order[pos];
     const uint4 d = v.desc[slot];
-    composite_chunk<FRAG>(d, slot, lds, v.list, v.recs, a, v.out, v.partial, v.sat, v.tmax, v.chunk_base);
+    composite_chunk<FRAG, kBoundViews>(d, slot, lds, v.list, v.recs, a, v.out, v.partial, v.sat, v.tmax, v.chunk_base);
 }
 
 template <int FRAG>
@@ -2281,9 +2284,6 @@ const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uin
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
                   hipStream_t s, bool first_major, const LongRuns* long_runs) {
-#ifndef GSR_COMP_BOUND
-    tmax = nullptr;  // the published maxima are only read by the bound variant
-#endif
     if (classes < 2 || classes > (uint32_t)kMaxLenClasses) return set_error(GSR_ERR_INVALID, "chunk length classes");
     const unsigned g = (unsigned)((num_tiles + kThreads - 1) / kThreads);
     // the per-block totals live in chunk_cnt past its num_tiles entries
@@ -2315,6 +2315,19 @@ int launch_long_runs(const uint32_t* tile_keys, uint32_t n_dup, const uint2* ran
     return GSR_OK;
 }
 
+template <int FRAG>
+static void composite_launch(unsigned grid, bool bound, hipStream_t s, const uint4* desc, const uint32_t* order,
+                             const uint32_t* n_chunks_dev, const uint32_t* tile_vals, const SplatRec* recs,
+                             const CompositeArgs& a, float* out, float4* partial, uint32_t* sat, float4* tmax,
+                             const uint32_t* chunk_base) {
+    if (bound)
+        k_composite<FRAG, true><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
+                                                              sat, tmax, chunk_base);
+    else
+        k_composite<FRAG, false><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
+                                                               sat, tmax, chunk_base);
+}
+
 int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n_chunks_dev, uint32_t max_chunks,
                      const uint32_t* chunk_cnt,
                      const uint32_t* chunk_base, uint32_t* sat, const uint32_t* tile_vals, const SplatRec* recs,
@@ -2323,22 +2336,23 @@ int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n
     const CompositeArgs a = make_args(u, t_min, bg, out_layout, tail_merge);
     if (max_chunks == 0) return GSR_OK;
     const unsigned grid = (unsigned)((max_chunks + kCompWaves - 1) / kCompWaves);
+    const bool bound = tmax != nullptr;  // the cross-chunk transmittance bound (launch_chunks initialised tmax)
     switch (frag_class) {
         case kFragGauss:
-            k_composite<kFragGauss><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial, sat,
-                                                              tmax, chunk_base);
+            composite_launch<kFragGauss>(grid, bound, s, desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
+                                         sat, tmax, chunk_base);
             break;
         case kFragBillboard:
-            k_composite<kFragBillboard><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
-                                                                  sat, tmax, chunk_base);
+            composite_launch<kFragBillboard>(grid, bound, s, desc, order, n_chunks_dev, tile_vals, recs, a, out,
+                                             partial, sat, tmax, chunk_base);
             break;
         case kFragFlatBall:
-            k_composite<kFragFlatBall><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
-                                                                 sat, tmax, chunk_base);
+            composite_launch<kFragFlatBall>(grid, bound, s, desc, order, n_chunks_dev, tile_vals, recs, a, out,
+                                            partial, sat, tmax, chunk_base);
             break;
         default:
-            k_composite<kFragGaussBall><<<grid, kCompThreads, 0, s>>>(desc, order, n_chunks_dev, tile_vals, recs, a, out, partial,
-                                                                  sat, tmax, chunk_base);
+            composite_launch<kFragGaussBall>(grid, bound, s, desc, order, n_chunks_dev, tile_vals, recs, a, out,
+                                             partial, sat, tmax, chunk_base);
             break;
     }
     GSR_LAUNCH_CHECK("composite");
@@ -2475,11 +2489,7 @@ int launch_chunks_views(FinishView* views, int k, int num_tiles, uint32_t chunk,
     ChunkViews cv{};
     for (int i = 0; i < k; ++i) {
         const FinishView& f = views[i];
-#ifdef GSR_COMP_BOUND
-        float4* tmax = f.tmax;
-#else
-        float4* tmax = nullptr;  // the published maxima are only read by the bound variant
-#endif
+        float4* tmax = kBoundViews ? f.tmax : nullptr;  // the published maxima are only read by the bound form
         cv.v[i] = ChunkView{f.ranges, f.chunk_cnt, f.chunk_base, f.n_extra_dev, f.desc, f.order, tmax};
     }
     const dim3 grid((unsigned)((num_tiles + kThreads - 1) / kThreads), (unsigned)k);

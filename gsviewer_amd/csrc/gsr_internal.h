@@ -442,7 +442,7 @@ struct RunFix {
     uint32_t* vals;             // the tile list (slots), repaired in place
     const uint32_t* key_range;  // the frame's {~kmin, kmax}
     uint32_t coarse;
-    uint32_t* scratch_keys;     // n_dup words each, free at this point (the tile sort's alternates)
+    uint32_t* scratch_keys;     // n_dup words each, free at this point (the tile sort's alternates): the long runs' global path
     uint32_t* scratch_vals;
     uint32_t* inst_keys = nullptr;     // each list position's depth key (binning + tile sort payload)
     uint32_t* long_starts = nullptr;   // long_runs_elems(n_dup) words: long_run_cap starts, then their lengths

@@ -114,7 +114,31 @@ __global__ __launch_bounds__(kThreads) void k_rs_upsweep(const uint32_t* __restr
 }
 
 // One wave per digit d: exclusive scan of row d (ntiles counts) in place; row total out.
-constexpr uint32_t kOffRegs = 16;  // counts per lane held in registers
+// Lane l owns the row's consecutive counts [l per, (l + 1) per).  Every load
+// of a round is issued before any is used: rows of up to 64 * kOffRegs counts
+// (2048-key tiles: 2M keys) in one round trip; longer rows in rounds of
+// kOffRegs (round 4 walked them load by load: 20-44 us per pass at C3's 6M
+// keys and 5860 binning blocks, profiles/r5_s16).
+constexpr uint32_t kOffRegs = 16;
+template <int kRegs>
+__device__ __forceinline__ void rs_offsets_regs(uint32_t* __restrict__ row, uint32_t b0, uint32_t b1,
+                                                uint32_t* __restrict__ total) {
+    uint32_t c[kRegs];
+#pragma unroll
+    for (int k = 0; k < kRegs; ++k) c[k] = b0 + (uint32_t)k < b1 ? row[b0 + k] : 0u;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kRegs; ++k) s += c[k];
+    const uint32_t inc = wave_inclusive_scan(s);
+    uint32_t run = inc - s;
+#pragma unroll
+    for (int k = 0; k < kRegs; ++k) {
+        if (b0 + (uint32_t)k < b1) row[b0 + k] = run;
+        run += c[k];
+    }
+    if (__lane_id() == 63) *total = inc;
+}
+
 __device__ __forceinline__ void rs_offsets(uint32_t* __restrict__ hist, uint32_t ntiles, const PassArgs& pa,
                                            uint32_t* __restrict__ totals, uint32_t d) {
     const Digit dg = digit_params(pa);
@@ -123,31 +147,27 @@ __device__ __forceinline__ void rs_offsets(uint32_t* __restrict__ hist, uint32_t
     const uint32_t per = (ntiles + 63) / 64;
     const uint32_t b0 = __lane_id() * per;
     const uint32_t b1 = min(ntiles, b0 + per);
-    if (per <= kOffRegs) {  // rows of <= 64 * kOffRegs tiles (1M keys: 489): one load round trip, counts in registers
+    if (per <= kOffRegs) return rs_offsets_regs<kOffRegs>(row, b0, b1, totals + d);
+    if (per <= 4 * kOffRegs) return rs_offsets_regs<4 * kOffRegs>(row, b0, b1, totals + d);
+    uint32_t s = 0;
+    for (uint32_t i0 = b0; i0 < b1; i0 += kOffRegs) {
         uint32_t c[kOffRegs];
 #pragma unroll
-        for (uint32_t k = 0; k < kOffRegs; ++k) c[k] = b0 + k < b1 ? row[b0 + k] : 0u;
-        uint32_t s = 0;
+        for (uint32_t k = 0; k < kOffRegs; ++k) c[k] = i0 + k < b1 ? row[i0 + k] : 0u;
 #pragma unroll
         for (uint32_t k = 0; k < kOffRegs; ++k) s += c[k];
-        const uint32_t inc = wave_inclusive_scan(s);
-        uint32_t run = inc - s;
-#pragma unroll
-        for (uint32_t k = 0; k < kOffRegs; ++k) {
-            if (b0 + k < b1) row[b0 + k] = run;
-            run += c[k];
-        }
-        if (__lane_id() == 63) totals[d] = inc;
-        return;
     }
-    uint32_t s = 0;
-    for (uint32_t i = b0; i < b1; ++i) s += row[i];
     const uint32_t inc = wave_inclusive_scan(s);
     uint32_t run = inc - s;
-    for (uint32_t i = b0; i < b1; ++i) {
-        const uint32_t t = row[i];
-        row[i] = run;
-        run += t;
+    for (uint32_t i0 = b0; i0 < b1; i0 += kOffRegs) {
+        uint32_t c[kOffRegs];
+#pragma unroll
+        for (uint32_t k = 0; k < kOffRegs; ++k) c[k] = i0 + k < b1 ? row[i0 + k] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < kOffRegs; ++k) {
+            if (i0 + k < b1) row[i0 + k] = run;
+            run += c[k];
+        }
     }
     if (__lane_id() == 63) totals[d] = inc;
 }
