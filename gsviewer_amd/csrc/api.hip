@@ -173,9 +173,11 @@ struct gsr_context {
     gsr::DevBuf<float4> tmax;                     // per chunk: published slice maxima of local T
     uint32_t chunk = 192;                         // instances per compositing chunk of a frame finished alone
                                                   // (gsr_render / gsr_render_finish): latency (r2_s17 sweep)
-    uint32_t chunk_target = 0;                    // a frame alone with many instances: chunks of at least
+    uint32_t chunk_target = 16384;                // a frame alone with many instances: chunks of at least
                                                   // n_dup / chunk_target (rounded up to 64; at most
-                                                  // chunk_views), 0: `chunk` always (frame_chunk)
+                                                  // chunk_views), 0: `chunk` always (frame_chunk).  16384:
+                                                  // C3 704-instance chunks (latency 1.56 -> 1.40 ms), c2h 320
+                                                  // (0.80 -> 0.66), C2 / C5 unchanged (profiles/r5_s17)
     uint32_t chunk_views = 3072;                  // ... of a group's frames (gsr_render_finish_views): with
                                                   // views in flight the other views fill the chip while a
                                                   // deep tile's long chunk runs, so few chunks (fewer partials,

@@ -1224,20 +1224,15 @@ __device__ __forceinline__ void load_prior(const float4* tmax, uint32_t tile, ui
     }
 }
 
-// B[k] = product over chunks j < kk of their published maxima of slice k
-// (chunks beyond the first 64 are read here, synchronously: very deep tiles).
+// B[k] = product over chunks j < min(kk, 64) of their published maxima of
+// slice k: an upper bound of the transmittance entering chunk kk (the factors
+// of chunks 64 .. kk - 1 are at most 1; reading them synchronously every batch
+// cost the deepest tiles more than the tighter bound saved, profiles/r5_s19).
 __device__ __forceinline__ void prior_bound(const float4* tmax, uint32_t tile, uint32_t base, uint32_t kk,
                                             const uint32_t prior[4], float B[4]) {
-    float v[4];
+    (void)tmax, (void)tile, (void)base, (void)kk;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = __uint_as_float(prior[k]);
-    for (uint32_t j = 64 + __lane_id(); j < kk; j += 64) {
-        const uint32_t* w = chunk_tmax(tmax, tile, base, j);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] *= __uint_as_float(ld_relaxed(w + k));
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) B[k] = uniform_f(wave_prod(v[k]));
+    for (int k = 0; k < 4; ++k) B[k] = uniform_f(wave_prod(__uint_as_float(prior[k])));
 }
 
 #ifdef GSR_COMP_STATS

@@ -44,6 +44,10 @@ constexpr int kRWide = GSR_WIDE_R;
 #define GSR_DEPTH_R 8
 #endif
 constexpr int kRDepth = GSR_DEPTH_R;
+// ... and for depth sorts of more than kBigDepthN keys: 4096-key tiles (C3's 6M keys: 2 passes 180 -> 155 us;
+// C2's 1M: 53 -> 58 us, profiles/r5_s22)
+constexpr int kRDepthBig = 16;
+constexpr size_t kBigDepthN = (size_t)1 << 21;
 // items per thread for host-known <= 8-bit digits (the tile sort); build knob for A/B.
 // 8 since the binning took over the tile sort's first pass: its one remaining
 // pass (1.76M instances at C2) ran 1.8 us faster in 2048-item tiles than in
@@ -114,62 +118,57 @@ __global__ __launch_bounds__(kThreads) void k_rs_upsweep(const uint32_t* __restr
 }
 
 // One wave per digit d: exclusive scan of row d (ntiles counts) in place; row total out.
-// Lane l owns the row's consecutive counts [l per, (l + 1) per).  Every load
-// of a round is issued before any is used: rows of up to 64 * kOffRegs counts
-// (2048-key tiles: 2M keys) in one round trip; longer rows in rounds of
-// kOffRegs (round 4 walked them load by load: 20-44 us per pass at C3's 6M
-// keys and 5860 binning blocks, profiles/r5_s16).
+// Rows of up to 64 * kOffRegs counts (2048-key tiles: 2M keys): lane l owns
+// the consecutive counts [l per, (l + 1) per), all loaded in one round trip.
+// Longer rows (C3: 2930 depth-sort tiles, 5860 binning blocks, 5190 tile-sort
+// tiles) lane-interleaved, count i = 64 r + lane in round r, kOffRegs rounds
+// of coalesced loads in flight, a wave scan per round: round 4's lane-owned
+// segments made every load instruction touch 64 lines (20-44 us per pass at
+// C3, profiles/r5_s16; ~5 us now).
 constexpr uint32_t kOffRegs = 16;
-template <int kRegs>
-__device__ __forceinline__ void rs_offsets_regs(uint32_t* __restrict__ row, uint32_t b0, uint32_t b1,
-                                                uint32_t* __restrict__ total) {
-    uint32_t c[kRegs];
-#pragma unroll
-    for (int k = 0; k < kRegs; ++k) c[k] = b0 + (uint32_t)k < b1 ? row[b0 + k] : 0u;
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < kRegs; ++k) s += c[k];
-    const uint32_t inc = wave_inclusive_scan(s);
-    uint32_t run = inc - s;
-#pragma unroll
-    for (int k = 0; k < kRegs; ++k) {
-        if (b0 + (uint32_t)k < b1) row[b0 + k] = run;
-        run += c[k];
-    }
-    if (__lane_id() == 63) *total = inc;
-}
-
 __device__ __forceinline__ void rs_offsets(uint32_t* __restrict__ hist, uint32_t ntiles, const PassArgs& pa,
                                            uint32_t* __restrict__ totals, uint32_t d) {
     const Digit dg = digit_params(pa);
     if (d > dg.mask) return;
     uint32_t* row = hist + (size_t)d * ntiles;
     const uint32_t per = (ntiles + 63) / 64;
-    const uint32_t b0 = __lane_id() * per;
-    const uint32_t b1 = min(ntiles, b0 + per);
-    if (per <= kOffRegs) return rs_offsets_regs<kOffRegs>(row, b0, b1, totals + d);
-    if (per <= 4 * kOffRegs) return rs_offsets_regs<4 * kOffRegs>(row, b0, b1, totals + d);
-    uint32_t s = 0;
-    for (uint32_t i0 = b0; i0 < b1; i0 += kOffRegs) {
+    const uint32_t lane = __lane_id();
+    if (per <= kOffRegs) {
+        const uint32_t b0 = lane * per;
+        const uint32_t b1 = min(ntiles, b0 + per);
         uint32_t c[kOffRegs];
 #pragma unroll
-        for (uint32_t k = 0; k < kOffRegs; ++k) c[k] = i0 + k < b1 ? row[i0 + k] : 0u;
+        for (uint32_t k = 0; k < kOffRegs; ++k) c[k] = b0 + k < b1 ? row[b0 + k] : 0u;
+        uint32_t s = 0;
 #pragma unroll
         for (uint32_t k = 0; k < kOffRegs; ++k) s += c[k];
-    }
-    const uint32_t inc = wave_inclusive_scan(s);
-    uint32_t run = inc - s;
-    for (uint32_t i0 = b0; i0 < b1; i0 += kOffRegs) {
-        uint32_t c[kOffRegs];
-#pragma unroll
-        for (uint32_t k = 0; k < kOffRegs; ++k) c[k] = i0 + k < b1 ? row[i0 + k] : 0u;
+        const uint32_t inc = wave_inclusive_scan(s);
+        uint32_t run = inc - s;
 #pragma unroll
         for (uint32_t k = 0; k < kOffRegs; ++k) {
-            if (i0 + k < b1) row[i0 + k] = run;
+            if (b0 + k < b1) row[b0 + k] = run;
             run += c[k];
         }
+        if (lane == 63) totals[d] = inc;
+        return;
     }
-    if (__lane_id() == 63) totals[d] = inc;
+    uint32_t carry = 0;
+    for (uint32_t r0 = 0; r0 < ntiles; r0 += 64 * kOffRegs) {
+        uint32_t c[kOffRegs];
+#pragma unroll
+        for (uint32_t k = 0; k < kOffRegs; ++k) {
+            const uint32_t i = r0 + k * 64 + lane;
+            c[k] = i < ntiles ? row[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kOffRegs; ++k) {
+            const uint32_t i = r0 + k * 64 + lane;
+            const uint32_t inc = wave_inclusive_scan(c[k]);
+            if (i < ntiles) row[i] = carry + inc - c[k];
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        }
+    }
+    if (lane == 0) totals[d] = carry;
 }
 
 // 4 digits per 256-thread block (one wave each): a quarter of the workgroups
@@ -529,10 +528,13 @@ int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size
     for (int v = 1; v < k; ++v)
         if ((views[v].rect_in != nullptr) != (views[0].rect_in != nullptr))
             return set_error(GSR_ERR_INVALID, "radix sort: payload on some views only");
-    if ((bits + passes - 1) / passes <= 8)
+    if ((bits + passes - 1) / passes <= 8) {
+        if (views[0].key_range && n > kBigDepthN)
+            return sort_passes_views<kRDepthBig, 8>(views, k, identity_vals, n, bits, passes, s, first_pass);
         return views[0].key_range
                    ? sort_passes_views<kRDepth, 8>(views, k, identity_vals, n, bits, passes, s, first_pass)
                    : sort_passes_views<kRTile, 8>(views, k, identity_vals, n, bits, passes, s, first_pass);
+    }
     return sort_passes_views<kRWide, kMaxBits>(views, k, identity_vals, n, bits, passes, s, first_pass);
 }
 
@@ -551,6 +553,10 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
     // widths (the depth sort) and, since round 3's fused binning, for host-known
     // <= 8-bit digits (the tile sort's remaining pass)
     if ((bits + passes - 1) / passes <= 8) {
+        if (key_range && n > kBigDepthN)
+            return sort_passes<kRDepthBig, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits,
+                                              passes, key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass,
+                                              drop_first, coarse, keys_last);
         if (key_range)
             return sort_passes<kRDepth, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
                                      key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first, coarse,

@@ -1,7 +1,8 @@
 """Compositor work statistics on the bench workload (GSR_COMP_STATS build):
 slice evaluations, those spent on already-saturated slices, records visited.
     python -m gsviewer_amd.build -D GSR_COMP_STATS --out gsviewer_amd/libgsr_stats.so
-    GSR_LIB_PATH=gsviewer_amd/libgsr_stats.so python tools/comp_stats.py [--views]"""
+    GSR_LIB_PATH=gsviewer_amd/libgsr_stats.so python tools/comp_stats.py [--views] [--c3]
+(--c3: the 6M-Gaussian frame of BASELINE config C3, seed 2)"""
 import ctypes
 import os
 import sys
@@ -18,7 +19,7 @@ from gsviewer_amd.rasterizer import HipContext, HipScene, RenderSettings, camera
 
 def main():
     lib = _lib.load()
-    g = garden_standin(1_000_000, seed=1)
+    g = garden_standin(6_000_000, seed=2) if "--c3" in sys.argv else garden_standin(1_000_000, seed=1)
     scene = HipScene.from_gaussian_data(g)
     ctx = HipContext()
     out = torch.empty((3, 1080, 1920), dtype=torch.float32, device="cuda")

@@ -23,6 +23,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--seed", type=int, default=1, help="garden stand-in seed (C3: --n 6000000 --seed 2)")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--frames", type=int, default=5)
@@ -43,7 +44,7 @@ def main():
     fn.restype = ctypes.c_int64
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
 
-    g = garden_standin(a.n, seed=1, sh_degree=3)
+    g = garden_standin(a.n, seed=a.seed, sh_degree=3)
     scene = HipScene(*[torch.from_numpy(np.ascontiguousarray(getattr(g, f))).cuda()
                        for f in ("xyz", "rot", "scale", "opacity", "sh")])
     ctx = HipContext()
