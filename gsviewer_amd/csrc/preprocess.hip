@@ -955,7 +955,8 @@ static unsigned preprocess_grid(int64_t n, bool alone = false) {
             c = 256;
         return c;
     }();
-    const unsigned per_cu = alone ? 3u : 4u;  // (measured: profiles/r4_s8, r4_s27)
+    // (measured: profiles/r4_s8, r4_s27; 6 or 12 per CU for C3's 6M alone: no change, r5_s28)
+    const unsigned per_cu = alone ? 3u : 4u;
     return std::max(1u, std::min((unsigned)((n + kThreads - 1) / kThreads), per_cu * (unsigned)cus));
 }
 
