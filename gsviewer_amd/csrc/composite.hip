@@ -629,7 +629,8 @@ constexpr int kRangeItems = 16;
 // tile with equal coarse keys, in slot order (the stable coarse sort's).  The
 // exact order is (full key, slot); a run without a descent of the full key is
 // already in it.  Otherwise each slot is written at its rank (the count of
-// smaller keys, and of equal keys earlier in the run: slots ascend along it).
+// smaller keys, and of equal keys earlier in the run: slots ascend along it;
+// an odd-even transposition here took 151 VGPRs: 64.7 -> 75.2 us at C3).
 // One thread owns the run (the thread holding its first instance); other
 // threads read the run's slots only for their (tile, coarse key), which the
 // permutation leaves unchanged.  The kFixRunMax + 1 instances from the start
@@ -792,17 +793,23 @@ __device__ __forceinline__ void fix_coarse_runs(const uint32_t* __restrict__ key
     uint32_t v0[kFixWin];
 #pragma unroll
     for (int j = 0; j < kFixWin; ++j) v0[j] = vw[j];
-    for (uint32_t r = 0; r < rounds; ++r) {
+    // Rounds in pairs (an even pass, then an odd one: the pass parity is static, so each pass is half the
+    // window's pairs with no parity test; one extra pass is harmless).  Strict > only: the slots ascend in a
+    // run and adjacent swaps of strictly greater keys never cross equal ones, so the sort is stable and ties
+    // stay in slot order (round 4's tie-break compared the slots too: C3's repair 78 -> 52 us, profiles/r5_s35).
+    auto cx = [&](int j) {
+        const bool gt = ((pairs >> j) & 1u) && fw[j] > fw[j + 1];
+        const uint32_t fa = fw[j], va = vw[j];
+        fw[j] = gt ? fw[j + 1] : fa;
+        vw[j] = gt ? vw[j + 1] : va;
+        fw[j + 1] = gt ? fa : fw[j + 1];
+        vw[j + 1] = gt ? va : vw[j + 1];
+    };
+    for (uint32_t r = 0; r < rounds; r += 2) {
 #pragma unroll
-        for (int j = 0; j + 1 < kFixWin; ++j) {
-            if ((j & 1) != (int)(r & 1u) || !((pairs >> j) & 1u)) continue;
-            const bool gt = fw[j] > fw[j + 1] || (fw[j] == fw[j + 1] && vw[j] > vw[j + 1]);
-            const uint32_t fa = fw[j], va = vw[j];
-            fw[j] = gt ? fw[j + 1] : fa;
-            vw[j] = gt ? vw[j + 1] : va;
-            fw[j + 1] = gt ? fa : fw[j + 1];
-            vw[j + 1] = gt ? va : vw[j + 1];
-        }
+        for (int j = 0; j + 1 < kFixWin; j += 2) cx(j);
+#pragma unroll
+        for (int j = 1; j + 1 < kFixWin; j += 2) cx(j);
     }
 #pragma unroll
     for (int j = 0; j < kFixWin; ++j)
