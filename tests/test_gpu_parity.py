@@ -275,15 +275,16 @@ def test_multi_chunk_merge(gpu, monkeypatch, chunk):
     _check(g, Camera(96, 128), _settings(t_min=1e-4), tol=TOL_TMIN + 2e-5)
 
 
-@pytest.mark.parametrize("target", ["64", "256"])
-def test_deep_frame_chunks(gpu, monkeypatch, target):
+@pytest.mark.parametrize("target,mode", [("64", 0), ("256", 0), ("64", -4), ("64", -5), ("64", -6)])
+def test_deep_frame_chunks(gpu, monkeypatch, target, mode):
     """A frame alone with many instances per chunk target (GSR_CHUNK_TARGET:
     chunks of at least n_dup / target instances, here forced on a small
     scene) takes the deep-frame form: longer chunks, first chunks dispatched
     first, later chunks stopped by the earlier ones' transmittance bound
-    (api.hip frame_chunk).  Against the oracle at the stated tolerances."""
+    (api.hip frame_chunk).  Against the oracle at the stated tolerances, for
+    every fragment class (the bound form is compiled per class)."""
     monkeypatch.setenv("GSR_CHUNK", "64")
     monkeypatch.setenv("GSR_CHUNK_TARGET", target)
     g = random_scene(20_000, sh_degree=3, seed=71, scale_range=(0.02, 0.09))
-    _check(g, Camera(96, 128), _settings(t_min=0.0))
-    _check(g, Camera(96, 128), _settings(t_min=1e-4), tol=TOL_TMIN + 2e-5)
+    _check(g, Camera(96, 128), _settings(t_min=0.0, render_mod=mode))
+    _check(g, Camera(96, 128), _settings(t_min=1e-4, render_mod=mode), tol=TOL_TMIN + 2e-5)
