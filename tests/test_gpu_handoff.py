@@ -2,11 +2,12 @@
 
 A group's tile of several chunks is folded inside the compositing launch by
 the chunk whose counter add comes last: it reads the other chunks' partials
-(stored `sc1`) and the slices' saturation words (agent-scope atomics).  Two
-visibility bugs were found there in round 3, each only when dispatch timing
-happened to line up (f4e3b53: partials read with plain loads; 8352f97:
-saturation words read with an agent-scope load that hit a line this XCD's
-poll had cached).  Here the context's test knob GSR_DEBUG_HANDOFF forces the
+(stored `sc1`) and the slices' saturation words (agent-scope atomics).
+Round 3 changed two of those reads after a run-to-run mismatch that appeared
+only when dispatch timing happened to line up (f4e3b53: the partials, then
+plain loads, now `sc1` loads; 8352f97: the saturation words, then an
+agent-scope load, now an atomic read); neither change is confirmed as the
+cause (below).  Here the context's test knob GSR_DEBUG_HANDOFF forces the
 orderings every time (composite_chunk):
 
 * bit 0: chunk 0 of every multi-chunk tile adds last (it waits for the other
