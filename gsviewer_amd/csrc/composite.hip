@@ -1242,6 +1242,14 @@ __device__ __forceinline__ void prior_bound(const float4* tmax, uint32_t tile, u
     for (int k = 0; k < 4; ++k) B[k] = uniform_f(wave_prod(__uint_as_float(prior[k])));
 }
 
+// The image is written non-temporally: nothing in the frame reads it back, and
+// default-policy stores kept its lines in the L2s and the MALL over the
+// records and lists the other chunks (and, in flight, other views) still
+// gather (20 views in flight: 0.1323-0.1334 -> 0.1308-0.1321 ms per frame on
+// one box, profiles/r5_s51; within the spread on another, r5_s52).  The tile
+// lists read non-temporally too: no change (r5_s52).
+__device__ __forceinline__ void st_out(float* p, float v) { __builtin_nontemporal_store(v, p); }
+
 #ifdef GSR_COMP_STATS
 // Tooling build only (tools/comp_stats.py): {slice evaluations, evaluations
 // of an already saturated slice, records visited, records in the chunks}.
@@ -1718,13 +1726,13 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         const float b = bt[k].x + T * a.bg[2];
         const size_t pidx = (size_t)row * a.width + x;
         if (a.out_layout == 0) {
-            out[pidx] = r;
-            out[plane + pidx] = g;
-            out[2 * plane + pidx] = b;
+            st_out(out + pidx, r);
+            st_out(out + plane + pidx, g);
+            st_out(out + 2 * plane + pidx, b);
         } else {
-            out[3 * pidx] = r;
-            out[3 * pidx + 1] = g;
-            out[3 * pidx + 2] = b;
+            st_out(out + 3 * pidx, r);
+            st_out(out + 3 * pidx + 1, g);
+            st_out(out + 3 * pidx + 2, b);
         }
     }
 }
@@ -1958,13 +1966,13 @@ __device__ __forceinline__ void merge_tile(const uint32_t* __restrict__ chunk_cn
     const size_t plane = (size_t)a.width * a.height;
     const size_t pidx = (size_t)row * a.width + x;
     if (a.out_layout == 0) {
-        out[pidx] = r;
-        out[plane + pidx] = g;
-        out[2 * plane + pidx] = b;
+        st_out(out + pidx, r);
+        st_out(out + plane + pidx, g);
+        st_out(out + 2 * plane + pidx, b);
     } else {
-        out[3 * pidx] = r;
-        out[3 * pidx + 1] = g;
-        out[3 * pidx + 2] = b;
+        st_out(out + 3 * pidx, r);
+        st_out(out + 3 * pidx + 1, g);
+        st_out(out + 3 * pidx + 2, b);
     }
 }
 

@@ -249,8 +249,27 @@ __device__ __forceinline__ V3 normalize3(float vx, float vy, float vz) {
     return V3{vx / nn, vy / nn, vz / nn};
 }
 
+// kNT: a frame alone reads the scene's attributes non-temporally.  They are
+// read once per frame, and the default policy's L2/MALL allocations evicted
+// what the depth sort and binning then re-read (their keys, ids and
+// rectangles): C2 frame alone preprocess 66 -> 60 us, depth sort 52.4 -> 48.8,
+// binning -2 (latency 0.326 -> 0.314 ms, profiles/r5_s50).  A group's frames
+// keep the default (in flight no faster with it); the positions too (read by
+// every lane, non-temporal no faster alone: r5_s51).
+template <bool kNT = false>
+__device__ __forceinline__ float4 load_stream(const float4* __restrict__ a, int64_t i) {
+    if constexpr (kNT) {
+        typedef float nt4 __attribute__((ext_vector_type(4)));
+        const nt4 v = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(a) + i);
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+        return a[i];
+    }
+}
+
+template <bool kNT = false>
 __device__ __forceinline__ float4 load_plane(const float4* __restrict__ sh, int64_t n, int p, int64_t i) {
-    return sh[(int64_t)p * n + i];
+    return load_stream<kNT>(sh, (int64_t)p * n + i);
 }
 
 // SH floats needed at effective degree DEG (gau_vert.glsl:289-327 gates).
@@ -744,17 +763,17 @@ constexpr int kKeyShards = 64;
 constexpr int kKeyShards0 = 1;
 
 // The rest of Gaussian i's data (its position is already loaded).
-template <int DEG>
+template <int DEG, bool kNT>
 __device__ __forceinline__ void load_attrs(GaussLoad<DEG>& g, const float4 po, const float4* __restrict__ rot,
                                            const float4* __restrict__ scale, const float4* __restrict__ sh, int64_t n,
                                            int64_t i) {
     g.po = po;
-    g.q1 = rot[i];
-    g.sc4 = scale[i];
+    g.q1 = load_stream<kNT>(rot, i);
+    g.sc4 = load_stream<kNT>(scale, i);
 #pragma unroll
     for (int p = 0; p < 12; ++p) {
         if (p < sh_planes_for<DEG>()) {
-            const float4 t = load_plane(sh, n, p, i);
+            const float4 t = load_plane<kNT>(sh, n, p, i);
             g.f[4 * p + 0] = t.x;
             g.f[4 * p + 1] = t.y;
             g.f[4 * p + 2] = t.z;
@@ -888,7 +907,7 @@ __global__ __launch_bounds__(kThreads) GSR_PRE_OCC void k_preprocess_fc_views(co
         GaussLoad<DEG> g;
         Cov3 S3;
         if (vm) {
-            load_attrs<DEG>(g, p, rot, scale, sh, n, i);
+            load_attrs<DEG, kAlone>(g, p, rot, scale, sh, n, i);
             S3 = cov3d(g.q1, g.sc4, vs.v[0].u);  // (the group shares rot_modifier and the scale factor)
         }
         const uint32_t slot = (uint32_t)(n - 1 - i);
