@@ -974,8 +974,12 @@ static unsigned preprocess_grid(int64_t n, bool alone = false) {
             c = 256;
         return c;
     }();
-    // (measured: profiles/r4_s8, r4_s27; 6 or 12 per CU for C3's 6M alone: no change, r5_s28)
-    const unsigned per_cu = alone ? 3u : 4u;
+    // (measured: profiles/r4_s8, r4_s27; 6 or 12 per CU for C3's 6M alone: no change, r5_s28; with the
+    // non-temporal scene reads 2 / 4 / 6 alone: preprocess 62.4 / 62.4 / 66 us against 60.5 for 3, r5_s53)
+#ifndef GSR_PRE_PER_CU_ALONE  // build knob for A/B
+#define GSR_PRE_PER_CU_ALONE 3
+#endif
+    const unsigned per_cu = alone ? (unsigned)GSR_PRE_PER_CU_ALONE : 4u;
     return std::max(1u, std::min((unsigned)((n + kThreads - 1) / kThreads), per_cu * (unsigned)cus));
 }
 
