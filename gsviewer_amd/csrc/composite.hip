@@ -1020,6 +1020,10 @@ struct ChunkWriteLds {
     uint32_t cls[kMaxLenClasses][kThreads / 64];  // partials of class k per wave
     uint32_t pre[1 + kMaxLenClasses];             // sums over the earlier blocks
     uint32_t base[kMaxLenClasses];                // first dispatch position of each class
+    // the block's multi-chunk tiles for the flattened emission of chunks j >= 1:
+    // inclusive scan of (chunks - 1) per thread, and each thread's tile terms
+    uint32_t incl[kThreads];
+    uint32_t tile[kThreads][8];  // t, r.x, r.y, count, full, base, full_before, part_pos
 };
 
 __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk,
@@ -1107,19 +1111,29 @@ __device__ __forceinline__ void chunk_write(const uint2* __restrict__ ranges, in
         chunk_base[t] = base;
         emit((uint32_t)t, r.x, r.y, cnt, full, base, full_before, part_pos, 0u);
     }
-    // chunks j >= 1 of the multi-chunk tiles: the whole wave writes one tile's
-    // at a time (a deep tile has ~200 chunks: one lane storing them all would
-    // wait on its own outstanding stores)
-    uint64_t multi = __ballot(valid && cnt > 1);
-    while (multi) {
-        const int src = (int)__builtin_ctzll(multi);
-        multi &= multi - 1;
-        // src is wave-uniform: v_readlane into SGPRs, no LDS permute round trips
-        auto rl = [src](uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, src); };
-        const uint32_t tt = rl((uint32_t)t), rx = rl(r.x), ry = rl(r.y);
-        const uint32_t c = rl(cnt), f = rl(full), bs = rl(base);
-        const uint32_t fb = rl(full_before), pp = rl(part_pos);
-        for (uint32_t j = 1 + __lane_id(); j < c; j += 64) emit(tt, rx, ry, c, f, bs, fb, pp, j);
+    // chunks j >= 1 of the multi-chunk tiles, flattened over the block: extra
+    // chunk e of the block belongs to the tile whose inclusive count first
+    // exceeds e (a binary search in LDS), so every thread stores about the
+    // same number.  (Round 4's form, each wave walking its multi-chunk tiles
+    // one at a time, ran ~40 serial steps per wave with only 128 waves at C2.)
+    sh.incl[threadIdx.x] = excl + mine;
+    {
+        uint32_t* tp = sh.tile[threadIdx.x];
+        tp[0] = (uint32_t)t; tp[1] = r.x; tp[2] = r.y; tp[3] = cnt;
+        tp[4] = full; tp[5] = base; tp[6] = full_before; tp[7] = part_pos;
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < total; e += kThreads) {
+        uint32_t lo = 0, hi = kThreads - 1;  // the first i with incl[i] > e (incl[kThreads - 1] = total > e)
+#pragma unroll
+        for (int step = 0; step < 8; ++step) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sh.incl[mid] > e) hi = mid; else lo = mid + 1;
+        }
+        const uint32_t* tp = sh.tile[lo];
+        const uint32_t c = tp[3];
+        const uint32_t j = e - (sh.incl[lo] - (c - 1u)) + 1u;
+        emit(tp[0], tp[1], tp[2], c, tp[4], tp[5], tp[6], tp[7], j);
     }
 }
 
