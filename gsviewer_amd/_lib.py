@@ -12,7 +12,23 @@ import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 # GSR_LIB_PATH selects an alternative build (A/B experiments); default: in-tree.
-LIB_PATH = os.environ.get("GSR_LIB_PATH") or os.path.join(_PKG, "libgsr.so")
+_DEFAULT_LIB = os.path.join(_PKG, "libgsr.so")
+LIB_PATH = os.environ.get("GSR_LIB_PATH") or _DEFAULT_LIB
+
+
+def check_fresh(lib):
+    """The in-tree library must be built from the sources beside it
+    (_srcid.py): a stale .so raises instead of standing in for the tree.
+    Skipped when the sources are absent (an installed package)."""
+    from gsviewer_amd import _srcid
+    if not os.path.isdir(_srcid.CSRC):
+        return
+    want = _srcid.source_digest()
+    got = lib.gsr_source_digest()
+    got = got.decode() if got else ""
+    if got != want:
+        raise RuntimeError(f"gsviewer_amd: {_DEFAULT_LIB} was built from other sources (digest {got}, tree {want}); "
+                           "rebuild it with `python -m gsviewer_amd.build`")
 
 
 class GsrCamera(ctypes.Structure):
@@ -100,6 +116,7 @@ _P = ctypes.c_void_p
 SIGNATURES = {
     "gsr_abi_version": (ctypes.c_int, []),
     "gsr_last_error": (ctypes.c_char_p, []),
+    "gsr_source_digest": (ctypes.c_char_p, []),
     "gsr_settings_default": (None, [ctypes.POINTER(GsrSettings)]),
     "gsr_scene_create": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int64, ctypes.c_int32, _P,
                                         ctypes.POINTER(_P)]),
@@ -130,6 +147,7 @@ SIGNATURES = {
     "gsr_debug_sort_pairs": (ctypes.c_int, [_P, _P, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _P, _P, _P]),
     "gsr_debug_copy": (ctypes.c_int64, [_P, ctypes.c_int32, _P, ctypes.c_int64, _P]),
     "gsr_debug_stall": (ctypes.c_int, [_P, ctypes.c_uint32]),
+    "gsr_context_knob": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "gsr_context_set_profiling": (ctypes.c_int, [_P, ctypes.c_int32]),
     "gsr_context_stage_times": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
     "gsr_context_group_spans": (ctypes.c_int64, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int64]),
@@ -152,7 +170,7 @@ STAGES = ["cull", "preprocess", "depth_sort", "binning", "tile_sort", "tile_rang
 
 GSR_DEBUG_RECORDS, GSR_DEBUG_DEPTH_ORDER, GSR_DEBUG_TILE_RANGES, GSR_DEBUG_TILE_LIST = 0, 1, 2, 3
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_VIEWS = 8  # GSR_MAX_VIEWS (include/gsr.h)
 
 _lib = None
@@ -184,6 +202,8 @@ def load(path: str = LIB_PATH):
             fn.argtypes = args
         if lib.gsr_abi_version() != ABI_VERSION:
             raise RuntimeError("gsviewer_amd: ABI version mismatch between libgsr.so and bindings")
+        if path == _DEFAULT_LIB:
+            check_fresh(lib)
         _lib = lib
         return lib
 

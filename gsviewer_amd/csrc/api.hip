@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "gsr_internal.h"
@@ -177,7 +178,7 @@ struct gsr_context {
                                                   // n_dup / chunk_target (rounded up to 64; at most
                                                   // chunk_views), 0: `chunk` always (frame_chunk).  16384:
                                                   // C3 704-instance chunks (latency 1.56 -> 1.40 ms), c2h 320
-                                                  // (0.80 -> 0.66), C2 / C5 unchanged (profiles/r5_s17)
+                                                  // (0.80 -> 0.66), C2 / C5 unchanged (profiles/r5_s17, r5_s20)
     uint32_t chunk_views = 3072;                  // ... of a group's frames (gsr_render_finish_views): with
                                                   // views in flight the other views fill the chip while a
                                                   // deep tile's long chunk runs, so few chunks (fewer partials,
@@ -202,6 +203,9 @@ struct gsr_context {
     gsr::DevBuf<uint32_t> long_runs;       // starts of the runs that outgrow the repair window (k_long_runs)
     bool rect_payload = true;              // the depth sort carries the packed tile rects (GSR_NO_RECT_PAYLOAD:
                                            // the binning gathers them by slot; A/B and test knob)
+    // the forms the last finished frame took (gsr_context_knob "frame_*")
+    bool last_packed = false, last_deep = false;
+    uint32_t last_coarse = 0, last_chunk = 0;
     uint32_t* host_counters = nullptr;      // pinned, host-mapped: (V, D, seq) stored by the last preprocess block
     uint32_t seq = 0;                       // frame sequence number the host waits for
     uint32_t* host_counters_dev = nullptr;  // its device address
@@ -792,6 +796,23 @@ int gsr_context_destroy(gsr_context* c) {
     return GSR_OK;
 }
 
+int gsr_context_knob(const gsr_context* c, const char* name, int64_t* value) {
+    if (!c || !name || !value) return set_error(GSR_ERR_INVALID, "null argument");
+    const std::pair<const char*, int64_t> knobs[] = {
+        {"rect_payload", c->rect_payload}, {"fused_cull", c->fused_cull}, {"bin_fused", c->bin_fused},
+        {"depth_coarse_alone", c->depth_coarse_alone}, {"chunk", c->chunk}, {"chunk_target", c->chunk_target},
+        {"chunk_views", c->chunk_views}, {"tail_merge_alone", c->tail_merge_alone},
+        {"tail_merge_group", c->tail_merge_group}, {"first_major", c->first_major},
+        {"first_major_alone", c->first_major_alone}, {"frame_packed", c->last_packed},
+        {"frame_coarse", c->last_coarse}, {"frame_chunk", c->last_chunk}, {"frame_deep", c->last_deep}};
+    for (const auto& k : knobs)
+        if (std::strcmp(k.first, name) == 0) {
+            *value = k.second;
+            return GSR_OK;
+        }
+    return set_error(GSR_ERR_INVALID, std::string("context_knob: unknown knob ") + name);
+}
+
 int gsr_context_stats(const gsr_context* c, gsr_frame_stats* out) {
     if (!c || !out) return set_error(GSR_ERR_INVALID, "null argument");
     *out = c->stats;
@@ -1235,6 +1256,10 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     c->frame_idx += 1;
     c->stats.n_visible = n_vis;
     c->stats.n_instances = n_dup;
+    c->last_packed = f.packed;
+    c->last_coarse = f.coarse;
+    c->last_chunk = f.blend == GSR_BLEND_UNORM8 ? 0u : frame_chunk(c, n_dup);
+    c->last_deep = c->last_chunk > c->chunk;
     return GSR_OK;
 }
 
@@ -1264,9 +1289,10 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         if (c->prof_on) return set_error(GSR_ERR_INVALID, "render_finish_views: profiling is per view");
         for (int w = 0; w < v; ++w)
             if (ctxs[w] == c) return set_error(GSR_ERR_INVALID, "render_finish_views: contexts must differ");
+        // (only gsr_render sorts coarsely, and it finishes its own frame: an internal invariant)
         if (f.coarse)
-            return set_error(GSR_ERR_INVALID, "render_finish_views: a frame begun by gsr_render_begin (coarse depth "
-                                              "order) is finished by gsr_render_finish");
+            return set_error(GSR_ERR_INVALID, "render_finish_views: internal error: a coarse depth order (gsr_render's "
+                                              "own) reached a group finish");
         if (f.u.width != f0.u.width || f.u.height != f0.u.height || f.t_min != f0.t_min || f.bg[0] != f0.bg[0] ||
             f.bg[1] != f0.bg[1] || f.bg[2] != f0.bg[2] || f.out_layout != f0.out_layout || f.blend != f0.blend ||
             frag_class_of(f.u.render_mod) != frag_class_of(f0.u.render_mod) || c->chunk_views != c0->chunk_views ||
@@ -1407,6 +1433,10 @@ int gsr_render_finish_views(gsr_context* const* ctxs, int32_t k, void* stream) {
         c->frame_idx += 1;
         c->stats.n_visible = fv[v].n_vis;
         c->stats.n_instances = fv[v].n_dup;
+        c->last_packed = c->pend.packed;
+        c->last_coarse = 0;
+        c->last_chunk = f0.blend == GSR_BLEND_UNORM8 ? 0u : c0->chunk_views;
+        c->last_deep = false;
     }
     return GSR_OK;
 }

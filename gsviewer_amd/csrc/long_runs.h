@@ -352,6 +352,12 @@ __device__ void tds_global(uint32_t* __restrict__ keys, uint32_t* __restrict__ v
     if (hi == lo) return;
     const uint32_t B = 32u - (uint32_t)__clz(hi - lo);
     const uint32_t P = tds_passes(B, true);
+    // The result lands in (keys, vals) only after an even number of passes
+    // (each pass swaps source and scratch); an odd count would leave the
+    // sorted run in the scratch and the list half permuted.  Trap rather than
+    // composite such a list (the sorters' invariants checked
+    // on the device; uniform, one scalar test per long run).
+    if (P & 1u) __builtin_trap();
     TdsPass dg;
     dg.kmin = lo;
     dg.w = (B + P - 1u) / P;
@@ -477,6 +483,8 @@ __device__ void long_runs_block(const LongRunArgs& a, TdsLds& S, uint32_t bid, u
         const uint32_t tile = a.tile_keys[b];
         const uint32_t cv = (a.inst_keys[b] - kmin) >> s0;
         const uint32_t L = run_end(a, b, a.ranges[tile].y, tile, cv, kmin, s0) - b;
+        // (a listed run lies in its tile's list: b < run end <= the tile's end, so every sorter below reads and
+        // writes [b, b + L) of the list and its scratch only)
         if (L <= kTdsCapWave) tds_wave(a.inst_keys, a.vals, b, L, S.wave[w]);
         if (lane == 0) a.lens[r] = L;
     }

@@ -182,6 +182,13 @@ class HipContext:
         _lib.check(_lib.load().gsr_context_stats(self._h, ctypes.byref(st)), "gsr_context_stats")
         return {f: getattr(st, f) for f, _ in st._fields_}
 
+    def knob(self, name: str) -> int:
+        """gsr_context_knob: a stage-form knob as read at creation, or the
+        form the last frame took ("frame_packed", "frame_coarse", ...)."""
+        v = ctypes.c_int64()
+        _lib.check(_lib.load().gsr_context_knob(self._h, name.encode(), ctypes.byref(v)), "gsr_context_knob")
+        return int(v.value)
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.load().gsr_context_destroy(self._h)  # synchronises: the workspace is free after it

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 6
+#define GSR_ABI_VERSION 7
 
 typedef enum gsr_status {
     GSR_OK = 0,
@@ -104,6 +104,10 @@ typedef struct gsr_frame_stats {
 
 int gsr_abi_version(void);
 const char* gsr_last_error(void);
+/* 16 hex digits of the digest of the sources the library was built from
+ * (gsviewer_amd/_srcid.py); the Python binding refuses a library older than
+ * the tree it sits in. */
+const char* gsr_source_digest(void);
 
 /* Reference start-up uniform state (main.py:128-137, renderer_ogl.py:183-187). */
 void gsr_settings_default(gsr_settings* s);
@@ -319,6 +323,18 @@ int gsr_debug_stall(void* stream, uint32_t microseconds);
  *   GSR_DEBUG_TILE_LIST    uint32 record slots of all (tile, splat) instances, by tile then depth */
 enum { GSR_DEBUG_RECORDS = 0, GSR_DEBUG_DEPTH_ORDER = 1, GSR_DEBUG_TILE_RANGES = 2, GSR_DEBUG_TILE_LIST = 3 };
 int64_t gsr_debug_copy(const gsr_context* ctx, int32_t what, void* dst_dev, int64_t max_bytes, void* stream);
+
+/* Test / A-B hook: the value of a stage-form knob of `ctx` as read from the
+ * environment at gsr_context_create, or the form the context's last frame
+ * took.  Knobs: "rect_payload" (0 = GSR_NO_RECT_PAYLOAD), "fused_cull",
+ * "bin_fused", "depth_coarse_alone", "chunk", "chunk_target", "chunk_views",
+ * "tail_merge_alone", "tail_merge_group", "first_major", "first_major_alone".
+ * Last frame: "frame_packed" (its depth sort carried the packed tile rects),
+ * "frame_coarse" (its depth sort's coarse bits, 0 = exact), "frame_chunk" (its
+ * compositing chunk length; 0 for the RGBA8 framebuffer), "frame_deep" (1: the
+ * deep-frame form: longer chunks and the cross-chunk transmittance bound).
+ * GSR_ERR_INVALID for an unknown name.  No GPU work. */
+int gsr_context_knob(const gsr_context* ctx, const char* name, int64_t* value);
 
 #ifdef __cplusplus
 }

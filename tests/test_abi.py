@@ -97,3 +97,35 @@ def test_workspace_size_needs_no_gpu():
         workspace_size(-1, 640, 480, 0)
     with pytest.raises(RuntimeError, match="context_reserve"):
         workspace_size(10, 0, 480, 0)
+
+
+def test_context_knobs_read_at_creation(monkeypatch):
+    """gsr_context_knob reports the stage forms a context read from the
+    environment at creation (host only: creating a context makes no HIP call)."""
+    from gsviewer_amd.rasterizer import HipContext
+    a = HipContext()
+    assert a.knob("rect_payload") == 1 and a.knob("chunk") == 192 and a.knob("frame_chunk") == 0
+    monkeypatch.setenv("GSR_NO_RECT_PAYLOAD", "1")
+    monkeypatch.setenv("GSR_CHUNK", "256")
+    b = HipContext()
+    assert b.knob("rect_payload") == 0 and b.knob("chunk") == 256
+    assert a.knob("rect_payload") == 1  # read once, at creation
+    with pytest.raises(RuntimeError, match="unknown knob"):
+        a.knob("no_such_knob")
+    a.close()
+    b.close()
+
+
+def test_stale_library_refused(monkeypatch):
+    """The in-tree library carries the digest of its sources; a library built
+    from other sources is refused (tools/gpu_round.sh loads, never builds)."""
+    from gsviewer_amd import _srcid
+    lib = _lib.load()
+    assert lib.gsr_source_digest().decode() == _srcid.source_digest()
+
+    class Stale:
+        @staticmethod
+        def gsr_source_digest():
+            return b"0000000000000000"
+    with pytest.raises(RuntimeError, match="built from other sources"):
+        _lib.check_fresh(Stale())

@@ -13,7 +13,14 @@ the batched finish: binning, tile lists, compositing, merge) with planar
   their own streams, stepped round the ring as bench.py's timed region does
   (each context renders its view again), t_min 1e-4;
 * the C2 frame alone through gsr_render (the drop-in render() path: coarse
-  depth order + run repair), t_min 1e-4.
+  depth order + run repair), t_min 1e-4;
+* C3, C5, C5+AABB and C5+OBB frames alone through gsr_render (VERDICT r5
+  #1): the coarse depth order with its run repair and long-run sorts at full
+  size, and at C3 the deep-frame form (704-instance chunks, first chunks
+  dispatched first, the cross-chunk transmittance bound) over 10.6 M
+  instances; C3 rendered three times to bound the deep form's run-to-run
+  difference (deep frames: each image lies within t_min of the full
+  composite, so two lie within t_min of each other).
 
 Per view: the image against the oracle with the stated tolerances (helpers.py)
 plus an absolute census of the channels above 2e-5 (+ t_min), bounded at what
@@ -180,3 +187,66 @@ def test_c2_frame_alone(gpu):
     cam = Camera(1080, 1920)
     r = gpu_frame(g, cam, st, with_debug=True)
     _check("C2 alone", g, st, [cam], [r], 1_000_000, 1920, 1080, 1e-4)
+
+
+RUN_TO_RUN = 2e-6  # float slack of the fold beside the deep form's t_min bound
+
+
+def _alone(case, n, seed, W, H, t_min, box="none", order_check=True, repeats=1):
+    """A frame alone through gsr_render (the drop-in render() path) on the
+    cached full-size scene, checked like the group frames; with repeats > 1
+    the same context renders the frame again and the images are returned."""
+    import torch
+
+    from gsviewer_amd.rasterizer import HipContext, camera_from, render_into
+    g, scene = _scene(n, seed)
+    st = _settings(t_min=t_min, **_box(g, box))
+    st.out_layout = 1
+    cam = Camera(H, W)
+    camc = camera_from(cam)
+    ctx = HipContext()
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    render_into(ctx, scene, camc, st, out)
+    torch.cuda.synchronize()
+    r = {"image": out.cpu().numpy(), "stats": ctx.stats(), "depth_coarse": ctx.knob("frame_coarse"),
+         "deep": ctx.knob("frame_deep"), "chunk": ctx.knob("frame_chunk")}
+    if order_check:
+        r.update(grab_debug(ctx, r["stats"]))
+    again = []
+    for _ in range(repeats - 1):
+        render_into(ctx, scene, camc, st, out)
+        torch.cuda.synchronize()
+        again.append(out.cpu().numpy())
+    ctx.close()
+    _check(case, g, st, [cam], [r], n, W, H, t_min, box, order_check)
+    return r, again
+
+
+def test_c3_frame_alone_deep(gpu):
+    """C3 alone: coarse order + repair + long runs over 10.6 M instances, the
+    deep-frame chunks and the cross-chunk bound, against the oracle; then the
+    run-to-run bound of the deep form (three renders of one context)."""
+    r, again = _alone("C3 alone", 6_000_000, 2, 1920, 1080, 1e-4, repeats=3)
+    assert r["deep"] == 1 and r["chunk"] > 192 and r["depth_coarse"] > 0, r
+    for k, img in enumerate(again):
+        d = np.abs(img.astype(np.float64) - r["image"].astype(np.float64))
+        cen = dict(case="C3 alone run-to-run", repeat=k + 1, max=float(d.max()), n_differ=int((d > 0).sum()),
+                   channels=int(d.size), bound=1e-4 + RUN_TO_RUN)
+        with open(CENSUS, "a") as f:
+            f.write(json.dumps(cen) + "\n")
+        assert d.max() <= 1e-4 + RUN_TO_RUN, cen
+
+
+def test_c5_frame_alone(gpu):
+    r, _ = _alone("C5 alone", 1_000_000, 1, 3840, 2160, 1e-4)
+    assert r["depth_coarse"] > 0
+
+
+def test_c5_frame_alone_aabb(gpu):
+    r, _ = _alone("C5+AABB alone", 1_000_000, 1, 3840, 2160, 1e-4, box="aabb", order_check=False)
+    assert r["stats"]["n_visible"] < 1_000_000
+
+
+def test_c5_frame_alone_obb(gpu):
+    r, _ = _alone("C5+OBB alone", 1_000_000, 1, 3840, 2160, 1e-4, box="obb")
+    assert r["stats"]["n_visible"] < 1_000_000

@@ -22,7 +22,6 @@ checks that form's global order and tile lists against the oracle):
   frame must stay within 1.5x the exact form's time;
 * a group of views (exact sort) against the same views alone (coarse).
 """
-import time
 
 import numpy as np
 import pytest
@@ -187,15 +186,19 @@ def _frame_ms(monkeypatch, g, cam, st, form, reps=10):
     st.out_layout = 1
     render_into(ctx, scene, c, st, out)
     torch.cuda.synchronize()
+    # device time by HIP events on the frames' stream (host timers
+    # at 0.2 ms a frame measure mostly the host), median over the frames
     ts = []
     for _ in range(reps):
-        t0 = time.perf_counter()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         render_into(ctx, scene, c, st, out)
-        torch.cuda.synchronize()
-        ts.append(time.perf_counter() - t0)
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
     ctx.close()
     scene.close()
-    return 1e3 * float(np.median(ts))
+    return float(np.median(ts))
 
 
 def test_plane_with_far_splat(gpu, monkeypatch):
@@ -210,8 +213,8 @@ def test_plane_with_far_splat(gpu, monkeypatch):
     _same(got, exact)
     lens = got["ranges"][:, 1].astype(np.int64) - got["ranges"][:, 0]
     assert lens.max() > 1000, lens.max()
-    ms_coarse = _frame_ms(monkeypatch, g, cam, _settings(t_min=1e-4), "coarse")
-    ms_exact = _frame_ms(monkeypatch, g, cam, _settings(t_min=1e-4), "exact")
+    ms_coarse = _frame_ms(monkeypatch, g, cam, _settings(t_min=1e-4), "coarse", reps=15)
+    ms_exact = _frame_ms(monkeypatch, g, cam, _settings(t_min=1e-4), "exact", reps=15)
     print(f"plane + far splat, 1080p: coarse {ms_coarse:.3f} ms, exact {ms_exact:.3f} ms")
     assert ms_coarse <= 1.5 * ms_exact, (ms_coarse, ms_exact)
 

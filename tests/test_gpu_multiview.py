@@ -301,7 +301,7 @@ def test_rect_payload_matches_gathered_rects(gpu, monkeypatch):
     import torch
 
     from gsviewer_amd.multiview import ViewBatchPipeline
-    from gsviewer_amd.rasterizer import camera_from, render_into
+    from gsviewer_amd.rasterizer import HipContext, camera_from, render_into
     scene, st, cams, ctxs, streams, outs = _setup(4)
     near = Camera(180, 320)
     near.target_dist = 0.4
@@ -309,16 +309,22 @@ def test_rect_payload_matches_gathered_rects(gpu, monkeypatch):
     got = {}
     for mode in ("payload", "gather"):
         if mode == "gather":
+            # the knob is read at context creation: fresh contexts
             monkeypatch.setenv("GSR_NO_RECT_PAYLOAD", "1")
+            for c in ctxs:
+                c.close()
+            ctxs = [HipContext() for _ in ctxs]
         o = torch.empty_like(outs[0])
         render_into(ctxs[0], scene, cams[3], st, o)
         assert 0 < ctxs[0].stats()["n_visible"] < scene.n
+        assert ctxs[0].knob("frame_packed") == (mode == "payload")  # the form this frame took
         # the context moves to another stream: its frame on this one must be done
         torch.cuda.synchronize()
         pipe = ViewBatchPipeline([(ctxs, cams, outs, streams[0])], scene, st)
         pipe.step()
         pipe.drain()
         torch.cuda.synchronize()
+        assert [c.knob("frame_packed") for c in ctxs] == [mode == "payload"] * len(ctxs)
         got[mode] = ([o.cpu().numpy()] + [x.cpu().numpy() for x in outs], [c.stats() for c in ctxs])
     for a, b in zip(got["payload"][0], got["gather"][0]):
         np.testing.assert_array_equal(a, b)
