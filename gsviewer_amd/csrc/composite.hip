@@ -1789,6 +1789,15 @@ __device__ __forceinline__ uint32_t comp_block() {
     return w * W + (r & 7u) * R + (r >> 3);
 }
 
+// Experiment (GSR_COMP_PERSIST = resident blocks per CU, 0 = off): a frame
+// alone's compositing as a resident grid whose waves take the dispatch order
+// (longest chunks first) in a snake, wave g positions g, 2G-1-g, 2G+g, ...,
+// so every wave's chunks sum to about the same work instead of the
+// dispatcher's greedy block placement.
+#ifndef GSR_COMP_PERSIST
+#define GSR_COMP_PERSIST 0
+#endif
+
 template <int FRAG, bool kBound>
 __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const uint4* __restrict__ desc,
                                                         const uint32_t* __restrict__ order,
@@ -1800,6 +1809,18 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
                                                         const uint32_t* __restrict__ chunk_base) {
     __shared__ float4 lds[kCompWaves][kBatch * 3];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (GSR_COMP_PERSIST > 0) {
+        const uint32_t total = (uint32_t)a.num_tiles + n_chunks_dev[0];
+        const uint32_t G = gridDim.x * kCompWaves, g = comp_block() * kCompWaves + wave;
+        for (uint32_t r = 0;; ++r) {  // (a wave's positions increase with r: the first past the end ends it)
+            const uint32_t pos = r * G + ((r & 1u) ? G - 1u - g : g);
+            if (pos >= total) break;
+            const uint32_t slot = order[pos];
+            composite_chunk<FRAG, kBound>(desc[slot], slot, lds[wave], list, recs, a, out, partial, sat, tmax,
+                                          chunk_base);
+        }
+        return;
+    }
     const uint32_t pos = comp_block() * kCompWaves + wave;
     if (pos >= (uint32_t)a.num_tiles + n_chunks_dev[0]) return;  // device count of extra chunks
     const uint32_t slot = order[pos];
@@ -2359,7 +2380,17 @@ int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n
                      float4* partial, float4* tmax, bool tail_merge, hipStream_t s) {
     const CompositeArgs a = make_args(u, t_min, bg, out_layout, tail_merge);
     if (max_chunks == 0) return GSR_OK;
-    const unsigned grid = (unsigned)((max_chunks + kCompWaves - 1) / kCompWaves);
+    unsigned grid = (unsigned)((max_chunks + kCompWaves - 1) / kCompWaves);
+    if (GSR_COMP_PERSIST > 0) {  // experiment: a resident grid (k_composite)
+        static int cus = 0;
+        if (!cus) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+                cus = 256;
+        }
+        grid = std::min(grid, (unsigned)(cus * GSR_COMP_PERSIST));
+    }
     const bool bound = tmax != nullptr;  // the cross-chunk transmittance bound (launch_chunks initialised tmax)
     switch (frag_class) {
         case kFragGauss:
