@@ -35,9 +35,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-SIMDS = 256 * 4        # MI355X CUs x SIMDs
-VALU_NS = 1.6          # measured issue cost of a wave64 f32 VALU instruction per SIMD (valu_rate.hip)
-TRANS_NS = 3.5         # ... of a transcendental (v_exp_f32)
+CUS = 256
+SIMDS = CUS * 4        # MI355X CUs x SIMDs
+CLOCK_GHZ = 2.4        # MI355X max clock (the chip holds less under load: issue fractions are lower bounds)
+# VALU issue per SIMD with several waves resident: a wave64 instruction every 2 cycles (SIMD-32,
+# MI355X_MICROARCH.md "Wave scheduling"; a transcendental twice that, its 8-cycle one-wave cost against 4);
+# round 4's marginal test on the compositor measured 0.73 ns per added VALU (profiles/r4_s16: 1.75 cycles)
+VALU_NS = 2.0 / CLOCK_GHZ
+TRANS_NS = 4.0 / CLOCK_GHZ
+REPEATS = 3            # instrumented repeats of the timed region (compositor busy union: the median)
 
 CONFIGS = {
     # name: (N, sh_degree, width, height, description)
@@ -200,7 +206,8 @@ def cpu_baseline(g, cam, seconds):
 # stage name -> kernel symbol in rocprofv3 summaries
 JSON_OUT = sys.stdout  # main() points it at the real stdout before routing fd 1 to stderr
 
-KERNEL_SYMBOL = {"composite": "k_composite<0>", "preprocess": "k_preprocess_fc_views<3, true>", "merge": "k_merge"}
+KERNEL_SYMBOL = {"composite": "k_composite<0, false>", "preprocess": "k_preprocess_fc_views<3, true>",
+                 "merge": "k_merge"}
 PMC_PROFILE = os.path.join(ROOT, "profiles", "LATEST")
 
 
@@ -212,13 +219,14 @@ def pmc_counters(kernel, args):
     are read back here rather than measured inside the timed region."""
     if kernel is None or args.config != "c2" or args.n or args.width or args.height or args.box != "none":
         return None, None
+    import csv
     try:
         d = open(PMC_PROFILE).read().strip()
-        path = os.path.join(ROOT, "profiles", d, "pmc_summary.csv")
-        rows = [ln.strip().split(",") for ln in open(path).read().splitlines()[1:]]
+        with open(os.path.join(ROOT, "profiles", d, "pmc_summary.csv")) as fh:
+            rows = list(csv.reader(fh))[1:]  # (kernel names hold commas: "k_composite<0, false>")
     except OSError:
         return None, None
-    return {r[1]: float(r[4]) for r in rows if r[0].strip('"') == kernel}, f"profiles/{d}/pmc_summary.csv ({kernel})"
+    return {r[1]: float(r[4]) for r in rows if r[0] == kernel}, f"profiles/{d}/pmc_summary.csv ({kernel})"
 
 
 def rocprof_avg_ms(kernel, args):
@@ -248,57 +256,129 @@ def pmc_traffic(kernel, args):
     return got["FETCH_SIZE"] + got["WRITE_SIZE"], src
 
 
-def valu_issue(kernel, args, ms_per_launch):
-    """The compositor's real limiter: VALU issue.  Issue cost per wave64
-    instruction per SIMD, measured on this chip with 8 waves/SIMD of
-    independent instructions (tools/microbench/valu_rate.hip, output in
-    profiles/<round>/valu_rate.txt): 1.6 ns for an f32 add/mul/fma or a
-    compare/select, 3.5 ns for a transcendental (v_exp_f32).  256 CUs x 4 SIMDs."""
-    got, src = pmc_counters(kernel, args)
-    if not got or "SQ_INSTS_VALU" not in got:
+def default_shape(args):
+    """The committed profiles describe the default C2 command only."""
+    return args.config == "c2" and not (args.n or args.width or args.height) and args.box == "none"
+
+
+def latest():
+    return open(PMC_PROFILE).read().strip()
+
+
+def committed_json(name, args):
+    """A JSON file of the committed profile of this same bench command
+    (profiles/<LATEST>/name), or None."""
+    if not default_shape(args):
         return None
-    valu, trans = got["SQ_INSTS_VALU"], got.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
-    t_issue = (VALU_NS * (valu - trans) + TRANS_NS * trans) * 1e-9 / SIMDS
-    return {"valu_instr_per_launch": valu, "trans_instr_per_launch": trans, "issue_us": t_issue * 1e6,
-            "launch_us": ms_per_launch * 1e3, "frac": t_issue / (ms_per_launch * 1e-3),
-            "issue_ns_per_instr": {"valu": VALU_NS, "trans": TRANS_NS}, "source": src}
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", latest(), name)))
+    except (OSError, ValueError):
+        return None
 
 
-def frame_valu_issue(args, share, ms_per_frame):
-    """VALU issue of the frame in flight over all its kernels (tools/frame_valu.py):
-    the view-batched kernels' SQ_INSTS_VALU (+ transcendentals) per view-frame
-    from the same committed PMC summary, priced like valu_issue, against the
-    measured frame time.  With views in flight the frame is VALU-issue bound
-    (DESIGN.md, "The frame in flight: VALU issue over all kernels")."""
-    if share <= 1 or args.config != "c2" or args.n or args.width or args.height or args.box != "none":
+def stage_bytes(n, nvis, inst, ntiles, W, H, rec_bytes, share=1, depth_passes=2):
+    """Each stage's own algorithmic bytes per frame (DESIGN.md "Kernels of a
+    frame"): the scene read once per group of `share` views (SoA: 16-B
+    position of every Gaussian, the rest of the record for the visible ones),
+    12 B key + rect per slot and a 48-B record per visible splat out; per radix
+    pass 12 B in + 12 B out per key (key, slot, payload); the binning's rect
+    and slot in, 8 B per instance out; the tile sort's pass 8 + 8 B per
+    instance; the compositor's 48-B record + 4-B slot per instance, the tile
+    ranges and the image."""
+    attrs = rec_bytes - 16 + 4  # SoA planes: 240 B per Gaussian at SH 3 (pos+opacity 16, rot 16, scale 16, SH 192)
+    return {
+        "preprocess": (n * 16 + nvis * attrs) / share + n * 12 + nvis * 48,
+        "depth_sort": n * 12 + nvis * 12 + (depth_passes - 1) * nvis * 24,
+        "binning": nvis * 8 + inst * 8,
+        "tile_sort": inst * 16,
+        "tile_ranges": inst * 4 + ntiles * 8,
+        "composite": inst * (48 + 4) + ntiles * 8 + W * H * 12,
+        "merge": W * H * 12,
+    }
+
+
+# kernels of the timed region (groups of views) -> the stage whose bytes they move
+REGION_STAGE = {
+    "k_preprocess_fc_views<3, false>": "preprocess",
+    "k_rs_scatter_views<8, true, 8>": "depth_sort",
+    "k_bin_scatter_views<true, 8>": "binning",
+    "k_rs_scatter_views<8, false, 8>": "tile_sort",
+    "k_tile_ranges_views<false>": "tile_ranges",
+    "k_composite_views<0>": "composite",
+}
+
+
+def per_kernel_table(region, n, nvis, inst, ntiles, W, H, rec_bytes, share):
+    """Per kernel of the timed region: its own algorithmic bytes per frame
+    (stage_bytes; a group's depth sort runs 4 exact passes) over its busy time
+    per frame in the committed rocprofv3 trace of this command (the union of
+    its launches, tools/region_kernels.py).  The four group streams overlap,
+    so busy times add up to more than the frame (concurrency ~2)."""
+    by = stage_bytes(n, nvis, inst, ntiles, W, H, rec_bytes, share=share, depth_passes=4)
+    rows = {}
+    for k, v in region["timed_region"]["kernels"].items():
+        st = REGION_STAGE.get(k)
+        row = {"busy_us_per_frame": round(v["busy_us_per_frame"], 2), "launches": v["launches"]}
+        if st:
+            gbps = by[st] / (v["busy_us_per_frame"] * 1e-6) / 1e9
+            row.update(stage=st, alg_bytes_per_frame=int(by[st]), GBps=round(gbps, 1),
+                       frac=round(gbps / HBM_PEAK_GBS, 4))
+        rows[k] = row
+    return {"kernels": rows, "region_span_us_per_frame": region["timed_region"]["span_us_per_frame"],
+            "region_busy_us": region["timed_region"]["busy_us"],
+            "source": f"profiles/{latest()}/region_kernels.json",
+            "note": "radix upsweeps, offsets scans, histograms and chunk kernels move few bytes (counts): "
+                    "listed with their busy time only"}
+
+
+def frame_resources(args, share, ms_per_frame, b_frame, fps):
+    """Demand of the frame in flight on each chip resource, as a fraction of
+    what the chip offers over the frame time, from the committed PMC summary
+    of this same command (every *_views kernel, per view-frame):
+    VALU issue (wave64 instructions at 2 cycles per SIMD, transcendentals 4,
+    MI355X_MICROARCH.md; 1024 SIMDs at 2.4 GHz: a lower bound under DVFS),
+    LDS (SQ_LDS_IDX_ACTIVE LDS-array cycles per CU, 256 CUs), HBM (the
+    counted FETCH x 2 + WRITE bytes, and SURVEY 8(d)'s B_frame, at 8 TB/s)."""
+    if share <= 1 or not default_shape(args):
         return None
     import csv
     try:
-        d = open(PMC_PROFILE).read().strip()
-        with open(os.path.join(ROOT, "profiles", d, "pmc_summary.csv")) as fh:
+        with open(os.path.join(ROOT, "profiles", latest(), "pmc_summary.csv")) as fh:
             rows = list(csv.reader(fh))[1:]  # (kernel names hold commas: "k_rs_scatter_views<8, true, 8>")
     except OSError:
         return None
-    valu, trans, disp = {}, {}, {}
+    tot, disp = {}, {}
     for r in rows:
-        k = r[0]
-        # the group kernels only: the fused preprocess of a frame alone is the same template
-        # instantiated <DEG, true> (it runs in the latency regions, not in the frame in flight)
-        if "_views" not in k or k.endswith(", true>"):
+        k, c = r[0], r[1]
+        if "_views" not in k or k.endswith(", true>"):  # the group kernels (not the frame alone's preprocess)
             continue
-        if r[1] == "SQ_INSTS_VALU":
-            valu[k], disp[k] = float(r[4]), int(r[2])
-        elif r[1] == "SQ_INSTS_VALU_TRANS_F32":
-            trans[k] = float(r[4])
-    groups = disp.get("k_composite_views<0>")
+        tot[c] = tot.get(c, 0.0) + float(r[4]) * int(r[2])
+        if k == "k_composite_views<0>":
+            disp[c] = int(r[2])
+    groups = disp.get("SQ_INSTS_VALU") or disp.get("FETCH_SIZE")
     if not groups:
         return None
-    v = sum(valu[k] * disp[k] for k in valu) / groups / share
-    t = sum(trans.get(k, 0.0) * disp[k] for k in valu) / groups / share
-    issue_us = (VALU_NS * (v - t) + TRANS_NS * t) * 1e-3 / SIMDS
-    return {"valu_instr_per_view_frame": v, "trans_instr_per_view_frame": t, "issue_us": issue_us,
-            "frame_us": ms_per_frame * 1e3, "frac": issue_us / (ms_per_frame * 1e3),
-            "source": f"profiles/{d}/pmc_summary.csv (*_views kernels)"}
+    per = {c: v / groups / share for c, v in tot.items()}  # per view-frame
+    t = ms_per_frame * 1e-3
+    fr, raw = {}, {}
+    if "SQ_INSTS_VALU" in per:
+        trans = per.get("SQ_INSTS_VALU_TRANS_F32", 0.0)
+        issue = (VALU_NS * (per["SQ_INSTS_VALU"] - trans) + TRANS_NS * trans) * 1e-9 / SIMDS
+        fr["VALU issue"] = issue / t
+        raw.update(valu_instr=per["SQ_INSTS_VALU"], trans_instr=trans, valu_issue_us=issue * 1e6)
+    if "SQ_LDS_IDX_ACTIVE" in per:
+        lds = per["SQ_LDS_IDX_ACTIVE"] / (CUS * CLOCK_GHZ * 1e9)
+        fr["LDS"] = lds / t
+        raw.update(lds_array_cycles=per["SQ_LDS_IDX_ACTIVE"], lds_us=lds * 1e6)
+    if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
+        by = per["FETCH_SIZE"] + per["WRITE_SIZE"]
+        fr["HBM (counted traffic)"] = by / t / (HBM_PEAK_GBS * 1e9)
+        raw.update(traffic_bytes=by)
+    fr["HBM (B_frame)"] = b_frame * fps / 1e9 / HBM_PEAK_GBS
+    return {"fractions": {k: round(v, 4) for k, v in fr.items()}, "per_view_frame": raw,
+            "frame_us": ms_per_frame * 1e3, "prices": {"valu_ns": VALU_NS, "trans_ns": TRANS_NS,
+                                                       "clock_ghz": CLOCK_GHZ},
+            "source": f"profiles/{latest()}/pmc_summary.csv (*_views kernels)"}
 
 
 def busy_union_ms(spans):
@@ -315,21 +395,6 @@ def busy_union_ms(spans):
     if cur is not None:
         tot += cur[1] - cur[0]
     return tot * 1e-5
-
-
-def rocprof_busy(args):
-    """The committed rocprofv3 kernel trace's figure for the same kernel and
-    command (profiles/<LATEST>/composite_busy.json, tools/busy_union.py): the
-    union of the k_composite_views launches' intervals per 20-frame region."""
-    if args.config != "c2" or args.n or args.width or args.height or args.box != "none":
-        return None
-    try:
-        d = open(PMC_PROFILE).read().strip()
-        got = json.load(open(os.path.join(ROOT, "profiles", d, "composite_busy.json")))
-        return {"us_per_view": got["us_per_view"], "busy_us_per_region": got["busy_us_per_region_median"],
-                "regions": got["regions_of_the_bench_shape"], "source": f"profiles/{d}/composite_busy.json"}
-    except (OSError, KeyError, ValueError):
-        return None
 
 
 def _free_port():
@@ -637,10 +702,14 @@ def main():
         leads = [gr[0][0] for gr in groups]
         for c in leads:
             _lib.check(lib.gsr_context_set_profiling(c.handle, 2), "set_profiling")
-        pipe.next = 0
-        gp_elapsed = timed_region(lambda: pipelined(calls), 1, dev)
+        # REPEATS repeats of the timed region (one busy union each, the median
+        # is the figure: a single region's union spans +-10 % run to run)
+        gp_elapsed = []
+        for _ in range(REPEATS):
+            pipe.next = 0
+            gp_elapsed.append(timed_region(lambda: pipelined(calls), 1, dev))
         tot_ms, tot_l, tot_v, tot_span = 0.0, 0, 0, 0.0
-        spans = []  # every launch's in-kernel (start, end), 100 MHz ticks, device-wide clock
+        spans = []  # per lead context: its launches' in-kernel (start, end), 100 MHz ticks, device-wide clock
         for c in leads:
             cms, cl, cv, csp = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
             _lib.check(lib.gsr_context_group_times(c.handle, ctypes.byref(cms), ctypes.byref(cl), ctypes.byref(cv),
@@ -649,14 +718,18 @@ def main():
             buf = (ctypes.c_uint64 * 128)()
             got = lib.gsr_context_group_spans(c.handle, buf, 64)
             _lib.check(0 if got >= 0 else int(got), "group_spans")
-            spans += [(buf[2 * i], buf[2 * i + 1]) for i in range(min(int(got), 64))]
+            spans.append([(buf[2 * i], buf[2 * i + 1]) for i in range(min(int(got), 64))])
             _lib.check(lib.gsr_context_set_profiling(c.handle, 0), "set_profiling")
+        # region r's launches: the r-th of every lead (each lead leads one launch per region)
+        per_region = [busy_union_ms([sp[r] for sp in spans if len(sp) > r]) for r in range(REPEATS)]
         vstats = [c.stats() for c in ctxs]
         group_comp = dict(launches=tot_l, views=tot_v, ms_per_launch=tot_span / max(tot_l, 1),
                           event_ms_per_launch=tot_ms / max(tot_l, 1), views_per_launch=tot_v / max(tot_l, 1),
-                          busy_ms=busy_union_ms(spans), span_launches=len(spans),
+                          busy_ms_regions=per_region, busy_ms=float(np.median(per_region)),
+                          launches_per_region=tot_l / REPEATS, views_per_region=tot_v / REPEATS,
+                          span_launches=sum(len(sp) for sp in spans),
                           mean_instances=float(np.mean([v["n_instances"] for v in vstats])),
-                          instrumented_ms_per_frame=1e3 * gp_elapsed / timed_frames)
+                          instrumented_ms_per_frame=1e3 * float(np.median(gp_elapsed)) / timed_frames)
 
     # Per-stage times: a third region (view 0, one at a time) with libgsr's
     # HIP events recorded on the render stream between the stages.
@@ -704,83 +777,74 @@ def main():
 
     roof = None
     if stage:
-        kernels = {k: v for k, v in stage.items() if k not in ("sync", "instrumented_ms_per_frame")}
-        dom = max(kernels, key=kernels.get)
         inst = stats["n_instances"]
         ntiles = stats["tiles_x"] * stats["tiles_y"]
         nvis = stats["n_visible"]
-        # algorithmic bytes per launch of each stage (DESIGN.md "Roofline")
-        alg = {
-            "composite": inst * (48 + 4) + ntiles * 8 + W * H * 12,
-            "preprocess": n * 8 + nvis * (rec_bytes - 16 + 48 + 4),  # masks + visible attrs in, record+key out
-            "cull": n * 16 + (n // 64) * 12,
-            "depth_sort": nvis * 4 * 8 * 2 + nvis * 4 * 4,
-            "tile_sort": inst * 8 * 2 * 2 + inst * 4 * 2,
-            "binning": nvis * (4 + 16 + 4 + 4 + 4) + inst * 8,
-            "tile_ranges": inst * 4 * 2 + ntiles * 8,
-            "merge": stats.get("n_chunks_multi", 0) * 256 * 16 + W * H * 12,
-        }[dom]
-        achieved = alg / (stage[dom] * 1e-3) / 1e9
+        # each stage's own algorithmic bytes per frame alone (DESIGN.md "Kernels of a frame")
+        alg = stage_bytes(n, nvis, inst, ntiles, W, H, rec_bytes, share=1)
+        kernels = {k: v for k, v in stage.items() if k in alg}
+        dom = max(kernels, key=kernels.get)
+        achieved = alg[dom] / (stage[dom] * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg[dom],
                 "ms_per_launch": stage[dom], "traffic_source": None,
-                "frame": {"bytes": b_frame, "GBps": b_frame * fps / 1e9, "frac": b_frame * fps / 1e9 / HBM_PEAK_GBS},
+                "frame": {"bytes": b_frame, "GBps": b_frame * fps / 1e9, "frac": b_frame * fps / 1e9 / HBM_PEAK_GBS,
+                          "basis": "SURVEY 8(d) B_frame = N*R + W*H*12 per frame, at the timed region's frame rate"},
                 "measured_copy_GBps": copy_gbps}
-
         traffic = pmc_traffic(KERNEL_SYMBOL.get(dom), args)
         if traffic:
             roof["traffic"], roof["traffic_source"] = traffic
-        if dom == "composite":
-            roof["valu_issue"] = valu_issue(KERNEL_SYMBOL[dom], args, stage[dom])
-        frame_valu = frame_valu_issue(args, share, ms_per_step)
         if group_comp is not None and group_comp["launches"] > 0 and group_comp["busy_ms"] > 0:
-            # The timed region's dominant kernel: k_composite_views<0>, one launch per group.
-            # Its time is the union of its launches' in-kernel spans over a repeat of the timed
-            # region (the four groups' launches overlap at the end of the region: a launch's own
-            # span counts waits for CUs the others hold, and their spans summed exceed the
-            # region), i.e. the time the chip was running it; per view, at most ms_per_step.
+            # The timed region's dominant kernel: k_composite_views<0>, one launch per group of
+            # `vpl` views.  Bytes: its OWN algorithmic bytes (the records and slots of its instances,
+            # the tile ranges, the image; the scene read is the preprocess's).  Time:
+            # the union of the launches' in-kernel spans over a repeat of the timed region (the four
+            # groups' launches overlap: a launch's own span counts waits for CUs the others hold),
+            # the median of REPEATS repeats, per launch; beside it the same union from the committed
+            # rocprofv3 kernel trace of this command (profiles/LATEST/region_kernels.json).
             vpl = group_comp["views_per_launch"]
-            views = group_comp["views"]
             busy_ms = group_comp["busy_ms"]
-            us_view = 1e3 * busy_ms / views
-            ms_launch = busy_ms / group_comp["launches"]
-            # SURVEY 8(d)'s algorithmic bytes: B_frame per view (every Gaussian record read once,
-            # the float32 image written once); beside it the kernel's own bytes (its instances'
-            # 48-B records + 4-B ids, tile ranges, image)
-            alg_launch = b_frame * vpl
-            ach = alg_launch / (ms_launch * 1e-3) / 1e9
-            alg_view_local = group_comp["mean_instances"] * (48 + 4) + ntiles * 8 + W * H * 12
-            ach_local = alg_view_local * vpl / (ms_launch * 1e-3) / 1e9
+            us_view = 1e3 * busy_ms / group_comp["views_per_region"]
+            ms_launch = busy_ms / group_comp["launches_per_region"]
+            alg_view = group_comp["mean_instances"] * (48 + 4) + ntiles * 8 + W * H * 12
+            ach = alg_view * vpl / (ms_launch * 1e-3) / 1e9
             single = {k: roof.pop(k) for k in ("kernel", "achieved", "frac", "traffic", "alg_bytes_per_launch",
-                                               "ms_per_launch", "traffic_source", "valu_issue") if k in roof}
-            single["kernel"] = "k_composite<0> (one view at a time, gsr_render)"
+                                               "ms_per_launch", "traffic_source") if k in roof}
+            single["kernel"] = f"{KERNEL_SYMBOL.get(dom, dom)} (one view at a time, gsr_render: {dom} stage)"
             gt = pmc_traffic("k_composite_views<0>", args)
             prof = rocprof_avg_ms("k_composite_views<0>", args)
-            rbusy = rocprof_busy(args)
-            roof.update({"kernel": "k_composite_views<0> (the timed region's compositing, one launch per group "
+            region = committed_json("region_kernels.json", args)
+            rk = None
+            if region:
+                kk = region["timed_region"]["kernels"].get("k_composite_views<0>")
+                rk = {"us_per_view": kk["busy_us_per_frame"] if kk else None,
+                      "source": f"profiles/{latest()}/region_kernels.json (tools/region_kernels.py)"}
+            agree = (abs(us_view / rk["us_per_view"] - 1.0) if rk and rk["us_per_view"] else None)
+            roof.update({"kernel": f"k_composite_views<0> (the timed region's compositing, one launch per group "
                                    f"of {vpl:g} views)",
-                         "basis": "SURVEY 8(d) B_frame = N*R + W*H*12 per view composited",
-                         "achieved": ach, "frac": ach / HBM_PEAK_GBS, "alg_bytes_per_launch": alg_launch,
-                         "alg_bytes_per_view": b_frame,
-                         "ms_per_launch": ms_launch, "us_per_view": us_view,
-                         "timing": f"union of the in-kernel spans (first block start to last wave end, 100 MHz "
-                                   f"s_memrealtime) of the {group_comp['span_launches']} k_composite_views launches "
-                                   f"of a repeat of the timed region ({group_comp['instrumented_ms_per_frame']:.4f} "
-                                   f"ms/frame instrumented), over its {views} views; ms_per_launch = that busy time "
-                                   f"/ launches",
+                         "basis": "the kernel's own algorithmic bytes per view: instances x (48-B record + 4-B slot) "
+                                  "+ tiles x 8 (ranges) + W*H*12 (image)",
+                         "achieved": ach, "frac": ach / HBM_PEAK_GBS, "alg_bytes_per_launch": alg_view * vpl,
+                         "alg_bytes_per_view": alg_view, "ms_per_launch": ms_launch, "us_per_view": us_view,
+                         "timing": f"live: union of the in-kernel spans (first block start to last wave end, 100 MHz "
+                                   f"s_memrealtime) of the k_composite_views launches of a repeat of the timed "
+                                   f"region, median of {REPEATS} repeats ({[round(x, 4) for x in group_comp['busy_ms_regions']]} "
+                                   f"ms; {group_comp['instrumented_ms_per_frame']:.4f} ms/frame instrumented); "
+                                   f"ms_per_launch = that busy time / launches per region",
                          "cross_check": {"us_per_view_le_ms_per_step": us_view <= 1e3 * ms_per_step,
                                          "ms_per_step_us": 1e3 * ms_per_step,
                                          "achieved_le_peak": ach <= HBM_PEAK_GBS,
-                                         "rocprof_us_per_view": rbusy["us_per_view"] if rbusy else None,
-                                         "rocprof_source": rbusy["source"] if rbusy else None},
-                         "kernel_local": {"alg_bytes_per_launch": alg_view_local * vpl, "alg_bytes_per_view":
-                                          alg_view_local, "achieved": ach_local, "frac": ach_local / HBM_PEAK_GBS,
-                                          "basis": "the kernel's own bytes: instances x (48-B record + 4-B id) + "
-                                                   "tiles x 8 + W*H*12 per view"},
+                                         "rocprof_us_per_view": rk["us_per_view"] if rk else None,
+                                         "rocprof_frac": (alg_view / (rk["us_per_view"] * 1e-6) / 1e9 / HBM_PEAK_GBS
+                                                          if rk and rk["us_per_view"] else None),
+                                         "live_vs_rocprof": agree,
+                                         "rocprof_source": rk["source"] if rk else None,
+                                         "printed": "achieved / frac use the live figure; rocprof_frac recomputes "
+                                                    "the same line from the committed trace"},
                          "views_per_launch": vpl,
                          "traffic": gt[0] if gt else None, "traffic_per_view": gt[0] / vpl if gt else None,
                          "traffic_source": gt[1] if gt else None,
-                         "rocprof": rbusy, "rocprof_stats_avg_launch": prof,
+                         "rocprof_stats_avg_launch": prof,
                          "contended_span": {
                              "ms_per_launch": group_comp["ms_per_launch"],
                              "event_ms_per_launch": group_comp["event_ms_per_launch"],
@@ -788,12 +852,20 @@ def main():
                                        "the others' time: not the kernel's cost); event_ms_per_launch: HIP events "
                                        "around the same launches on the group's stream"},
                          "single_view": single})
-        roof["frame_valu_issue"] = frame_valu
-        if frame_valu:
-            # HBM is the contract's roofline; what binds the frame in flight is VALU issue
-            roof["binding_resource"] = {"name": "VALU issue", "frac": frame_valu["frac"],
-                                        "basis": "frame_valu_issue: the frame's VALU + transcendental instructions "
-                                                 "priced at the measured issue rates, over the frame time"}
+            if region:
+                roof["per_kernel"] = per_kernel_table(region, n, nvis, group_comp["mean_instances"], ntiles, W, H,
+                                                      rec_bytes, vpl)
+        res_fr = frame_resources(args, share, ms_per_step, b_frame, fps)
+        if res_fr:
+            roof["resources"] = res_fr
+            top = max(res_fr["fractions"], key=res_fr["fractions"].get)
+            roof["binding_resource"] = {
+                "name": top, "frac": res_fr["fractions"][top],
+                "basis": "the frame in flight's demand on each resource over the timed region's frame time "
+                         "(resources.fractions); the largest is named",
+                "reading": ("no resource saturates: the frame is latency-bound (dependent record and LDS waits, "
+                            "launch floors and dispatch tails under four group streams)"
+                            if res_fr["fractions"][top] < 0.6 else "saturating")}
 
     cpu = None
     if not args.no_cpu_baseline and world == 1 and g is not None:

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 PMC passes of a bench command, one counter pass per run:
 #   bash tools/pmc.sh TAG PRESET [-- extra bench.py args]
-# PRESET: traffic (FETCH_SIZE, WRITE_SIZE, VALU counts: the roofline's inputs),
+# PRESET: traffic (FETCH_SIZE, WRITE_SIZE, VALU and LDS counts: the roofline's inputs),
 #         stalls (issue / wait / LDS counters of the compositor),
 #         lds (LDS instructions, bank conflicts, LDS-busy cycles).
 # Env GSR_LIB_PATH selects a variant library.  Writes gpurun_out/TAG/pmc_summary.csv
@@ -15,7 +15,7 @@ O=gpurun_out/$TAG
 mkdir -p $O
 B="python bench.py --steps 20 --warmup 5 --no-cpu-baseline $*"  # the driver's region
 case $PRESET in
-    traffic) PASSES=("FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_WAVES") ;;
+    traffic) PASSES=("FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_WAVES SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT") ;;
     stalls) PASSES=("SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS"
                     "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INST_CYCLES_SALU") ;;
     lds) PASSES=("SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_TRANS_F32 SQ_WAVES") ;;
