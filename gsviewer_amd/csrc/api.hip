@@ -188,6 +188,8 @@ struct gsr_context {
     bool views_interleave = true;                 // a group's compositing dispatch class-major over its views
     bool first_major = true;                      // ... every tile's first chunk before any later one
     bool first_major_alone = false;               // the same for a frame finished alone (gsr_render_finish)
+    bool bound_alone = false;                     // every frame alone with t_min > 0 takes the deep form's
+                                                  // first-major order and cross-chunk bound (GSR_BOUND_ALONE)
     bool bin_fused = true;                        // the tile sort's pass 0 fused into the binning (k_bin_scatter)
     bool tail_merge_group = true;                 // a group's multi-chunk tiles folded in the compositing launch
     bool tail_merge_alone = false;                // ... and a frame alone's (else k_merge)
@@ -763,6 +765,7 @@ int gsr_context_create(gsr_context** out) {
     }
     if (std::getenv("GSR_NO_RECT_PAYLOAD")) (*out)->rect_payload = false;
     if (const char* e = std::getenv("GSR_FUSED_CULL")) (*out)->fused_cull = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("GSR_BOUND_ALONE")) (*out)->bound_alone = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_FIRST_MAJOR_ALONE"))
         (*out)->first_major_alone = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_VIEWS_INTERLEAVE")) (*out)->views_interleave = std::strtol(e, nullptr, 10) != 0;
@@ -803,7 +806,8 @@ int gsr_context_knob(const gsr_context* c, const char* name, int64_t* value) {
         {"depth_coarse_alone", c->depth_coarse_alone}, {"chunk", c->chunk}, {"chunk_target", c->chunk_target},
         {"chunk_views", c->chunk_views}, {"tail_merge_alone", c->tail_merge_alone},
         {"tail_merge_group", c->tail_merge_group}, {"first_major", c->first_major},
-        {"first_major_alone", c->first_major_alone}, {"frame_packed", c->last_packed},
+        {"first_major_alone", c->first_major_alone}, {"bound_alone", c->bound_alone},
+        {"frame_packed", c->last_packed},
         {"frame_coarse", c->last_coarse}, {"frame_chunk", c->last_chunk}, {"frame_deep", c->last_deep}};
     for (const auto& k : knobs)
         if (std::strcmp(k.first, name) == 0) {
@@ -1221,7 +1225,7 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         // a frame of many instances (frame_chunk longer than `chunk`): longer chunks, first chunks
         // dispatched first, and later chunks stopped by the earlier ones' transmittance bound
         const uint32_t chunk = frame_chunk(c, n_dup);
-        const bool deep = chunk > c->chunk;
+        const bool deep = chunk > c->chunk || (c->bound_alone && f.t_min > 0.f);
         const size_t max_chunks = (size_t)num_tiles + n_dup / chunk + 1;
         if ((rc = c->chunk_cnt.ensure(chunk_cnt_elems(num_tiles), "chunk_cnt"))) return rc;
         if ((rc = c->chunk_base.ensure((size_t)num_tiles, "chunk_base"))) return rc;
@@ -1259,7 +1263,7 @@ int gsr_render_finish(gsr_context* c, void* stream) {
     c->last_packed = f.packed;
     c->last_coarse = f.coarse;
     c->last_chunk = f.blend == GSR_BLEND_UNORM8 ? 0u : frame_chunk(c, n_dup);
-    c->last_deep = c->last_chunk > c->chunk;
+    c->last_deep = f.blend != GSR_BLEND_UNORM8 && (c->last_chunk > c->chunk || (c->bound_alone && f.t_min > 0.f));
     return GSR_OK;
 }
 
