@@ -188,6 +188,8 @@ struct gsr_context {
     bool views_interleave = true;                 // a group's compositing dispatch class-major over its views
     bool first_major = true;                      // ... every tile's first chunk before any later one
     bool first_major_alone = false;               // the same for a frame finished alone (gsr_render_finish)
+    bool chunk_single = true;                     // a frame alone's chunk descriptors by one block when they fit
+                                                  // (k_chunk_single; GSR_CHUNK_SINGLE=0: count + write launches)
     bool bound_alone = false;                     // every frame alone with t_min > 0 takes the deep form's
                                                   // first-major order and cross-chunk bound (GSR_BOUND_ALONE)
     bool bin_fused = true;                        // the tile sort's pass 0 fused into the binning (k_bin_scatter)
@@ -766,6 +768,7 @@ int gsr_context_create(gsr_context** out) {
     if (std::getenv("GSR_NO_RECT_PAYLOAD")) (*out)->rect_payload = false;
     if (const char* e = std::getenv("GSR_FUSED_CULL")) (*out)->fused_cull = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_BOUND_ALONE")) (*out)->bound_alone = std::strtol(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("GSR_CHUNK_SINGLE")) (*out)->chunk_single = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_FIRST_MAJOR_ALONE"))
         (*out)->first_major_alone = std::strtol(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("GSR_VIEWS_INTERLEAVE")) (*out)->views_interleave = std::strtol(e, nullptr, 10) != 0;
@@ -807,6 +810,7 @@ int gsr_context_knob(const gsr_context* c, const char* name, int64_t* value) {
         {"chunk_views", c->chunk_views}, {"tail_merge_alone", c->tail_merge_alone},
         {"tail_merge_group", c->tail_merge_group}, {"first_major", c->first_major},
         {"first_major_alone", c->first_major_alone}, {"bound_alone", c->bound_alone},
+        {"chunk_single", c->chunk_single},
         {"frame_packed", c->last_packed},
         {"frame_coarse", c->last_coarse}, {"frame_chunk", c->last_chunk}, {"frame_deep", c->last_deep}};
     for (const auto& k : knobs)
@@ -1236,7 +1240,7 @@ int gsr_render_finish(gsr_context* c, void* stream) {
         float4* const tmax = deep ? c->tmax.p : nullptr;  // (after its ensure: it may have moved)
         if ((rc = launch_chunks(ranges, num_tiles, chunk, c->len_classes, c->chunk_cnt.p, c->chunk_base.p, counters + 2,
                                 c->chunk_desc.p, c->chunk_order.p, tmax, s, c->first_major_alone || deep,
-                                f.coarse ? &long_runs : nullptr)))
+                                f.coarse ? &long_runs : nullptr, c->chunk_single ? n_dup / chunk : 0xffffffffu)))
             return rc;
         if ((rc = prof_record(c, slot, EV_RANGES_END_COMPOSITE_START, s))) return rc;
         if ((rc = launch_composite(c->chunk_desc.p, c->chunk_order.p, counters + 2, (uint32_t)max_chunks, c->chunk_cnt.p, c->chunk_base.p,

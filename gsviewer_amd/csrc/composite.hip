@@ -1150,6 +1150,198 @@ __global__ __launch_bounds__(kThreads) void k_chunk_write(const uint2* __restric
                 order, tmax, sh);
 }
 
+// The chunk descriptors of a frame of at most kCsMaxTiles tiles and
+// kCsMaxExtra extra chunks in ONE block (k_chunk_single): the count launch's
+// block totals and the write launch's prefix sums become one block's scans,
+// saving a launch and the totals' round trip through global memory (round 6,
+// 16.8 us of k_chunk_count_long + k_chunk_write at C2).  Same
+// descriptors, slots, dispatch order and class totals as chunk_count +
+// chunk_write.  Thread t takes tiles [t T, t T + T); the extra chunks
+// (j >= 1) are emitted flattened over the block: owner[e] = the tile of extra
+// chunk e, filled by a prefix max over the tiles' first extra chunks.  The
+// coarse order's long runs ride along as blocks 1.. (long_runs.h).
+constexpr int kCsThreads = 1024;
+constexpr int kCsWaves = kCsThreads / 64;
+constexpr uint32_t kCsMaxTiles = 8192;    // 1080p: 8160
+constexpr uint32_t kCsMaxExtra = 16384;   // extra chunks (fb, pp, excl in 16 bits: < 2^16 with the tiles)
+constexpr int kCsPer = (int)(kCsMaxTiles / kCsThreads);  // tiles per thread
+constexpr int kCsClasses = 8;                            // length classes it handles (the default; more: two launches)
+constexpr int kCsVals = 1 + kCsClasses;                  // scanned per thread: extra, full, partials of each class
+
+struct ChunkSingleLds {
+    uint2 info[kCsMaxTiles];            // per tile: excl extra | full before << 16, partial dispatch position
+    uint16_t owner[kCsMaxExtra];        // extra chunk -> its tile (after the prefix max)
+    uint32_t red[kCsVals][kCsWaves];    // per-wave sums of the scanned values
+    uint32_t seg[kCsWaves];             // per-wave maxima of the owner segments
+};
+union ChunkSingleShared {
+    ChunkSingleLds c;
+    TdsLds t;
+};
+
+// chunks_of, first_full_of and first_class_of of one tile with two divisions
+// (the single block keeps each tile's three terms in registers between its
+// counting and its emission)
+__device__ __forceinline__ void tile_chunk_terms(uint2 r, uint32_t chunk, uint32_t classes, bool first_major,
+                                                 uint32_t& cnt, uint32_t& f, uint32_t& pc) {
+    const uint32_t len = r.y - r.x;
+    const uint32_t q = len / chunk, rem = len - q * chunk;
+    cnt = len == 0 ? 1u : q + (rem != 0u ? 1u : 0u);
+    f = first_major ? (len >= chunk ? 1u : 0u) : q;
+    pc = (len != 0 && rem == 0) ? 0u : (classes - 1u) - rem * (classes - 1u) / chunk;
+    if (first_major && len >= chunk) pc = 0u;
+}
+
+__device__ __forceinline__ void chunk_single(const uint2* __restrict__ ranges, int num_tiles, uint32_t chunk, uint32_t classes,
+                             bool first_major, uint32_t* __restrict__ chunk_cnt, uint32_t* __restrict__ chunk_base,
+                             uint32_t* __restrict__ n_extra_dev, uint4* __restrict__ desc,
+                             uint32_t* __restrict__ order, float4* __restrict__ tmax, uint32_t* __restrict__ cls_tot,
+                             ChunkSingleLds& sh) {
+    const uint32_t tid = threadIdx.x, w = tid >> 6, lane = __lane_id();
+    const uint32_t nt = (uint32_t)num_tiles;
+    const uint32_t per = (nt + kCsThreads - 1) / kCsThreads;
+    const uint32_t t0 = tid * per;
+    uint2 r[kCsPer];
+#pragma unroll
+    for (int i = 0; i < kCsPer; ++i) r[i] = ((uint32_t)i < per && t0 + i < nt) ? ranges[t0 + i] : make_uint2(0u, 0u);
+    // this thread's sums: [0] extra chunks, [1] full (dispatch sense), [1 + k] partials of class k
+    uint32_t v[kCsVals];
+    uint32_t tc[kCsPer], tfp[kCsPer];  // per tile: chunks; full | partial class << 24
+#pragma unroll
+    for (int k = 0; k < kCsVals; ++k) v[k] = 0u;
+#pragma unroll
+    for (int i = 0; i < kCsPer; ++i) {
+        tc[i] = 0u;
+        tfp[i] = 0u;
+        if ((uint32_t)i < per && t0 + i < nt) {
+            uint32_t cnt, f, pc;
+            tile_chunk_terms(r[i], chunk, classes, first_major, cnt, f, pc);
+            tc[i] = cnt;
+            tfp[i] = f | (pc << 24);
+            v[0] += cnt - 1u;
+            v[1] += f;
+#pragma unroll
+            for (int k = 1; k < kCsClasses; ++k) v[1 + k] += (pc == (uint32_t)k) ? 1u : 0u;
+        }
+    }
+    // one block scan of every value: exclusive prefixes in v, totals in tot
+    uint32_t tot[kCsVals];
+#pragma unroll
+    for (int k = 0; k < kCsVals; ++k) {
+        const uint32_t inc = wave_inclusive_scan(v[k]);
+        if (lane == 63) sh.red[k][w] = inc;
+        v[k] = inc - v[k];
+    }
+    __syncthreads();
+    // lane q < kCsWaves holds wave q's sum; a wave scan over those lanes gives the waves before w
+#pragma unroll
+    for (int k = 0; k < kCsVals; ++k) {
+        const uint32_t x = lane < (uint32_t)kCsWaves ? sh.red[k][lane] : 0u;
+        const uint32_t inc = wave_inclusive_scan(x);
+        const uint32_t before = w > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)inc, (int)w - 1) : 0u;
+        v[k] += before;
+        tot[k] = (uint32_t)__builtin_amdgcn_readlane((int)inc, kCsWaves - 1);
+    }
+    // class bases (first dispatch position of each class): full chunks, then the partial classes in order
+    uint32_t base[kCsClasses];
+    {
+        uint32_t run = 0;
+#pragma unroll
+        for (int k = 0; k < kCsClasses; ++k) {
+            base[k] = run;
+            run += (uint32_t)k < classes ? tot[1 + k] : 0u;  // (base[0] = 0: tot[1] full chunks, then class 1 ...)
+        }
+    }
+    if (tid == 0) {
+        *n_extra_dev = tot[0];
+#pragma unroll
+        for (int k = 0; k < kCsClasses; ++k)  // (unrolled: a runtime index would put tot in scratch)
+            if ((uint32_t)k < classes) cls_tot[k] = tot[1 + k];
+        cls_tot[classes] = tot[0];  // the later chunks (first-major order)
+    }
+    for (uint32_t e = tid; e < tot[0]; e += kCsThreads) sh.owner[e] = 0;
+    auto emit = [&](uint32_t tt, uint2 rr, uint32_t c, uint32_t f, uint32_t slot, uint32_t fb, uint32_t pp, uint32_t j) {
+        const uint32_t b = rr.x + j * chunk;
+        desc[slot] = make_uint4(tt, b, min(rr.y, b + chunk), (c << 16) | j);
+        order[first_major && j > 0 ? slot : (j < f ? fb + j : pp)] = slot;
+        if (tmax && c > 1) tmax[slot] = make_float4(1.f, 1.f, 1.f, 1.f);  // nothing composited yet
+    };
+    __syncthreads();  // (owner cleared before any tile marks its first extra chunk)
+    // chunk 0 of every tile, the tiles' terms for the extra chunks, their first extra chunk's owner
+    uint32_t ex = v[0], fu = v[1];
+#pragma unroll
+    for (int i = 0; i < kCsPer; ++i) {
+        const uint32_t t = t0 + (uint32_t)i;
+        if ((uint32_t)i < per && t < nt) {
+            const uint32_t cnt = tc[i], f = tfp[i] & 0xffffffu, pc = tfp[i] >> 24;
+            uint32_t pp = 0;
+#pragma unroll
+            for (int k = 1; k < kCsClasses; ++k)
+                if (pc == (uint32_t)k) {
+                    pp = base[k] + v[1 + k];
+                    v[1 + k] += 1u;
+                }
+            chunk_cnt[t] = cnt;
+            chunk_base[t] = nt + ex;
+            emit(t, r[i], cnt, f, t, fu, pp, 0u);
+            sh.info[t] = make_uint2(ex | (fu << 16), pp);
+            if (cnt > 1) sh.owner[ex] = (uint16_t)t;
+            ex += cnt - 1u;
+            fu += f;
+        }
+    }
+    __syncthreads();
+    // owner[e] = the last marked tile at or before e (tiles mark in increasing order): a prefix max,
+    // each thread over a contiguous segment
+    const uint32_t E = tot[0];
+    const uint32_t sp = (E + kCsThreads - 1) / kCsThreads;
+    const uint32_t e0 = min(E, tid * sp), e1 = min(E, e0 + sp);
+    uint32_t m = 0;
+    for (uint32_t e = e0; e < e1; ++e) m = max(m, (uint32_t)sh.owner[e]);
+    const uint32_t wm = wave_reduce_max(m);  // (a wave's segments are consecutive)
+    uint32_t incl_m = m;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t x = __shfl_up(incl_m, o, 64);
+        if (lane >= (uint32_t)o) incl_m = max(incl_m, x);
+    }
+    if (lane == 63) sh.seg[w] = wm;
+    __syncthreads();
+    uint32_t run = __shfl_up(incl_m, 1, 64);
+    if (lane == 0) run = 0;
+    for (uint32_t q = 0; q < w; ++q) run = max(run, sh.seg[q]);
+    for (uint32_t e = e0; e < e1; ++e) {
+        run = max(run, (uint32_t)sh.owner[e]);
+        sh.owner[e] = (uint16_t)run;
+    }
+    __syncthreads();
+    for (uint32_t e = tid; e < E; e += kCsThreads) {
+        const uint32_t t = sh.owner[e];
+        const uint2 in = sh.info[t];
+        const uint2 rr = ranges[t];
+        uint32_t cnt, f, pc;
+        tile_chunk_terms(rr, chunk, classes, first_major, cnt, f, pc);
+        const uint32_t j = e - (in.x & 0xffffu) + 1u;
+        emit(t, rr, cnt, f, nt + e, in.x >> 16, in.y, j);
+    }
+}
+
+__global__ __launch_bounds__(kCsThreads) void k_chunk_single(const uint2* __restrict__ ranges, int num_tiles,
+                                                             uint32_t chunk, uint32_t classes, uint32_t first_major,
+                                                             uint32_t* __restrict__ chunk_cnt,
+                                                             uint32_t* __restrict__ chunk_base,
+                                                             uint32_t* __restrict__ n_extra_dev,
+                                                             uint4* __restrict__ desc, uint32_t* __restrict__ order,
+                                                             float4* __restrict__ tmax, uint32_t* __restrict__ cls_tot,
+                                                             LongRunArgs la) {
+    __shared__ ChunkSingleShared S;
+    if (blockIdx.x == 0)
+        chunk_single(ranges, num_tiles, chunk, classes, first_major != 0, chunk_cnt, chunk_base, n_extra_dev, desc,
+                     order, tmax, cls_tot, S.c);
+    else
+        long_runs_block(la, S.t, blockIdx.x - 1, gridDim.x - 1);
+}
+
 struct ChunkView {
     const uint2* ranges;
     uint32_t* chunk_cnt;  // block totals after its num_tiles entries
@@ -2328,11 +2520,24 @@ const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uin
 
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
-                  hipStream_t s, bool first_major, const LongRuns* long_runs) {
+                  hipStream_t s, bool first_major, const LongRuns* long_runs, uint32_t max_extra) {
     if (classes < 2 || classes > (uint32_t)kMaxLenClasses) return set_error(GSR_ERR_INVALID, "chunk length classes");
     const unsigned g = (unsigned)((num_tiles + kThreads - 1) / kThreads);
     // the per-block totals live in chunk_cnt past its num_tiles entries
     uint32_t* tot = chunk_cnt + num_tiles;
+    // one block for the whole frame when it fits (k_chunk_single); the long runs as its blocks 1..
+    if ((uint32_t)num_tiles <= kCsMaxTiles && max_extra <= kCsMaxExtra &&
+        classes <= (uint32_t)kCsClasses) {
+        const bool runs = long_runs && long_runs->n_dup > 0 && long_runs->fix.coarse;
+        LongRunArgs la{};
+        if (runs)
+            if (int rc = long_run_args(long_runs->tile_keys, long_runs->n_dup, ranges, long_runs->fix, la)) return rc;
+        k_chunk_single<<<1 + (runs ? kLongGrid : 0), kCsThreads, 0, s>>>(
+            ranges, num_tiles, chunk, classes, first_major ? 1u : 0u, chunk_cnt, chunk_base, n_extra_dev, desc, order,
+            tmax, const_cast<uint32_t*>(chunk_class_totals(chunk_cnt, num_tiles, classes)), la);
+        GSR_LAUNCH_CHECK("chunk_single");
+        return GSR_OK;
+    }
     if (long_runs && long_runs->n_dup > 0 && long_runs->fix.coarse) {
         LongRunArgs la;
         if (int rc = long_run_args(long_runs->tile_keys, long_runs->n_dup, ranges, long_runs->fix, la)) return rc;

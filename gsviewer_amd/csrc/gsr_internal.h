@@ -489,7 +489,8 @@ struct LongRuns {
 };
 int launch_chunks(const uint2* ranges, int num_tiles, uint32_t chunk, uint32_t classes, uint32_t* chunk_cnt,
                   uint32_t* chunk_base, uint32_t* n_extra_dev, uint4* desc, uint32_t* order, float4* tmax,
-                  hipStream_t s, bool first_major = false, const LongRuns* long_runs = nullptr);
+                  hipStream_t s, bool first_major = false, const LongRuns* long_runs = nullptr,
+                  uint32_t max_extra = 0xffffffffu);  // (an upper bound of the extra chunks: n_dup / chunk)
 const uint32_t* chunk_class_totals(const uint32_t* chunk_cnt, int num_tiles, uint32_t classes);
 int launch_composite(const uint4* desc, const uint32_t* order, const uint32_t* n_chunks_dev, uint32_t max_chunks,
                      const uint32_t* chunk_cnt, const uint32_t* chunk_base, uint32_t* sat,

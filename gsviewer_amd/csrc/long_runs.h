@@ -91,7 +91,7 @@ __device__ __forceinline__ uint32_t tds_passes(uint32_t B, bool even) {
 
 // ---------------------------------------------------------------- wave path
 // One wave sorts the list [b, b + L), 2 <= L <= kTdsCapWave.
-__device__ void tds_wave(const uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t b, uint32_t L,
+__device__ __forceinline__ void tds_wave(const uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t b, uint32_t L,
                          TdsWaveLds& W) {
     const uint32_t lane = __lane_id();
     const uint32_t nr = (L + 63u) / 64u;
@@ -263,7 +263,7 @@ __device__ __forceinline__ void tds_rank_block(const uint32_t (&k)[kI], uint32_t
 }
 
 // One workgroup sorts [b, b + L), kTdsCapWave < L <= kTdsCapBlock, in registers.
-__device__ void tds_block(const uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t b, uint32_t L,
+__device__ __forceinline__ void tds_block(const uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t b, uint32_t L,
                           TdsLds& S) {
     const uint32_t t = threadIdx.x, w = t >> 6, lane = __lane_id();
     // wave w's span: items [w * span, (w + 1) * span), rounds of 64
@@ -331,7 +331,7 @@ constexpr uint32_t kTdsSub = kTdsCapBlock / 2;
 constexpr int kSweep = 8;  // loads in flight per thread in the global path's sweeps
 constexpr int kTdsSubItems = (int)kTdsSub / kTdsThreads;
 
-__device__ void tds_global(uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t* __restrict__ keys_alt,
+__device__ __forceinline__ void tds_global(uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, uint32_t* __restrict__ keys_alt,
                            uint32_t* __restrict__ vals_alt, uint32_t b, uint32_t L, TdsLds& S) {
     const uint32_t t = threadIdx.x, w = t >> 6, lane = __lane_id();
     uint32_t lo = 0xffffffffu, hi = 0u;
@@ -449,7 +449,7 @@ struct LongRunArgs {
 
 // The end of the run starting at b (tile `tile`, coarse key cv), at most hi:
 // 64 probes a round, the first failing one narrows the bracket 64-fold.
-__device__ uint32_t run_end(const LongRunArgs& a, uint32_t b, uint32_t hi, uint32_t tile, uint32_t cv, uint32_t kmin,
+__device__ __forceinline__ uint32_t run_end(const LongRunArgs& a, uint32_t b, uint32_t hi, uint32_t tile, uint32_t cv, uint32_t kmin,
                             uint32_t s0) {
     const uint32_t lane = __lane_id();
     uint32_t lo = b, up = hi;  // p(lo) holds; every position >= up fails (or is past the tile)
@@ -469,7 +469,7 @@ __device__ uint32_t run_end(const LongRunArgs& a, uint32_t b, uint32_t hi, uint3
 }
 
 // The runs of block `bid` of G (S: the block's LDS; every thread of the block calls it).
-__device__ void long_runs_block(const LongRunArgs& a, TdsLds& S, uint32_t bid, uint32_t G) {
+__device__ __forceinline__ void long_runs_block(const LongRunArgs& a, TdsLds& S, uint32_t bid, uint32_t G) {
     const uint32_t n_long = *a.count;
     if (bid >= n_long) return;
     const uint32_t w = threadIdx.x >> 6, lane = __lane_id();

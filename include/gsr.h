@@ -330,7 +330,9 @@ int64_t gsr_debug_copy(const gsr_context* ctx, int32_t what, void* dst_dev, int6
  * "bin_fused", "depth_coarse_alone", "chunk", "chunk_target", "chunk_views",
  * "tail_merge_alone", "tail_merge_group", "first_major", "first_major_alone",
  * "bound_alone" (GSR_BOUND_ALONE: every frame alone with t_min > 0 takes the deep
- * form's first-major order and cross-chunk bound; measured slower at C2).
+ * form's first-major order and cross-chunk bound; measured slower at C2),
+ * "chunk_single" (GSR_CHUNK_SINGLE=0: a frame alone's chunk descriptors by the
+ * count + write launches instead of one block).
  * Last frame: "frame_packed" (its depth sort carried the packed tile rects),
  * "frame_coarse" (its depth sort's coarse bits, 0 = exact), "frame_chunk" (its
  * compositing chunk length; 0 for the RGBA8 framebuffer), "frame_deep" (1: the

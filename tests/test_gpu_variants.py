@@ -11,7 +11,10 @@
 * GSR_FUSED_CULL (default 1): culling inside the preprocess, uncompacted
   slots, culled keys dropped by the depth sort's first pass, against k_cull +
   the compaction scan + k_preprocess (tests/helpers.grab_debug maps the
-  uncompacted slots to the compacted ones by rank).
+  uncompacted slots to the compacted ones by rank);
+* GSR_CHUNK_SINGLE (default 1): a frame alone's chunk descriptors, dispatch
+  order and class totals written by one block (k_chunk_single) against the
+  count + write launches.
 
 Images, records, depth order, tile lists and tile ranges must be bit-identical, on a frame rendered alone (gsr_render) and on a group of
 views (gsr_render_finish_views), for frame sizes whose tile ids take one
@@ -26,7 +29,7 @@ from helpers import batched_frames, gpu_frame
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [{}, {"GSR_BIN_FUSED": "0"}, {"GSR_TAIL_MERGE": "0", "GSR_TAIL_MERGE_ALONE": "1"},
-            {"GSR_FUSED_CULL": "0"}]
+            {"GSR_FUSED_CULL": "0"}, {"GSR_CHUNK_SINGLE": "0"}]
 
 
 def _settings(**kw):
@@ -35,7 +38,8 @@ def _settings(**kw):
 
 
 def _frames(monkeypatch, env, g, scene, cams):
-    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE", "GSR_FUSED_CULL", "GSR_DEPTH_COARSE"):
+    for k in ("GSR_BIN_FUSED", "GSR_TAIL_MERGE", "GSR_TAIL_MERGE_ALONE", "GSR_FUSED_CULL", "GSR_DEPTH_COARSE",
+              "GSR_CHUNK_SINGLE"):
         monkeypatch.delenv(k, raising=False)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -86,3 +90,19 @@ def test_group_frames_repeatable(gpu):
         for v in range(3):
             np.testing.assert_array_equal(got[v]["image"], ref[v], err_msg=f"repeat {it} view {v}")
     scene.close()
+
+
+def test_chunk_single_deep_form(gpu, monkeypatch):
+    """The deep form's chunking (longer chunks, first chunks dispatched
+    first, published maxima initialised) by one block and by the count +
+    write launches: identical frames at t_min = 0 (the bound then never
+    stops a chunk, so the images depend on the descriptors only)."""
+    g = garden_standin(300_000, seed=1, sh_degree=1)
+    cam = Camera(720, 1280)
+    monkeypatch.setenv("GSR_CHUNK_TARGET", "256")  # D / 256 chunks: longer than 192, the deep form
+    got = {}
+    for single in ("1", "0"):
+        monkeypatch.setenv("GSR_CHUNK_SINGLE", single)
+        got[single] = gpu_frame(g, cam, _settings(t_min=0.0), with_debug=True)
+    for key in ("tile_list", "ranges", "image"):
+        np.testing.assert_array_equal(got["1"][key], got["0"][key], err_msg=key)
