@@ -188,7 +188,7 @@ struct gsr_context {
     bool views_interleave = true;                 // a group's compositing dispatch class-major over its views
     bool first_major = true;                      // ... every tile's first chunk before any later one
     bool first_major_alone = false;               // the same for a frame finished alone (gsr_render_finish)
-    bool chunk_single = true;                     // a frame alone's chunk descriptors by one block when they fit
+    bool chunk_single = false;                    // a frame alone's chunk descriptors by one block when they fit
                                                   // (k_chunk_single; GSR_CHUNK_SINGLE=0: count + write launches)
     bool bound_alone = false;                     // every frame alone with t_min > 0 takes the deep form's
                                                   // first-major order and cross-chunk bound (GSR_BOUND_ALONE)
