@@ -20,6 +20,10 @@
 #include "gsr_internal.h"
 #include "long_runs.h"
 
+#ifndef GSR_COMP_PIPE
+#define GSR_COMP_PIPE 0  // (experiment: software-pipelined record reads in the compositor, composite_chunk)
+#endif
+
 namespace gsr {
 namespace {
 
@@ -1649,13 +1653,28 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         // by VALU and SALU issue: profiles/r4_s16)
         uint64_t todo = (sb[0] | sb[1] | sb[2] | sb[3]) & (nb >= 64 ? ~0ull : ((1ull << nb) - 1ull));
         if (todo) {
+#if GSR_COMP_PIPE
+        // experiment: the next record's three broadcast reads issued before this
+        // record's arithmetic, so they are not waited on one record at a time (+12 VGPRs)
+        int j = (int)__builtin_ctzll(todo);
+        float4 n0 = my[j * 3 + 0], n1 = my[j * 3 + 1], n2 = my[j * 3 + 2];
+#endif
 #pragma unroll 1
         do {
+#if GSR_COMP_PIPE
+            const float4 q0 = n0, q1 = n1, q2 = n2;
+            todo &= ~(1ull << j);
+            const int jn = todo ? (int)__builtin_ctzll(todo) : j;
+            n0 = my[jn * 3 + 0];
+            n1 = my[jn * 3 + 1];
+            n2 = my[jn * 3 + 2];
+#else
             const int j = (int)__builtin_ctzll(todo);
             todo &= ~(1ull << j);
             const float4 q0 = my[j * 3 + 0];  // cx cy opacity coverage
             const float4 q1 = my[j * 3 + 1];  // qa qb qc mid
             const float4 q2 = my[j * 3 + 2];  // r g b kT
+#endif
 #ifdef GSR_COMP_STATS
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -1779,6 +1798,9 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                 rg[k] = __builtin_elementwise_fma(crg, ww, rg[k]);
                 bt[k] = __builtin_elementwise_fma(cbt, ww, bt[k]);
             }
+#if GSR_COMP_PIPE
+            j = jn;
+#endif
         } while (todo);
         }
         if (t_min > 0.f) {

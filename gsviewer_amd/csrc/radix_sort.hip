@@ -56,6 +56,11 @@ constexpr size_t kBigDepthN = (size_t)1 << 21;
 #define GSR_TILE_R 8
 #endif
 constexpr int kRTile = GSR_TILE_R;
+// ... and for tile sorts of more than kBigTileN instances (C3's 10.6 M): 4096-item tiles like the big depth sorts
+#ifndef GSR_BIG_TILE_N
+#define GSR_BIG_TILE_N 0xffffffffu
+#endif
+constexpr size_t kBigTileN = GSR_BIG_TILE_N;
 constexpr int kRMin = kRWide < kRDepth ? (kRWide < kRTile ? kRWide : kRTile) : (kRDepth < kRTile ? kRDepth : kRTile);
 constexpr int kMinTileItems = kThreads * kRMin;  // sizes the digit matrix for any R
 
@@ -531,6 +536,8 @@ int radix_sort_pairs_views(RadixViewArgs* views, int k, bool identity_vals, size
     if ((bits + passes - 1) / passes <= 8) {
         if (views[0].key_range && n > kBigDepthN)
             return sort_passes_views<kRDepthBig, 8>(views, k, identity_vals, n, bits, passes, s, first_pass);
+        if (!views[0].key_range && n > kBigTileN)
+            return sort_passes_views<kRDepthBig, 8>(views, k, identity_vals, n, bits, passes, s, first_pass);
         return views[0].key_range
                    ? sort_passes_views<kRDepth, 8>(views, k, identity_vals, n, bits, passes, s, first_pass)
                    : sort_passes_views<kRTile, 8>(views, k, identity_vals, n, bits, passes, s, first_pass);
@@ -561,6 +568,10 @@ int radix_sort_pairs(uint32_t** keys_io, uint32_t** vals_io, uint32_t** keys_alt
             return sort_passes<kRDepth, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
                                      key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first, coarse,
                                      keys_last);
+        if (n > kBigTileN)
+            return sort_passes<kRDepthBig, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits,
+                                              passes, key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass,
+                                              drop_first, coarse, keys_last);
         return sort_passes<kRTile, 8>(keys_io, vals_io, keys_alt, vals_alt, identity_vals, n, n_dev, bits, passes,
                                   key_range, tmp, totals, s, rect_in, pay_io, pay_alt, first_pass, drop_first, coarse,
                                      keys_last);
