@@ -151,6 +151,12 @@ constexpr int kDepthPassesAlone = 3;
 // frame's global depth order (GSR_DEBUG_DEPTH_ORDER) is the coarse one;
 // gsr_sort_depth stays exact.
 constexpr uint32_t kDepthCoarseAlone = 16;
+// ... for scenes of at most kCoarseMaxN Gaussians.  Above it the run repair and the keys the binning and the tile
+// sort carry cost more (they scale with the instances) than the two passes save, and a frame alone sorts exactly in
+// kDepthPassesBigAlone passes of <= 8 bits (round 6, profiles/r6_s11: C3 alone 1.244 -> 1.195 ms; 3 passes of <= 11
+// bits: 1.259; c2h and C5, 1M Gaussians, within 1 % either way; C2 coarse 0.309 against 0.327 exact, r6_s12)
+constexpr size_t kCoarseMaxN = (size_t)1 << 21;
+constexpr int kDepthPassesBigAlone = 4;
 constexpr uint32_t kDepthCoarseMax = 16;  // 2 passes of <= 8 bits: the last pass's keys are the carried ones
 
 struct gsr_context {
@@ -503,14 +509,17 @@ int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const 
     const uint2* rect_in = f.packed ? c->trect.p : nullptr;
     uint32_t** pay_io = f.packed ? &f.pa : nullptr;
     uint32_t** pay_alt = f.packed ? &f.pb : nullptr;
-    // a frame alone with the fused binning (which carries the sorted keys to the repair): the coarse order
-    if (c->depth_passes_now && c->depth_coarse_alone && c->bin_fused) {
+    // a frame alone with the fused binning (which carries the sorted keys to the repair): the coarse order,
+    // for scenes of at most kCoarseMaxN Gaussians; larger ones sort exactly in 4 passes of <= 8 bits
+    if (c->depth_passes_now && c->depth_coarse_alone && c->bin_fused && f.n <= kCoarseMaxN) {
         f.coarse = c->depth_coarse_alone;
         return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, (int)f.coarse, 2, key_range,
                                 c->radix_tmp.p, totals, s, rect_in, pay_io, pay_alt, 0, c->fused_cull, f.coarse);
     }
-    return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32,
-                            c->depth_passes_now ? c->depth_passes_now : kDepthPasses, key_range,
+    const int passes = !c->depth_passes_now                                     ? kDepthPasses
+                       : (c->depth_coarse_alone && f.n > kCoarseMaxN)           ? kDepthPassesBigAlone
+                                                                                : c->depth_passes_now;
+    return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32, passes, key_range,
                             c->radix_tmp.p, totals, s, rect_in, pay_io, pay_alt, 0, c->fused_cull);
 }
 

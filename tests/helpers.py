@@ -105,7 +105,9 @@ def gpu_frame(g, cam, settings, with_debug=False, radii=False):
     settings.out_layout = 1
     render_into(ctx, scene, camera_from(cam), settings, out, rad)
     torch.cuda.synchronize()
-    res = {"image": out.cpu().numpy(), "stats": ctx.stats(), "depth_coarse": depth_coarse_bits("alone")}
+    # the coarse bits this frame's depth sort took (0: exact; scenes over 2M Gaussians sort exactly, api.hip
+    # kCoarseMaxN)
+    res = {"image": out.cpu().numpy(), "stats": ctx.stats(), "depth_coarse": ctx.knob("frame_coarse")}
     if radii:
         res["radii"] = rad.cpu().numpy()
     if with_debug:
