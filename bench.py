@@ -514,6 +514,9 @@ def main():
     ap.add_argument("--lookahead", type=int, default=None,
                     help="with --share > 1: at most this many groups begun and not yet finished (default: all "
                          "groups; a group is finished when it is begun again or drained)")
+    ap.add_argument("--priorities", default=None,
+                    help="experiment: comma-separated HIP stream priorities of the group streams (lower = "
+                         "higher priority; torch.cuda.Stream.priority_range()), cycled over the streams")
     ap.add_argument("--host-threads", action="store_true",
                     help="with --share > 1: one host thread per group drives its stream (parallel enqueue)")
     ap.add_argument("--no-profile", action="store_true", help="do not record per-stage HIP events")
@@ -616,7 +619,12 @@ def main():
     ctxs = [HipContext() for _ in range(K)]
     for c in ctxs:  # workspace sized up front: no device allocation inside any frame
         c.reserve(n, W, H)
-    streams = [torch.cuda.Stream(device=dev) for _ in range(K)]
+    if args.priorities:
+        pri = [int(x) for x in args.priorities.split(",")]
+        print(f"bench: stream priority range {torch.cuda.Stream.priority_range()}, using {pri}", file=sys.stderr)
+        streams = [torch.cuda.Stream(device=dev, priority=pri[i % len(pri)]) for i in range(K)]
+    else:
+        streams = [torch.cuda.Stream(device=dev) for _ in range(K)]
     outs = [torch.empty((3, H, W), dtype=torch.float32, device=dev) for _ in range(K)]
     cams = [cam] + [view_of(rank + world * j, H, W) for j in range(1, K)]
     camcs = [camera_from(c) for c in cams]
