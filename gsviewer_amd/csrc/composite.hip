@@ -1501,7 +1501,8 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                                                 const SplatRec* __restrict__ recs, const CompositeArgs& a,
                                                 float* __restrict__ out, float4* __restrict__ partial,
                                                 uint32_t* __restrict__ sat, float4* __restrict__ tmax,
-                                                const uint32_t* __restrict__ chunk_base) {
+                                                const uint32_t* __restrict__ chunk_base,
+                                                uint32_t* __restrict__ trace_evals = nullptr) {
     const int tile = (int)d.x;
     const uint32_t begin = d.y, end = d.z;
     const uint32_t nchunks = d.w >> 16;
@@ -1603,6 +1604,9 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
 #ifdef GSR_COMP_STATS
     uint32_t st_evals = 0, st_wasted = 0, st_records = 0, st_empty = 0;
 #endif
+#ifdef GSR_COMP_TRACE
+    uint32_t tr_evals = 0;  // (record, slice) evaluations of this chunk (tools/comp_trace.py)
+#endif
     for (uint32_t b = begin; b < end && live; b += kBatch) {
         __builtin_amdgcn_wave_barrier();
         // sb[k] bit j: record j of the batch touches 16x4 slice k (and the
@@ -1683,6 +1687,10 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
                     if (!__any(bt[k].y >= t_min)) st_wasted += 1;
                 }
             st_records += 1;
+#endif
+#ifdef GSR_COMP_TRACE
+#pragma unroll
+            for (int k = 0; k < 4; ++k) tr_evals += (uint32_t)((sb[k] >> j) & 1ull);
 #endif
 #ifdef GSR_COMP_DENSE
             if (FRAG == kFragGauss) {
@@ -1842,6 +1850,9 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
         }
     }
 
+#ifdef GSR_COMP_TRACE
+    if (trace_evals) *trace_evals = tr_evals;
+#endif
 #ifdef GSR_COMP_STATS
     if (lane == 0) {
         atomicAdd(&g_comp_stats[0], (unsigned long long)st_evals);
@@ -2051,15 +2062,19 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const uint4 d = desc[slot];
-    composite_chunk<FRAG, kBound>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax, chunk_base);
 #ifdef GSR_COMP_TRACE
+    uint32_t evals = 0;
+    composite_chunk<FRAG, kBound>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax, chunk_base, &evals);
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if (__lane_id() == 0 && slot < kTraceMax) {
         const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));     // HW_ID
         const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));   // XCC_ID
-        g_comp_trace[2 * slot] = make_uint4(slot, hw, d.z - d.y, xcc);
+        // .w: the XCC in bits 0-3, the chunk's (record, slice) evaluations above
+        g_comp_trace[2 * slot] = make_uint4(slot, hw, d.z - d.y, (xcc & 15u) | (evals << 4));
         g_comp_trace[2 * slot + 1] = make_uint4((uint32_t)t0, (uint32_t)t1, (uint32_t)r0, (uint32_t)r1);
     }
+#else
+    composite_chunk<FRAG, kBound>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax, chunk_base);
 #endif
 }
 

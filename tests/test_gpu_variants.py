@@ -12,7 +12,7 @@
   slots, culled keys dropped by the depth sort's first pass, against k_cull +
   the compaction scan + k_preprocess (tests/helpers.grab_debug maps the
   uncompacted slots to the compacted ones by rank);
-* GSR_CHUNK_SINGLE (default 1): a frame alone's chunk descriptors, dispatch
+* GSR_CHUNK_SINGLE (default 0): a frame alone's chunk descriptors, dispatch
   order and class totals written by one block (k_chunk_single) against the
   count + write launches.
 
@@ -29,7 +29,7 @@ from helpers import batched_frames, gpu_frame
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [{}, {"GSR_BIN_FUSED": "0"}, {"GSR_TAIL_MERGE": "0", "GSR_TAIL_MERGE_ALONE": "1"},
-            {"GSR_FUSED_CULL": "0"}, {"GSR_CHUNK_SINGLE": "0"}]
+            {"GSR_FUSED_CULL": "0"}, {"GSR_CHUNK_SINGLE": "1"}]
 
 
 def _settings(**kw):
@@ -106,3 +106,4 @@ def test_chunk_single_deep_form(gpu, monkeypatch):
         got[single] = gpu_frame(g, cam, _settings(t_min=0.0), with_debug=True)
     for key in ("tile_list", "ranges", "image"):
         np.testing.assert_array_equal(got["1"][key], got["0"][key], err_msg=key)
+

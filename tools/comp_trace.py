@@ -67,7 +67,8 @@ def main():
     slot = tr[:, 0, 0]
     live = used & (slot == np.arange(got))
     tr = tr[live]
-    hw, work, xcc = tr[:, 0, 1], tr[:, 0, 2].astype(np.int64), tr[:, 0, 3]
+    hw, work = tr[:, 0, 1], tr[:, 0, 2].astype(np.int64)
+    xcc, evals = tr[:, 0, 3] & 15, (tr[:, 0, 3] >> 4).astype(np.int64)  # (record, slice) evaluations
     t0 = tr[:, 1, 0].astype(np.int64)
     t1 = tr[:, 1, 1].astype(np.int64)
     r0 = tr[:, 1, 2].astype(np.int64)
@@ -108,11 +109,32 @@ def main():
         xcc_finish_us={int(x): float(e_us[xcc == x].max()) for x in np.unique(xcc)},
         us_per_record_median=float(np.median(dur_us[work > 0] / work[work > 0])),
         empty_wave_us_median=float(np.median(dur_us[work == 0])) if (work == 0).any() else None,
-        total_wave_us=float(dur_us.sum()), total_work=int(work.sum()),
+        total_wave_us=float(dur_us.sum()), total_work=int(work.sum()), total_evals=int(evals.sum()),
+        evals_quantiles={str(p): float(np.quantile(evals, p)) for p in (0.1, 0.5, 0.9, 0.99, 1.0)},
+        # how much of a wave's duration its instance count and its slice evaluations explain
+        corr_dur_instances=float(np.corrcoef(dur_us, work)[0, 1]) if len(tr) > 2 else None,
+        corr_dur_evals=float(np.corrcoef(dur_us, evals)[0, 1]) if len(tr) > 2 else None,
+        us_per_eval_median=float(np.median(dur_us[evals > 0] / evals[evals > 0])) if (evals > 0).any() else None,
     )
+    # the waves that retire last (after 90 % of them): what they carry against the rest
+    late = e_us >= q(0.9)
+    full = work == work.max()
+    res["late_waves"] = dict(
+        n=int(late.sum()), start_us_median=float(np.median(s_us[late])), dur_us_median=float(np.median(dur_us[late])),
+        evals_median=float(np.median(evals[late])), instances_median=float(np.median(work[late])))
+    res["full_chunks"] = dict(
+        n=int(full.sum()), instances=int(work.max()),
+        dur_us_quantiles={str(p): float(np.quantile(dur_us[full], p)) for p in (0.1, 0.5, 0.9, 1.0)},
+        evals_quantiles={str(p): float(np.quantile(evals[full], p)) for p in (0.1, 0.5, 0.9, 1.0)},
+        corr_dur_evals=float(np.corrcoef(dur_us[full], evals[full])[0, 1]) if full.sum() > 2 else None)
+    # a wave's duration fitted as a + b * evals + c * instances (least squares): the residual is what neither explains
+    A = np.stack([np.ones(len(tr)), evals, work], 1).astype(np.float64)
+    coef, *_ = np.linalg.lstsq(A, dur_us, rcond=None)
+    res["fit_us"] = dict(const=float(coef[0]), per_eval=float(coef[1]), per_instance=float(coef[2]),
+                         r2=float(1 - ((A @ coef - dur_us) ** 2).sum() / ((dur_us - dur_us.mean()) ** 2).sum()))
     print(json.dumps(res, indent=1))
     if a.dump:
-        np.save(a.dump, np.stack([s_us, e_us, work, xcc, simd_key], 1))
+        np.save(a.dump, np.stack([s_us, e_us, work, xcc, simd_key, evals], 1))
 
 
 if __name__ == "__main__":
