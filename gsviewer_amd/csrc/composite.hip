@@ -1495,7 +1495,29 @@ __device__ unsigned long long g_comp_stats[5];
 // (atomicMax of the complement; zero = none): k_merge folds each slice only up
 // to that chunk.  All words are accessed relaxed at agent scope; a stale read
 // only costs work, never accuracy.
-template <int FRAG, bool kBound>
+// Wave priority by remaining work (experiment, GSR_COMP_PRIO: bit 0 a frame
+// alone's launch, bit 1 a group's): at each batch the wave sets its priority to
+// min(3, batches left), so on a SIMD the waves with the most work left issue
+// first instead of the oldest (the SIMD's default arbitration, priority then
+// age: the youngest of 8 resident waves barely advanced until the older ones
+// retired, then ran alone at the launch's end, profiles/r6_s18).
+#ifndef GSR_COMP_PRIO
+#define GSR_COMP_PRIO 0
+#endif
+#ifndef GSR_COMP_PRIO_MODE
+#define GSR_COMP_PRIO_MODE 0  // 0: batches left; 1: batches done (least progress first)
+#endif
+__device__ __forceinline__ void batch_priority(uint32_t begin, uint32_t b, uint32_t end) {
+    const uint32_t left = (uint32_t)__builtin_amdgcn_readfirstlane((int)((end - b + kBatch - 1) / kBatch));
+    const uint32_t done = (uint32_t)__builtin_amdgcn_readfirstlane((int)((b - begin) / kBatch));
+    const uint32_t p = GSR_COMP_PRIO_MODE == 0 ? min(left, 3u) : 3u - min(done, 3u);
+    if (p >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (p == 2) __builtin_amdgcn_s_setprio(2);
+    else if (p == 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
+template <int FRAG, bool kBound, bool kPrio = false>
 __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t slot, float4* __restrict__ my,
                                                 const uint32_t* __restrict__ list,
                                                 const SplatRec* __restrict__ recs, const CompositeArgs& a,
@@ -1608,6 +1630,7 @@ __device__ __forceinline__ void composite_chunk(const uint4 d, const uint32_t sl
     uint32_t tr_evals = 0;  // (record, slice) evaluations of this chunk (tools/comp_trace.py)
 #endif
     for (uint32_t b = begin; b < end && live; b += kBatch) {
+        if constexpr (kPrio) batch_priority(begin, b, end);
         __builtin_amdgcn_wave_barrier();
         // sb[k] bit j: record j of the batch touches 16x4 slice k (and the
         // slice is live): one ballot per slice and batch instead of a
@@ -2050,7 +2073,7 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
             const uint32_t pos = r * G + ((r & 1u) ? G - 1u - g : g);
             if (pos >= total) break;
             const uint32_t slot = order[pos];
-            composite_chunk<FRAG, kBound>(desc[slot], slot, lds[wave], list, recs, a, out, partial, sat, tmax,
+            composite_chunk<FRAG, kBound, (GSR_COMP_PRIO & 1) != 0>(desc[slot], slot, lds[wave], list, recs, a, out, partial, sat, tmax,
                                           chunk_base);
         }
         return;
@@ -2064,7 +2087,7 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
     const uint4 d = desc[slot];
 #ifdef GSR_COMP_TRACE
     uint32_t evals = 0;
-    composite_chunk<FRAG, kBound>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax, chunk_base, &evals);
+    composite_chunk<FRAG, kBound, (GSR_COMP_PRIO & 1) != 0>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax, chunk_base, &evals);
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if (__lane_id() == 0 && slot < kTraceMax) {
         const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));     // HW_ID
@@ -2074,7 +2097,7 @@ __global__ __launch_bounds__(kCompThreads) GSR_COMP_OCC void k_composite(const u
         g_comp_trace[2 * slot + 1] = make_uint4((uint32_t)t0, (uint32_t)t1, (uint32_t)r0, (uint32_t)r1);
     }
 #else
-    composite_chunk<FRAG, kBound>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax, chunk_base);
+    composite_chunk<FRAG, kBound, (GSR_COMP_PRIO & 1) != 0>(d, slot, lds[wave], list, recs, a, out, partial, sat, tmax, chunk_base);
 #endif
 }
 
@@ -2150,7 +2173,7 @@ __device__ __forceinline__ void composite_views_wave(const CompViews& vs, const 
     if (pos >= (uint32_t)a.num_tiles + v.n_chunks_dev[0]) return;
     const uint32_t slot = v.order[pos];
     const uint4 d = v.desc[slot];
-    composite_chunk<FRAG, kBoundViews>(d, slot, lds, v.list, v.recs, a, v.out, v.partial, v.sat, v.tmax, v.chunk_base);
+    composite_chunk<FRAG, kBoundViews, (GSR_COMP_PRIO & 2) != 0>(d, slot, lds, v.list, v.recs, a, v.out, v.partial, v.sat, v.tmax, v.chunk_base);
 }
 
 template <int FRAG>
