@@ -519,8 +519,9 @@ int depth_sort(gsr_context* c, PendingFrame& f, const uint32_t* counters, const 
     const int passes = !c->depth_passes_now                                     ? kDepthPasses
                        : (c->depth_coarse_alone && f.n > kCoarseMaxN)           ? kDepthPassesBigAlone
                                                                                 : c->depth_passes_now;
+    // (an exact order: nothing reads the sorted keys, so the last pass writes none)
     return radix_sort_pairs(&f.ka, &f.va, &f.kb, &f.vb, true, f.n, counters, 32, passes, key_range,
-                            c->radix_tmp.p, totals, s, rect_in, pay_io, pay_alt, 0, c->fused_cull);
+                            c->radix_tmp.p, totals, s, rect_in, pay_io, pay_alt, 0, c->fused_cull, 0u, false);
 }
 
 // Wait until the last preprocess block has stored this frame's (V, D, seq) to
@@ -1132,10 +1133,10 @@ int gsr_render_begin_sorts(gsr_context* const* ctxs, int32_t k, void* stream) {
         f.packed = rects_packable(c, f.u);
         if (f.packed != rects_packable(ctxs[0], ctxs[0]->pend.u))
             return set_error(GSR_ERR_INVALID, "render_begin_sorts: views differ in frame size or rect payload");
-        // a group's frames: the exact sort (kDepthCoarseAlone)
+        // a group's frames: the exact sort (kDepthCoarseAlone); its last pass writes no keys (none are read)
         views[v] = RadixViewArgs{&f.ka, &f.va, &f.kb, &f.vb, c->zero.p + zl.counters, c->zero.p + zl.key_range,
                                  c->radix_tmp.p, c->zero.p + zl.totals_depth, f.packed ? c->trect.p : nullptr,
-                                 f.packed ? &f.pa : nullptr, f.packed ? &f.pb : nullptr, c->fused_cull, 0u, true};
+                                 f.packed ? &f.pa : nullptr, f.packed ? &f.pb : nullptr, c->fused_cull, 0u, false};
         f.coarse = 0;
     }
     int rc;
